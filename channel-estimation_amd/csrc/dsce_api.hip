@@ -1,0 +1,906 @@
+// dsce_api.hip — C-ABI (include/dsce.h) and host-side orchestration of the
+// HIP engine: operator packing (banded / CSR / compact layouts), device memory,
+// the setup pipeline (script:208-313) and the batched Monte-Carlo loop
+// (script:350-564).
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "dsce.h"
+#include "dsce_kernels.h"
+
+namespace dsce {
+
+struct HipError : std::runtime_error {
+    HipError(hipError_t e, const char* what, const char* file, int line)
+        : std::runtime_error(std::string("HIP error '") + hipGetErrorString(e) + "' at " + file + ":" +
+                             std::to_string(line) + " (" + what + ")") {}
+};
+struct ApiError : std::runtime_error {
+    int code;
+    ApiError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+static inline double2 cx(const double* p, size_t i) { return make_double2(p[2 * i], p[2 * i + 1]); }
+static inline bool nz(double2 v) { return v.x != 0.0 || v.y != 0.0; }
+
+struct HostBand {
+    std::vector<int> row0, nrows, klo, khi;
+    std::vector<long long> off;
+    std::vector<double2> vals;
+    long long elems = 0;
+};
+
+// rows [0, nrow) grouped in blocks of DSCE_RB; range(row) -> [lo, hi)
+template <class RangeFn>
+static HostBand band_geometry(int nrow, RangeFn range, int kscale) {
+    HostBand b;
+    long long off = 0;
+    for (int r0 = 0; r0 < nrow; r0 += DSCE_RB) {
+        const int nr = std::min(DSCE_RB, nrow - r0);
+        int lo = 1 << 30, hi = -1;
+        for (int r = r0; r < r0 + nr; ++r) {
+            int a, c;
+            range(r, a, c);
+            if (c > a) {
+                lo = std::min(lo, a);
+                hi = std::max(hi, c);
+            }
+        }
+        if (hi < 0) { lo = 0; hi = 0; }
+        b.row0.push_back(r0);
+        b.nrows.push_back(nr);
+        b.klo.push_back(lo * kscale);
+        b.khi.push_back(hi * kscale);
+        b.off.push_back(off);
+        off += (long long)(hi - lo) * kscale * DSCE_RB;
+    }
+    b.elems = off;
+    return b;
+}
+
+struct DevBand {
+    Band k{};
+};
+
+struct Scheme {
+    dsce_scheme_desc d{};
+    int N = 0, LK = 0;
+    std::vector<double2> G, Q, P;   // dense host copies (column-major)
+    std::vector<int> pilot_pos, data_pos;
+    std::vector<uint8_t> considered;
+    std::vector<double2> symbols;
+    SchemeK k{};
+    HostBand gband, qband, wband;
+    Band Wb{};
+    long long w_elems = 0, w_struct = 0;
+    double2* W = nullptr;
+    double2* Wd = nullptr;
+    std::vector<double2> R_hP, R_est, R_noI;
+    bool mmse_ready = false;
+    int64_t bits_all = 0, bits_noedge = 0;
+    std::vector<int> g_start, q_start;
+    int GL = 0, QL = 0;
+    int maxdelay = 0;
+};
+
+}  // namespace dsce
+
+using namespace dsce;
+
+struct dsce_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool chan_set = false;
+    ChannelK ch{};
+    std::vector<double> pdp_norm;
+    std::vector<double> pn;
+    int nsnr = 0, niter = 4;
+    double* d_pn = nullptr;
+    std::vector<std::unique_ptr<Scheme>> schemes;
+    int batch = 8192;
+    McBuffers buf{};
+    size_t buf_key[6] = {0, 0, 0, 0, 0, 0};
+    std::vector<void*> buf_allocs;
+    unsigned long long* d_counters = nullptr;
+    size_t counters_n = 0;
+    std::vector<void*> allocs;
+    bool timing = false;
+    std::map<std::string, std::pair<int64_t, double>> ktime;
+    struct Ev {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Ev> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+template <class T>
+T* dalloc(dsce_ctx* c, size_t n, std::vector<void*>* list = nullptr) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    DSCE_HIP_CHECK(hipMalloc(&p, n * sizeof(T)));
+    (list ? list : &c->allocs)->push_back(p);
+    return (T*)p;
+}
+template <class T>
+T* dupload(dsce_ctx* c, const std::vector<T>& v) {
+    T* p = dalloc<T>(c, v.size());
+    if (!v.empty()) DSCE_HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return p;
+}
+
+hipEvent_t get_event(dsce_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    DSCE_HIP_CHECK(hipEventCreate(&e));
+    return e;
+}
+
+struct Timed {
+    dsce_ctx* c;
+    dsce_ctx::Ev ev;
+    bool on;
+    Timed(dsce_ctx* ctx, const char* name) : c(ctx), on(ctx->timing) {
+        if (on) {
+            ev.name = name;
+            ev.a = get_event(c);
+            ev.b = get_event(c);
+            DSCE_HIP_CHECK(hipEventRecord(ev.a, c->stream));
+        }
+    }
+    ~Timed() {
+        if (on) {
+            (void)hipEventRecord(ev.b, c->stream);
+            c->pending.push_back(ev);
+        }
+    }
+};
+
+void collect_timing(dsce_ctx* c) {
+    for (auto& e : c->pending) {
+        float ms = 0.f;
+        DSCE_HIP_CHECK(hipEventElapsedTime(&ms, e.a, e.b));
+        auto& t = c->ktime[e.name];
+        t.first += 1;
+        t.second += ms;
+        c->event_pool.push_back(e.a);
+        c->event_pool.push_back(e.b);
+    }
+    c->pending.clear();
+}
+
+Band upload_band(dsce_ctx* c, const HostBand& h, bool with_vals) {
+    Band b{};
+    b.nblk = (int)h.row0.size();
+    b.row0 = dupload(c, h.row0);
+    b.nrows = dupload(c, h.nrows);
+    b.klo = dupload(c, h.klo);
+    b.khi = dupload(c, h.khi);
+    b.off = dupload(c, h.off);
+    b.vals = with_vals ? dupload(c, h.vals) : nullptr;
+    return b;
+}
+
+void check_ctx(dsce_ctx* c) {
+    if (!c) throw ApiError(DSCE_EINVAL, "null context");
+    DSCE_HIP_CHECK(hipSetDevice(c->device));
+}
+
+Scheme& get_scheme(dsce_ctx* c, int id) {
+    if (id < 0 || id >= (int)c->schemes.size()) throw ApiError(DSCE_EINVAL, "bad scheme id");
+    return *c->schemes[id];
+}
+
+// ---------------------------------------------------------------------------
+// operator packing
+// ---------------------------------------------------------------------------
+void pack_scheme(dsce_ctx* c, Scheme& s) {
+    const int N = s.N, LK = s.LK, Nsym = s.d.n_tx_symbols;
+    // column supports (first/last non-zero sample) of G and Q
+    std::vector<int> gs(LK), ge(LK), qs(LK), qe(LK);
+    for (int col = 0; col < LK; ++col) {
+        int a = N, b = -1, qa = N, qb = -1;
+        for (int n = 0; n < N; ++n) {
+            if (nz(s.G[(size_t)col * N + n])) { a = std::min(a, n); b = n; }
+            if (nz(s.Q[(size_t)col * N + n])) { qa = std::min(qa, n); qb = n; }
+        }
+        if (b < 0) { a = 0; b = -1; }
+        if (qb < 0) { qa = 0; qb = -1; }
+        gs[col] = a; ge[col] = b; qs[col] = qa; qe[col] = qb;
+    }
+    s.GL = 1;
+    s.QL = 1;
+    for (int col = 0; col < LK; ++col) {
+        s.GL = std::max(s.GL, ge[col] - gs[col] + 1);
+        s.QL = std::max(s.QL, qe[col] - qs[col] + 1);
+    }
+    s.g_start = gs;
+    s.q_start = qs;
+    std::vector<double2> gcol((size_t)LK * s.GL, make_double2(0, 0)), qcol((size_t)LK * s.QL, make_double2(0, 0));
+    for (int col = 0; col < LK; ++col) {
+        for (int i = 0; i < s.GL && gs[col] + i < N; ++i) gcol[(size_t)col * s.GL + i] = s.G[(size_t)col * N + gs[col] + i];
+        for (int i = 0; i < s.QL && qs[col] + i < N; ++i) qcol[(size_t)col * s.QL + i] = s.Q[(size_t)col * N + qs[col] + i];
+    }
+    // G band: rows = samples, k = columns
+    std::vector<int> rlo(N, 0), rhi(N, 0);
+    for (int n = 0; n < N; ++n) {
+        int lo = LK, hi = -1;
+        for (int col = 0; col < LK; ++col)
+            if (nz(s.G[(size_t)col * N + n])) { lo = std::min(lo, col); hi = col; }
+        rlo[n] = hi < 0 ? 0 : lo;
+        rhi[n] = hi < 0 ? 0 : hi + 1;
+    }
+    s.gband = band_geometry(N, [&](int r, int& a, int& b) { a = rlo[r]; b = rhi[r]; }, 1);
+    s.gband.vals.assign(s.gband.elems, make_double2(0, 0));
+    for (size_t blk = 0; blk < s.gband.row0.size(); ++blk)
+        for (int rl = 0; rl < s.gband.nrows[blk]; ++rl)
+            for (int k = s.gband.klo[blk]; k < s.gband.khi[blk]; ++k)
+                s.gband.vals[s.gband.off[blk] + (size_t)(k - s.gband.klo[blk]) * DSCE_RB + rl] =
+                    s.G[(size_t)k * N + s.gband.row0[blk] + rl];
+    // Q^H band: rows = columns of Q, k = samples
+    s.qband = band_geometry(LK, [&](int r, int& a, int& b) { a = qs[r]; b = qe[r] + 1; }, 1);
+    s.qband.vals.assign(s.qband.elems, make_double2(0, 0));
+    for (size_t blk = 0; blk < s.qband.row0.size(); ++blk)
+        for (int rl = 0; rl < s.qband.nrows[blk]; ++rl)
+            for (int k = s.qband.klo[blk]; k < s.qband.khi[blk]; ++k) {
+                const double2 q = s.Q[(size_t)(s.qband.row0[blk] + rl) * N + k];
+                s.qband.vals[s.qband.off[blk] + (size_t)(k - s.qband.klo[blk]) * DSCE_RB + rl] = make_double2(q.x, -q.y);
+            }
+    // W band: rows r, k = (c, p); c overlaps where Q-support(r) meets (H G)-support(c)
+    int maxd = 0;
+    for (int q = 0; q < c->ch.ntap; ++q) maxd = std::max(maxd, c->ch.tap_delay[q]);
+    s.maxdelay = maxd;
+    const int NP = s.d.n_pilots;
+    s.wband = band_geometry(
+        LK,
+        [&](int r, int& a, int& b) {
+            a = LK;
+            b = -1;
+            for (int col = 0; col < LK; ++col) {
+                if (qe[r] < qs[r] || ge[col] < gs[col]) continue;
+                if (gs[col] <= qe[r] && qs[r] <= ge[col] + maxd) { a = std::min(a, col); b = col + 1; }
+            }
+            if (b < 0) { a = 0; b = 0; }
+        },
+        NP);
+    s.w_elems = s.wband.elems;
+    s.w_struct = 0;
+    for (size_t blk = 0; blk < s.wband.row0.size(); ++blk)
+        s.w_struct += (long long)s.wband.nrows[blk] * (s.wband.khi[blk] - s.wband.klo[blk]);
+    // precoder CSR and its conjugate transpose
+    std::vector<int> pptr(LK + 1, 0), pcol;
+    std::vector<double2> pval;
+    for (int r = 0; r < LK; ++r) {
+        for (int k = 0; k < Nsym; ++k) {
+            const double2 v = s.P[(size_t)k * LK + r];
+            if (nz(v)) { pcol.push_back(k); pval.push_back(v); }
+        }
+        pptr[r + 1] = (int)pcol.size();
+    }
+    std::vector<int> hptr(Nsym + 1, 0), hcol;
+    std::vector<double2> hval;
+    for (int k = 0; k < Nsym; ++k) {
+        for (int r = 0; r < LK; ++r) {
+            const double2 v = s.P[(size_t)k * LK + r];
+            if (nz(v)) { hcol.push_back(r); hval.push_back(make_double2(v.x, -v.y)); }
+        }
+        hptr[k + 1] = (int)hcol.size();
+    }
+    // slicer grid of the constellation
+    std::vector<double> lvI, lvQ;
+    for (auto& z : s.symbols) { lvI.push_back(z.x); lvQ.push_back(z.y); }
+    std::sort(lvI.begin(), lvI.end());
+    lvI.erase(std::unique(lvI.begin(), lvI.end()), lvI.end());
+    std::sort(lvQ.begin(), lvQ.end());
+    lvQ.erase(std::unique(lvQ.begin(), lvQ.end()), lvQ.end());
+    if ((int)(lvI.size() * lvQ.size()) != s.d.mod_order)
+        throw ApiError(DSCE_EINVAL, "constellation is not a full rectangular grid");
+    std::vector<int> grid(lvI.size() * lvQ.size(), -1);
+    for (int m = 0; m < s.d.mod_order; ++m) {
+        const int iI = (int)(std::lower_bound(lvI.begin(), lvI.end(), s.symbols[m].x) - lvI.begin());
+        const int iQ = (int)(std::lower_bound(lvQ.begin(), lvQ.end(), s.symbols[m].y) - lvQ.begin());
+        grid[(size_t)iI * lvQ.size() + iQ] = m;
+    }
+    // kernel view
+    SchemeK& k = s.k;
+    k.N = N;
+    k.LK = LK;
+    k.Nsym = Nsym;
+    k.NP = NP;
+    k.ND = s.d.n_data;
+    k.M = s.d.mod_order;
+    k.mbits = s.d.bits_per_symbol;
+    k.despread = s.d.despread;
+    k.real_detect = s.d.real_detect;
+    k.inv_sqrt_kappa = 1.0 / sqrt(s.d.kappa);
+    k.data_div = s.d.data_div;
+    k.pilot_pos = dupload(c, s.pilot_pos);
+    k.data_pos = dupload(c, s.data_pos);
+    k.considered = dupload(c, s.considered);
+    k.symbols = dupload(c, s.symbols);
+    k.nI = (int)lvI.size();
+    k.nQ = (int)lvQ.size();
+    k.lvI = dupload(c, lvI);
+    k.lvQ = dupload(c, lvQ);
+    k.grid_sym = dupload(c, grid);
+    k.p_ptr = dupload(c, pptr);
+    k.p_col = dupload(c, pcol);
+    k.p_val = dupload(c, pval);
+    k.ph_ptr = dupload(c, hptr);
+    k.ph_col = dupload(c, hcol);
+    k.ph_val = dupload(c, hval);
+    k.G = upload_band(c, s.gband, true);
+    k.QH = upload_band(c, s.qband, true);
+    k.q_start = dupload(c, qs);
+    k.q_col = dupload(c, qcol);
+    k.QL = s.QL;
+    k.g_start = dupload(c, gs);
+    k.g_col = dupload(c, gcol);
+    k.GL = s.GL;
+    s.Wb = upload_band(c, s.wband, false);
+    // bits per realisation
+    s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;
+    int64_t ce = 0;
+    for (auto v : s.considered) ce += v ? 1 : 0;
+    s.bits_noedge = ce * s.d.bits_per_symbol;
+}
+
+// ---------------------------------------------------------------------------
+// setup pipeline: R_hP, R_est, R_noI, R_Dij, W, W0 (script:208-313)
+// ---------------------------------------------------------------------------
+void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
+    hipStream_t st = c->stream;
+    const int N = s.N, LK = s.LK, NP = s.d.n_pilots, Nsym = s.d.n_tx_symbols, nsnr = c->nsnr;
+    std::vector<void*> tmp;
+    auto talloc = [&](size_t bytes) {
+        void* p;
+        DSCE_HIP_CHECK(hipMalloc(&p, bytes));
+        tmp.push_back(p);
+        return p;
+    };
+    try {
+        double2* dG = (double2*)talloc(s.G.size() * sizeof(double2));
+        double2* dQ = (double2*)talloc(s.Q.size() * sizeof(double2));
+        double2* dP = (double2*)talloc(s.P.size() * sizeof(double2));
+        DSCE_HIP_CHECK(hipMemcpy(dG, s.G.data(), s.G.size() * sizeof(double2), hipMemcpyHostToDevice));
+        DSCE_HIP_CHECK(hipMemcpy(dQ, s.Q.data(), s.Q.size() * sizeof(double2), hipMemcpyHostToDevice));
+        DSCE_HIP_CHECK(hipMemcpy(dP, s.P.data(), s.P.size() * sizeof(double2), hipMemcpyHostToDevice));
+        int* dpil = (int*)talloc(NP * sizeof(int));
+        DSCE_HIP_CHECK(hipMemcpy(dpil, s.pilot_pos.data(), NP * sizeof(int), hipMemcpyHostToDevice));
+        double* j0tab = (double*)talloc((2 * N - 1) * sizeof(double));
+        setup_time_correlation(st, N, c->ch.fD, c->ch.dt, c->ch.model, j0tab);
+        SetupArgs a{};
+        a.N = N;
+        a.LK = LK;
+        a.NP = NP;
+        a.Nsym = Nsym;
+        a.ntap = c->ch.ntap;
+        a.nsnr = nsnr;
+        a.pilot_pos = dpil;
+        a.G = dG;
+        a.Q = dQ;
+        a.P = dP;
+        a.j0tab = j0tab;
+        for (int q = 0; q < c->ch.ntap; ++q) {
+            a.tap_delay[q] = c->ch.tap_delay[q];
+            a.pdp[q] = c->pdp_norm[c->ch.tap_delay[q]];
+        }
+        a.kappa = s.d.kappa;
+        a.thr = thr;
+        double2* m = (double2*)talloc((size_t)NP * a.ntap * N * sizeof(double2));
+        setup_mcoef(st, a, s.k.g_start, s.GL, s.k.q_start, s.QL, m);
+        double2* rhp = (double2*)talloc((size_t)NP * NP * sizeof(double2));
+        setup_rhp(st, a, m, rhp);
+        double2* gp = (double2*)talloc((size_t)N * Nsym * sizeof(double2));
+        setup_gp(st, a, gp);
+        double* dg = (double*)talloc(NP * sizeof(double));
+        setup_rest_diag(st, a, gp, s.k.q_start, s.QL, dg);
+        std::vector<double2> hrhp((size_t)NP * NP);
+        std::vector<double> hdiag(NP);
+        DSCE_HIP_CHECK(hipMemcpyAsync(hrhp.data(), rhp, hrhp.size() * sizeof(double2), hipMemcpyDeviceToHost, st));
+        DSCE_HIP_CHECK(hipMemcpyAsync(hdiag.data(), dg, NP * sizeof(double), hipMemcpyDeviceToHost, st));
+        DSCE_HIP_CHECK(hipStreamSynchronize(st));
+        // R_est / R_noI per SNR (script:238-253): tiny NP x NP assembly on the host
+        std::vector<double> qn(NP, 0.0);
+        for (int i = 0; i < NP; ++i) {
+            const int col = s.pilot_pos[i];
+            double acc = 0.0;
+            for (int n = 0; n < N; ++n) {
+                const double2 q = s.Q[(size_t)col * N + n];
+                acc += q.x * q.x + q.y * q.y;
+            }
+            qn[i] = acc;
+        }
+        s.R_hP = hrhp;
+        s.R_est.assign((size_t)nsnr * NP * NP, make_double2(0, 0));
+        s.R_noI.assign((size_t)nsnr * NP * NP, make_double2(0, 0));
+        for (int k = 0; k < nsnr; ++k) {
+            for (int j = 0; j < NP; ++j)
+                for (int i = 0; i < NP; ++i) {
+                    const size_t ix = (size_t)j * NP + i;
+                    double2 noN = i == j ? make_double2(hdiag[i], 0.0) : hrhp[ix];
+                    double2 est = noN;
+                    if (i == j) est.x = hdiag[i] + c->pn[k] * qn[i] / s.d.kappa;
+                    s.R_est[(size_t)k * NP * NP + ix] = est;
+                    // R_est - (R_est_noNoise - R_hP)
+                    const double2 diff = c_sub(noN, hrhp[ix]);
+                    s.R_noI[(size_t)k * NP * NP + ix] = c_sub(est, diff);
+                }
+        }
+        // inverses: [var][snr]
+        double2* dR = (double2*)talloc((size_t)2 * nsnr * NP * NP * sizeof(double2));
+        double2* dRi = (double2*)talloc((size_t)2 * nsnr * NP * NP * sizeof(double2));
+        DSCE_HIP_CHECK(hipMemcpy(dR, s.R_est.data(), (size_t)nsnr * NP * NP * sizeof(double2), hipMemcpyHostToDevice));
+        DSCE_HIP_CHECK(hipMemcpy(dR + (size_t)nsnr * NP * NP, s.R_noI.data(), (size_t)nsnr * NP * NP * sizeof(double2),
+                                 hipMemcpyHostToDevice));
+        setup_rinv(st, NP, 2 * nsnr, dR, dRi);
+        // R_Dij packed, then W / W0 per SNR
+        double2* rd = (double2*)talloc((size_t)s.w_elems * sizeof(double2));
+        Band Wb = s.Wb;
+        setup_rdij(st, a, Wb, m, s.k.g_start, s.GL, s.k.q_start, s.QL, rd);
+        if (!s.W) {
+            s.W = dalloc<double2>(c, (size_t)2 * nsnr * s.w_elems);
+            s.Wd = dalloc<double2>(c, (size_t)2 * nsnr * LK * NP);
+        }
+        for (int var = 0; var < 2; ++var)
+            for (int k = 0; k < nsnr; ++k) {
+                const size_t vi = (size_t)var * nsnr + k;
+                setup_w(st, a, Wb, s.w_elems, rd, dRi + vi * NP * NP, s.W + vi * s.w_elems, s.Wd + vi * LK * NP);
+            }
+        DSCE_HIP_CHECK(hipStreamSynchronize(st));
+        DSCE_HIP_CHECK(hipGetLastError());
+    } catch (...) {
+        for (void* p : tmp) (void)hipFree(p);
+        throw;
+    }
+    for (void* p : tmp) DSCE_HIP_CHECK(hipFree(p));
+    s.mmse_ready = true;
+}
+
+// ---------------------------------------------------------------------------
+// Monte-Carlo batches
+// ---------------------------------------------------------------------------
+void ensure_buffers(dsce_ctx* c, int R) {
+    size_t N = 0, LK = 0, NP = 0, ND = 0;
+    for (auto& s : c->schemes) {
+        N = std::max<size_t>(N, s->N);
+        LK = std::max<size_t>(LK, s->LK);
+        NP = std::max<size_t>(NP, s->d.n_pilots);
+        ND = std::max<size_t>(ND, s->d.n_data);
+    }
+    const size_t key[6] = {(size_t)R, N, LK, NP, ND, (size_t)c->nsnr};
+    if (memcmp(key, c->buf_key, sizeof(key)) == 0) return;
+    for (void* p : c->buf_allocs) (void)hipFree(p);
+    c->buf_allocs.clear();
+    memcpy(c->buf_key, key, sizeof(key));
+    const size_t U = (size_t)R * c->nsnr;
+    McBuffers& b = c->buf;
+    auto* L = &c->buf_allocs;
+    b.R = R;
+    b.nsnr = c->nsnr;
+    b.U = (int)U;
+    b.ir = dalloc<double2>(c, (size_t)c->ch.ntap * N * R, L);
+    b.xp = dalloc<double2>(c, NP * R, L);
+    b.sidx = dalloc<uint16_t>(c, ND * R, L);
+    b.r0 = dalloc<double2>(c, N * R, L);
+    b.h = dalloc<double2>(c, LK * R, L);
+    b.xs = dalloc<double2>(c, LK * R, L);
+    b.ss = dalloc<double2>(c, N * R, L);
+    b.y = dalloc<double2>(c, LK * U, L);
+    b.yest = dalloc<double2>(c, LK * U, L);
+    b.yperf = dalloc<double2>(c, LK * U, L);
+    b.hp = dalloc<double2>(c, NP * U, L);
+    b.hest = dalloc<double2>(c, LK * U, L);
+    b.v = dalloc<double2>(c, LK * U, L);
+    b.u = dalloc<double2>(c, LK * U, L);
+    b.t = dalloc<double2>(c, N * U, L);
+    b.e = dalloc<double2>(c, LK * U, L);
+    b.qe = dalloc<uint16_t>(c, ND * U, L);
+    b.qp = dalloc<uint16_t>(c, ND * U, L);
+}
+
+struct Trace {
+    int scheme, snr, lane;
+    double* y;
+    double* hp;
+    double* hest;
+    double* h;
+};
+
+void copy_col(dsce_ctx* c, double* dst, const double2* src, int rows, int stride, int lane) {
+    DSCE_HIP_CHECK(hipMemcpy2DAsync(dst, sizeof(double2), src + lane, (size_t)stride * sizeof(double2),
+                                    sizeof(double2), rows, hipMemcpyDeviceToHost, c->stream));
+}
+
+int var_of_stage(int stage, int niter) { return (stage == 0 || stage <= niter / 2) ? 0 : 1; }
+
+void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, const Trace* tr) {
+    McBuffers& b = c->buf;
+    b.R = R;
+    b.U = R * c->nsnr;
+    {
+        Timed t(c, "k_jakes");
+        launch_jakes(c->stream, c->ch, seed, rep0, R, b.ir);
+    }
+    (void)valid;
+    for (size_t si = 0; si < c->schemes.size(); ++si) {
+        Scheme& s = *c->schemes[si];
+        MmseK mm{};
+        mm.W = s.W;
+        mm.Wd = s.Wd;
+        mm.w_elems = s.w_elems;
+        mm.nsnr = c->nsnr;
+        mm.Wb = s.Wb;
+        const bool tracing = tr && tr->scheme == (int)si;
+        const int tunit = tracing ? tr->snr * R + tr->lane : 0;
+        {
+            Timed t(c, "tx");
+            launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
+        }
+        {
+            Timed t(c, "rx_front");
+            launch_rx_front(c->stream, s.k, c->ch, c->d_pn, seed, rep0, b);
+        }
+        if (tracing) {
+            copy_col(c, tr->y, b.y, s.LK, b.U, tunit);
+            copy_col(c, tr->h, b.h, s.LK, R, tr->lane);
+        }
+        for (int it = 0; it <= c->niter; ++it) {
+            if (it > 0) {
+                {
+                    Timed t(c, "k_wcontract");
+                    launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
+                }
+                {
+                    Timed t(c, "perfect_ic");
+                    launch_perfect_ic(c->stream, s.k, c->ch, b);
+                }
+            }
+            {
+                Timed t(c, "k_stage");
+                launch_stage(c->stream, s.k, mm, it, var_of_stage(it, c->niter), c->niter, it == c->niter, b,
+                             c->d_counters, (int)si, nullptr);
+            }
+            if (tracing) {
+                copy_col(c, tr->hp + (size_t)2 * it * s.d.n_pilots, b.hp, s.d.n_pilots, b.U, tunit);
+                copy_col(c, tr->hest + (size_t)2 * it * s.LK, b.hest, s.LK, b.U, tunit);
+            }
+        }
+    }
+    DSCE_HIP_CHECK(hipGetLastError());
+}
+
+int api_fail(dsce_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define API_BEGIN try {
+#define API_END                                                 \
+    }                                                           \
+    catch (const ApiError& e) { return api_fail(ctx, e.code, e.what()); } \
+    catch (const HipError& e) { return api_fail(ctx, DSCE_EHIP, e.what()); } \
+    catch (const std::bad_alloc&) { return api_fail(ctx, DSCE_ENOMEM, "host out of memory"); } \
+    catch (const std::exception& e) { return api_fail(ctx, DSCE_EINVAL, e.what()); }     \
+    return DSCE_OK;
+
+}  // namespace
+
+extern "C" {
+
+int dsce_abi_version(void) { return DSCE_ABI_VERSION; }
+
+int dsce_device_count(int* count) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (count) *count = n;
+    return DSCE_OK;
+}
+
+int dsce_create(int hip_device, dsce_ctx** out) {
+    if (!out) return DSCE_EINVAL;
+    *out = nullptr;
+    auto* ctx = new (std::nothrow) dsce_ctx();
+    if (!ctx) return DSCE_ENOMEM;
+    ctx->device = hip_device;
+    try {
+        DSCE_HIP_CHECK(hipSetDevice(hip_device));
+        DSCE_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    } catch (const std::exception& e) {
+        delete ctx;
+        return DSCE_EHIP;
+    }
+    *out = ctx;
+    return DSCE_OK;
+}
+
+void dsce_destroy(dsce_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (void* p : ctx->buf_allocs) (void)hipFree(p);
+    for (void* p : ctx->allocs) (void)hipFree(p);
+    for (auto& e : ctx->pending) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* dsce_last_error(const dsce_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!d || !d->pdp_norm || d->n_samples <= 1 || d->n_taps <= 0 || d->n_paths <= 0 || d->sampling_rate <= 0)
+        throw ApiError(DSCE_EINVAL, "invalid channel description");
+    if (d->doppler_model != 0 && d->doppler_model != 1) throw ApiError(DSCE_EINVAL, "doppler_model must be 0 or 1");
+    if (!ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "set the channel before adding schemes");
+    ChannelK ch{};
+    ch.N = d->n_samples;
+    ch.fD = d->max_doppler;
+    ch.dt = 1.0 / d->sampling_rate;
+    ch.paths = d->n_paths;
+    ch.model = d->doppler_model;
+    ctx->pdp_norm.assign(d->pdp_norm, d->pdp_norm + d->n_taps);
+    int nt = 0;
+    for (int i = 0; i < d->n_taps; ++i) {
+        if (d->pdp_norm[i] != 0.0) {
+            if (nt >= 8) throw ApiError(DSCE_EINVAL, "at most 8 non-zero channel taps are supported");
+            ch.tap_delay[nt] = i;
+            ch.sqrt_pdp[nt] = sqrt(d->pdp_norm[i]);
+            ++nt;
+        }
+    }
+    if (nt == 0) throw ApiError(DSCE_EINVAL, "power delay profile is all zero");
+    if (d->max_doppler <= 0) throw ApiError(DSCE_EINVAL, "max_doppler must be > 0 (time-variant channel)");
+    ch.ntap = nt;
+    ctx->ch = ch;
+    ctx->chan_set = true;
+    API_END
+}
+
+int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!pn_time || n_snr <= 0 || n_iter < 0) throw ApiError(DSCE_EINVAL, "invalid SNR list");
+    ctx->pn.assign(pn_time, pn_time + n_snr);
+    ctx->nsnr = n_snr;
+    ctx->niter = n_iter;
+    ctx->d_pn = dupload(ctx, ctx->pn);
+    for (auto& s : ctx->schemes) s->mmse_ready = false;
+    const size_t n = ctx->schemes.size() * 4 * (size_t)n_snr * (n_iter + 1);
+    ctx->counters_n = 0;
+    (void)n;
+    API_END
+}
+
+int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!ctx->chan_set) throw ApiError(DSCE_ESTATE, "dsce_set_channel first");
+    if (!d || !d->G || !d->Q || !d->P || !d->pilot_pos || !d->considered || !d->symbols)
+        throw ApiError(DSCE_EINVAL, "null operator");
+    const int LK = d->n_subcarriers * d->n_symbols;
+    if (LK <= 0 || d->n_pilots <= 0 || d->n_pilots > DSCE_MAX_NP || d->n_data <= 0 ||
+        d->n_tx_symbols != d->n_pilots + d->n_data)
+        throw ApiError(DSCE_EINVAL, "inconsistent scheme dimensions");
+    if (d->mod_order < 2 || d->mod_order > 256 || (d->mod_order & (d->mod_order - 1)) ||
+        (1 << d->bits_per_symbol) != d->mod_order || 32 % d->bits_per_symbol)
+        throw ApiError(DSCE_EINVAL, "modulation order must be a power of two <= 256");
+    if (!d->despread && !d->data_pos) throw ApiError(DSCE_EINVAL, "data_pos required in select mode");
+    if (d->kappa <= 0 || d->data_div <= 0) throw ApiError(DSCE_EINVAL, "kappa/data_div must be positive");
+    auto s = std::make_unique<Scheme>();
+    s->d = *d;
+    s->N = ctx->ch.N;
+    s->LK = LK;
+    const size_t nG = (size_t)s->N * LK;
+    s->G.resize(nG);
+    s->Q.resize(nG);
+    for (size_t i = 0; i < nG; ++i) {
+        s->G[i] = cx(d->G, i);
+        s->Q[i] = cx(d->Q, i);
+    }
+    s->P.resize((size_t)LK * d->n_tx_symbols);
+    for (size_t i = 0; i < s->P.size(); ++i) s->P[i] = cx(d->P, i);
+    s->pilot_pos.assign(d->pilot_pos, d->pilot_pos + d->n_pilots);
+    for (int p : s->pilot_pos)
+        if (p < 0 || p >= LK) throw ApiError(DSCE_EINVAL, "pilot position out of range");
+    if (!d->despread) {
+        s->data_pos.assign(d->data_pos, d->data_pos + d->n_data);
+        for (int p : s->data_pos)
+            if (p < 0 || p >= LK) throw ApiError(DSCE_EINVAL, "data position out of range");
+    } else {
+        s->data_pos.assign(1, 0);
+    }
+    s->considered.assign(d->considered, d->considered + d->n_data);
+    s->symbols.resize(d->mod_order);
+    for (int m = 0; m < d->mod_order; ++m) s->symbols[m] = cx(d->symbols, m);
+    pack_scheme(ctx, *s);
+    if (scheme_id) *scheme_id = (int32_t)ctx->schemes.size();
+    ctx->schemes.push_back(std::move(s));
+    API_END
+}
+
+int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (ctx->nsnr <= 0) throw ApiError(DSCE_ESTATE, "dsce_set_snr first");
+    if (ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "no scheme added");
+    for (auto& s : ctx->schemes) build_mmse(ctx, *s, zero_threshold);
+    API_END
+}
+
+int dsce_set_batch(dsce_ctx* ctx, int32_t reps) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (reps < 64) throw ApiError(DSCE_EINVAL, "batch must be >= 64");
+    ctx->batch = (reps + 63) / 64 * 64;
+    API_END
+}
+
+static void prepare_run(dsce_ctx* ctx) {
+    if (ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "no scheme added");
+    for (auto& s : ctx->schemes)
+        if (!s->mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    const size_t n = ctx->schemes.size() * 4 * (size_t)ctx->nsnr * (ctx->niter + 1);
+    if (ctx->counters_n != n) {
+        ctx->d_counters = dalloc<unsigned long long>(ctx, n);
+        ctx->counters_n = n;
+    }
+    DSCE_HIP_CHECK(hipMemsetAsync(ctx->d_counters, 0, n * sizeof(unsigned long long), ctx->stream));
+}
+
+int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!err_counts) throw ApiError(DSCE_EINVAL, "err_counts is null");
+    if (n_rep % 64) throw ApiError(DSCE_EINVAL, "n_rep must be a multiple of 64 (one wavefront of realisations)");
+    prepare_run(ctx);
+    uint64_t done = 0;
+    while (done < n_rep) {
+        const uint64_t left = n_rep - done;
+        const int R = (int)std::min<uint64_t>((uint64_t)ctx->batch, left);
+        ensure_buffers(ctx, R <= ctx->batch ? ctx->batch : R);
+        run_batch(ctx, seed, first_rep + done, R, R, nullptr);
+        done += (uint64_t)R;
+    }
+    std::vector<unsigned long long> h(ctx->counters_n);
+    DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, ctx->stream));
+    DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->timing) collect_timing(ctx);
+    for (size_t i = 0; i < h.size(); ++i) err_counts[i] += (int64_t)h[i];
+    API_END
+}
+
+int dsce_bits_per_rep(dsce_ctx* ctx, int32_t id, int64_t* bits2) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!bits2) throw ApiError(DSCE_EINVAL, "null output");
+    bits2[0] = s.bits_all;
+    bits2[1] = s.bits_noedge;
+    API_END
+}
+
+int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_out) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!ctx->chan_set) throw ApiError(DSCE_ESTATE, "dsce_set_channel first");
+    if (!ir_out) throw ApiError(DSCE_EINVAL, "null output");
+    const int N = ctx->ch.N, R = 64;
+    double2* ir = dalloc<double2>(ctx, (size_t)ctx->ch.ntap * N * R);
+    launch_jakes(ctx->stream, ctx->ch, seed, rep, R, ir);
+    std::vector<double2> h((size_t)ctx->ch.ntap * N * R);
+    DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ir, h.size() * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+    DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    DSCE_HIP_CHECK(hipFree(ir));
+    ctx->allocs.pop_back();
+    const int ntot = (int)ctx->pdp_norm.size();
+    for (size_t i = 0; i < (size_t)N * ntot * 2; ++i) ir_out[i] = 0.0;
+    for (int q = 0; q < ctx->ch.ntap; ++q)
+        for (int n = 0; n < N; ++n) {
+            const double2 v = h[((size_t)q * N + n) * R + 0];
+            const size_t o = (size_t)ctx->ch.tap_delay[q] * N + n;
+            ir_out[2 * o] = v.x;
+            ir_out[2 * o + 1] = v.y;
+        }
+    API_END
+}
+
+int dsce_get_correlation(dsce_ctx* ctx, int32_t id, double* r_hp, double* r_est, double* r_noi) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!s.mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    if (r_hp) memcpy(r_hp, s.R_hP.data(), s.R_hP.size() * sizeof(double2));
+    if (r_est) memcpy(r_est, s.R_est.data(), s.R_est.size() * sizeof(double2));
+    if (r_noi) memcpy(r_noi, s.R_noI.data(), s.R_noI.size() * sizeof(double2));
+    API_END
+}
+
+int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!s.mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    if (k < 0 || k >= ctx->nsnr || var < 0 || var > 1 || !w_out) throw ApiError(DSCE_EINVAL, "bad W index");
+    std::vector<double2> packed(s.w_elems);
+    DSCE_HIP_CHECK(hipMemcpy(packed.data(), s.W + ((size_t)var * ctx->nsnr + k) * s.w_elems,
+                             s.w_elems * sizeof(double2), hipMemcpyDeviceToHost));
+    const size_t LK = s.LK, NP = s.d.n_pilots;
+    memset(w_out, 0, LK * LK * NP * 2 * sizeof(double));
+    const HostBand& b = s.wband;
+    for (size_t blk = 0; blk < b.row0.size(); ++blk) {
+        const int clo = b.klo[blk] / (int)NP, chi = b.khi[blk] / (int)NP;
+        for (int rl = 0; rl < b.nrows[blk]; ++rl)
+            for (int cc = clo; cc < chi; ++cc)
+                for (size_t p = 0; p < NP; ++p) {
+                    const double2 v = packed[b.off[blk] + ((size_t)(cc - clo) * NP + p) * DSCE_RB + rl];
+                    const size_t o = (size_t)(b.row0[blk] + rl) + LK * cc + LK * LK * p;
+                    w_out[2 * o] = v.x;
+                    w_out[2 * o + 1] = v.y;
+                }
+    }
+    API_END
+}
+
+int dsce_trace_unit(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, int32_t k, double* y, double* hp,
+                    double* hest, double* h) {
+    API_BEGIN
+    check_ctx(ctx);
+    get_scheme(ctx, id);
+    if (k < 0 || k >= ctx->nsnr || !y || !hp || !hest || !h) throw ApiError(DSCE_EINVAL, "bad trace arguments");
+    prepare_run(ctx);
+    ensure_buffers(ctx, ctx->batch);
+    Trace tr{id, k, 0, y, hp, hest, h};
+    run_batch(ctx, seed, rep, 64, 64, &tr);
+    DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->timing) collect_timing(ctx);
+    API_END
+}
+
+int dsce_enable_timing(dsce_ctx* ctx, int32_t enable) {
+    API_BEGIN
+    check_ctx(ctx);
+    ctx->timing = enable != 0;
+    if (!ctx->timing) ctx->ktime.clear();
+    API_END
+}
+
+int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms) {
+    API_BEGIN
+    if (!ctx || !kernel) throw ApiError(DSCE_EINVAL, "null argument");
+    auto it = ctx->ktime.find(kernel);
+    if (launches) *launches = it == ctx->ktime.end() ? 0 : it->second.first;
+    if (total_ms) *total_ms = it == ctx->ktime.end() ? 0.0 : it->second.second;
+    API_END
+}
+
+int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (cmac) *cmac = (double)s.w_struct * ctx->nsnr * ctx->niter;
+    if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
+    API_END
+}
+
+}  // extern "C"

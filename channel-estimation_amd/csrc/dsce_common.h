@@ -1,0 +1,139 @@
+// dsce_common.h — shared device/host definitions of the MI355X engine.
+//
+// Data layout in HBM: every per-realisation or
+// per-unit vector is stored "structure of arrays", element-major with the
+// realisation / unit index fastest ([element][unit]).  A wavefront maps its 64
+// lanes to 64 units (unit = snr * R + rep), so every operator (G, Q, P, W) is
+// wave-uniform and is read with scalar loads, while per-unit vectors are read
+// and written with fully coalesced 16-byte lanes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DSCE_RB 24          // rows per band block (MMSE contraction / banded matvec tile)
+#define DSCE_MAX_NP 64
+#define DSCE_MAX_TAPS 64
+
+// ---------------------------------------------------------------------------
+// complex fp64 helpers (interleaved double2 = (re, im))
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ double2 c_make(double r, double i) { return make_double2(r, i); }
+__host__ __device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__host__ __device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__host__ __device__ __forceinline__ double2 c_mul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__host__ __device__ __forceinline__ double2 c_scale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+__host__ __device__ __forceinline__ double2 c_conj(double2 a) { return make_double2(a.x, -a.y); }
+// a / b  (plain formula; rounding-level differences to numpy's Smith division)
+__host__ __device__ __forceinline__ double2 c_div(double2 a, double2 b) {
+    double d = b.x * b.x + b.y * b.y;
+    return make_double2((a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d);
+}
+// acc += a * b
+__device__ __forceinline__ void c_fma(double2& acc, double2 a, double2 b) {
+    acc.x = fma(a.x, b.x, acc.x);
+    acc.x = fma(-a.y, b.y, acc.x);
+    acc.y = fma(a.x, b.y, acc.y);
+    acc.y = fma(a.y, b.x, acc.y);
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 and the random-stream spec of include/dsce.h
+// ---------------------------------------------------------------------------
+enum { STREAM_THETA = 1, STREAM_PHI = 2, STREAM_BITS = 3, STREAM_PILOTS = 4, STREAM_NOISE = 5 };
+
+__host__ __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                        uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__host__ __device__ __forceinline__ uint4 stream_block(uint64_t seed, uint64_t rep, uint32_t stream, uint32_t sub,
+                                                       uint32_t idx) {
+    return philox4x32_10(idx, (uint32_t)rep, (uint32_t)(rep >> 32), ((stream & 0xFFFFu) << 16) | (sub & 0xFFFFu),
+                         (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+__host__ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// ---------------------------------------------------------------------------
+// Banded block operator: rows grouped in blocks of <= DSCE_RB rows; every
+// block has a contiguous reduction range [klo, khi) and its values are stored
+// densely as vals[off + (k - klo) * DSCE_RB + r_local] (rows padded to RB with
+// zeros).  Used for G (rows = samples, k = symbols), Q^H (rows = symbols,
+// k = samples) and the MMSE estimator W (rows = symbols, k = (col, pilot)).
+// ---------------------------------------------------------------------------
+struct Band {
+    int nblk;
+    const int* row0;
+    const int* nrows;
+    const int* klo;
+    const int* khi;
+    const long long* off;
+    const double2* vals;
+};
+
+// ---------------------------------------------------------------------------
+// Scheme operators as seen by the Monte-Carlo kernels (all device pointers).
+// ---------------------------------------------------------------------------
+struct SchemeK {
+    int N, LK, Nsym, NP, ND, M, mbits, despread, real_detect;
+    double inv_sqrt_kappa, data_div;
+    const int* pilot_pos;
+    const int* data_pos;
+    const uint8_t* considered;
+    const double2* symbols;       // M, sorted by bit label
+    // nearest-neighbour slicer on the constellation grid
+    int nI, nQ;
+    const double* lvI;            // nI ascending real levels
+    const double* lvQ;            // nQ ascending imag levels (nQ = 1, {0} for PAM)
+    const int* grid_sym;          // nI * nQ -> symbol index
+    // precoder P (LK x Nsym) and P^H (Nsym x LK), CSR
+    const int* p_ptr;
+    const int* p_col;
+    const double2* p_val;
+    const int* ph_ptr;
+    const int* ph_col;
+    const double2* ph_val;
+    Band G;                       // N x LK
+    Band QH;                      // LK x N (conj(Q)^T)
+    // perfect-CSI diag(D): Q columns compact (support start + QL values)
+    const int* q_start;
+    const double2* q_col;         // LK x QL
+    int QL;
+    const int* g_start;
+    const double2* g_col;         // LK x GL
+    int GL;
+};
+
+struct ChannelK {
+    int N, ntap;                  // ntap = number of non-zero taps
+    int tap_delay[DSCE_MAX_TAPS];
+    double sqrt_pdp[DSCE_MAX_TAPS];
+    double fD, dt;
+    int paths, model;
+};
+
+// host-side launch helpers (defined in the .hip translation units)
+#define DSCE_HIP_CHECK(expr)                                                       \
+    do {                                                                           \
+        hipError_t _e = (expr);                                                    \
+        if (_e != hipSuccess) throw dsce::HipError(_e, #expr, __FILE__, __LINE__); \
+    } while (0)

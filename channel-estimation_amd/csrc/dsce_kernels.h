@@ -1,0 +1,81 @@
+// dsce_kernels.h — host-callable launchers of the HIP kernels.
+#pragma once
+
+#include "dsce_common.h"
+
+namespace dsce {
+
+struct McBuffers {
+    int R;            // repetitions per batch (multiple of 64)
+    int nsnr;
+    int U;            // units = nsnr * R, unit = snr * R + rep
+    // per repetition (channel shared by all schemes)
+    double2* ir;      // [ntap][N][R]
+    // per repetition and scheme
+    double2* xp;      // [NP][R]
+    uint16_t* sidx;   // [ND][R]
+    double2* r0;      // [N][R]
+    double2* h;       // [LK][R]   perfect-CSI diag(D)
+    double2* xs;      // [LK][R]   scratch: precoded symbols
+    double2* ss;      // [N][R]    scratch: time signal
+    // per unit
+    double2* y;       // [LK][U]
+    double2* yest;    // [LK][U]
+    double2* yperf;   // [LK][U]
+    double2* hp;      // [NP][U]   LS pilot estimates of the current stage
+    double2* hest;    // [LK][U]   diag(D_hat) of the current stage
+    double2* v;       // [LK][U]   P [xP; Q(x_est)]
+    double2* u;       // [LK][U]   P [xP; Q(x_perfect)]
+    double2* t;       // [N][U]    scratch: r / G u
+    double2* e;       // [LK][U]   scratch: y ./ h (despreading)
+    uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
+    uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
+};
+
+struct MmseK {
+    const double2* W;     // [var][snr][w_elems] packed band layout
+    const double2* Wd;    // [var][snr][LK][NP] diagonal entries W[(c,c),p]
+    long long w_elems;
+    int nsnr;
+    Band Wb;              // block geometry (vals unused; per-(var,snr) base added)
+};
+
+// Monte-Carlo pipeline
+void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir);
+void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
+               uint64_t rep0, McBuffers& b);
+void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
+                     uint64_t rep0, McBuffers& b);
+void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
+                  McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t* dummy);
+void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
+void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b);
+
+// setup (correlation matrices and MMSE estimator)
+struct SetupArgs {
+    int N, LK, NP, Nsym, ntap, nsnr;
+    const int* pilot_pos;
+    const double2* G;        // dense N x LK (column-major)
+    const double2* Q;        // dense N x LK
+    const double2* P;        // dense LK x Nsym
+    const double* j0tab;     // 2N-1 time correlation, index lag + N - 1
+    int tap_delay[DSCE_MAX_TAPS];
+    double pdp[DSCE_MAX_TAPS];
+    double kappa;
+    const double* pn;        // nsnr
+    double thr;
+};
+
+void setup_time_correlation(hipStream_t s, int N, double fD, double dt, int model, double* j0tab);
+void setup_mcoef(hipStream_t s, const SetupArgs& a, const int* g_start, int GL, const int* q_start, int QL,
+                 double2* m /* [NP][ntap][N] */);
+void setup_rhp(hipStream_t s, const SetupArgs& a, const double2* m, double2* rhp);
+void setup_gp(hipStream_t s, const SetupArgs& a, double2* gp /* N x Nsym */);
+void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const int* q_start, int QL, double* diag);
+void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv);
+void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
+                const int* q_start, int QL, double2* rd /* packed, w_elems */);
+void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
+             const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);
+
+}  // namespace dsce

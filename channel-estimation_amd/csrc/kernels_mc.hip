@@ -1,0 +1,484 @@
+// kernels_mc.hip — per-realisation hot path of DoublySelectiveChannelEstimation.m
+// (script:350-564) as CDNA4 HIP kernels.
+//
+// Mapping: one wavefront = 64 lanes = 64 independent units (realisation, or
+// realisation x SNR point).  Operators shared by all units (G, Q, P, W,
+// constellation) are addressed with wave-uniform indices, so the compiler
+// reads them with scalar loads (s_load / s_buffer_load) and broadcasts them to
+// the lanes; per-unit vectors live in HBM as [element][unit] and every access
+// is a coalesced 16-byte-per-lane vector load.  Complex arithmetic is fp64
+// throughout (the reference is fp64 MATLAB).
+//
+// Compile with -ffp-contract=off: the RNG transforms and the Jakes phase must
+// round exactly like the NumPy oracle; explicit fma() is used where fusion is
+// wanted (matvec inner loops).
+#include "dsce_kernels.h"
+
+#include <math.h>
+
+namespace dsce {
+
+static constexpr double TWO_PI = 6.283185307179586;   // 2*pi rounded (== 2.0*np.pi)
+static constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------------------
+// wave reductions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// a2: Jakes / Uniform sum-of-sinusoids impulse response, FastFading.m:222-238.
+// grid (ceil(N/256), R, ntap), block 256: the 2 x Paths random parameters of
+// one (realisation, tap) are drawn once into LDS, every lane owns one sample n.
+// Output IR[tap][n][rep] (only non-zero-power taps).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+                                               double2* __restrict__ ir) {
+    extern __shared__ double sm[];
+    double* ds = sm;
+    double* ph = sm + ch.paths;
+    const int tap = blockIdx.z;
+    const int rl = blockIdx.y;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    for (int p = threadIdx.x; p < ch.paths; p += blockDim.x) {
+        const uint32_t e = (uint32_t)(tap + ch.ntap * p);       // rand([Ntap 1 Paths]) column-major
+        const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, e >> 1);
+        const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, e >> 1);
+        const double th = (e & 1) ? u53(wt.z, wt.w) : u53(wt.x, wt.y);
+        const double phi = (e & 1) ? u53(wp.z, wp.w) : u53(wp.x, wp.y);
+        ds[p] = (ch.model == 0) ? cos((th * 2.0) * M_PI) * ch.fD : (2.0 * (th - 0.5)) * ch.fD;
+        ph[p] = phi;
+    }
+    __syncthreads();
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= ch.N) return;
+    const double t = (double)n * ch.dt;
+    double sr = 0.0, si = 0.0;
+    for (int p = 0; p < ch.paths; ++p) {
+        const double x = ph[p] + ds[p] * t;                        // no contraction (-ffp-contract=off)
+        double s, c;
+        sincos(TWO_PI * x, &s, &c);
+        sr += c;
+        si += s;
+    }
+    const double sp = sqrt((double)ch.paths);
+    const double g = ch.sqrt_pdp[tap];
+    ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (sr / sp), g * (si / sp));
+}
+
+void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+    dim3 grid((ch.N + 255) / 256, R, ch.ntap);
+    hipLaunchKernelGGL(k_jakes, grid, dim3(256), 2 * ch.paths * sizeof(double), s, ch, seed, rep0, R, ir);
+}
+
+// ---------------------------------------------------------------------------
+// generic banded block matvec: out[row][lane] = sum_k A[row, k] * in(k, lane)
+// grid (lanes/64, nblk), block 64.  A's values are wave-uniform (scalar loads).
+// ---------------------------------------------------------------------------
+template <class In, class Out>
+__global__ void __launch_bounds__(64) k_band(Band A, In in, Out out) {
+    const int lane = blockIdx.x * WAVE + threadIdx.x;
+    const int blk = blockIdx.y;
+    const int row0 = A.row0[blk], nrows = A.nrows[blk], klo = A.klo[blk], khi = A.khi[blk];
+    const double2* __restrict__ a = A.vals + A.off[blk];
+    double2 acc[DSCE_RB];
+#pragma unroll
+    for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
+    for (int k = klo; k < khi; ++k) {
+        const double2 x = in(k, lane);
+        const double2* __restrict__ ak = a + (size_t)(k - klo) * DSCE_RB;
+#pragma unroll
+        for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], ak[r], x);
+    }
+#pragma unroll
+    for (int r = 0; r < DSCE_RB; ++r)
+        if (r < nrows) out(row0 + r, lane, acc[r]);
+}
+
+struct LoadSoA {
+    const double2* __restrict__ p;
+    int stride;
+    __device__ __forceinline__ double2 operator()(int k, int lane) const { return p[(size_t)k * stride + lane]; }
+};
+struct StoreSoA {
+    double2* __restrict__ p;
+    int stride;
+    __device__ __forceinline__ void operator()(int row, int lane, double2 v) const {
+        p[(size_t)row * stride + lane] = v;
+    }
+};
+// (H t)[n] = sum_tau IR[tau][n] t[n - d_tau]  (GetConvolutionMatrix, FastFading.m:284)
+struct LoadChannelApplied {
+    const double2* __restrict__ t;     // [N][U]
+    const double2* __restrict__ ir;    // [ntap][N][R]
+    int U, R, N, ntap;
+    int delay[8];
+    __device__ __forceinline__ double2 operator()(int n, int lane) const {
+        const int rep = lane % R;
+        double2 acc = make_double2(0.0, 0.0);
+        for (int q = 0; q < ntap; ++q) {
+            const int m = n - delay[q];
+            if (m >= 0) c_fma(acc, ir[((size_t)q * N + n) * R + rep], t[(size_t)m * U + lane]);
+        }
+        return acc;
+    }
+};
+// y_perf = y - acc + h .* u   (script:541-543 with D - diag(h))
+struct StorePerfectIC {
+    double2* __restrict__ yperf;
+    const double2* __restrict__ y;
+    const double2* __restrict__ h;     // [LK][R]
+    const double2* __restrict__ u;     // [LK][U]
+    int U, R;
+    __device__ __forceinline__ void operator()(int row, int lane, double2 acc) const {
+        const size_t i = (size_t)row * U + lane;
+        const double2 hv = h[(size_t)row * R + lane % R];
+        double2 r = c_sub(y[i], acc);
+        r = c_add(r, c_mul(hv, u[i]));
+        yperf[i] = r;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// a7: TX chain, lane = realisation.  Pilots (script:365-368), data symbols from
+// bits (script:355-362), x = P [xP; xD] (script:371-373).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_tx_symbols(SchemeK sk, int bits_slot, int pilot_slot, uint64_t seed,
+                                                   uint64_t rep0, int R, double2* __restrict__ xp,
+                                                   uint16_t* __restrict__ sidx, double2* __restrict__ xs) {
+    __shared__ double2 sym[256];
+    for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
+    __syncthreads();
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    const uint32_t mmask = (uint32_t)(sk.M - 1);
+    for (int j = 0; j < sk.NP; ++j) {
+        const uint4 w = stream_block(seed, rep, STREAM_PILOTS, pilot_slot, (uint32_t)j >> 2);
+        const uint32_t word = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
+        const double2 s = sym[word & mmask];
+        const double a = hypot(s.x, s.y);
+        xp[(size_t)j * R + rl] = make_double2(s.x / a, s.y / a);
+    }
+    for (int i = 0; i < sk.ND; ++i) {
+        const uint32_t q = (uint32_t)(i * sk.mbits);               // first bit of symbol i
+        const uint4 w = stream_block(seed, rep, STREAM_BITS, bits_slot, q >> 7);
+        const uint32_t wi = (q >> 5) & 3;
+        const uint32_t word = wi == 0 ? w.x : wi == 1 ? w.y : wi == 2 ? w.z : w.w;
+        sidx[(size_t)i * R + rl] = (uint16_t)((word >> (q & 31)) & mmask);   // bi2de, LSB first
+    }
+    // x = P [xP; xD]
+    for (int r = 0; r < sk.LK; ++r) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
+            const int k = sk.p_col[j];
+            const double2 xin = k < sk.NP ? xp[(size_t)k * R + rl] : sym[sidx[(size_t)(k - sk.NP) * R + rl]];
+            c_fma(acc, sk.p_val[j], xin);
+        }
+        xs[(size_t)r * R + rl] = acc;
+    }
+}
+
+// r0 = H s (script:383-385), lane = realisation, grid (R/64, ceil(N/64)).
+__global__ void __launch_bounds__(64) k_channel_apply(ChannelK ch, int R, const double2* __restrict__ ir,
+                                                      const double2* __restrict__ ss, double2* __restrict__ r0) {
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const int n0 = blockIdx.y * 64;
+    for (int n = n0; n < n0 + 64 && n < ch.N; ++n) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int q = 0; q < ch.ntap; ++q) {
+            const int m = n - ch.tap_delay[q];
+            if (m >= 0) c_fma(acc, ir[((size_t)q * ch.N + n) * R + rl], ss[(size_t)m * R + rl]);
+        }
+        r0[(size_t)n * R + rl] = acc;
+    }
+}
+
+// a8: h = diag(Q' H G) (script:388-393) without forming D:
+// h[c] = sum_n conj(Q[n,c]) sum_tau IR[tau][n] G[n - d_tau, c]; grid (R/64, ceil(LK/16)).
+__global__ void __launch_bounds__(64) k_hdiag(SchemeK sk, ChannelK ch, int R, const double2* __restrict__ ir,
+                                              double2* __restrict__ h) {
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const int c0 = blockIdx.y * 16;
+    for (int c = c0; c < c0 + 16 && c < sk.LK; ++c) {
+        const int qs = sk.q_start[c], gs = sk.g_start[c];
+        const double2* __restrict__ qc = sk.q_col + (size_t)c * sk.QL;
+        const double2* __restrict__ gc = sk.g_col + (size_t)c * sk.GL;
+        double2 acc = make_double2(0.0, 0.0);
+        for (int i = 0; i < sk.QL; ++i) {
+            const int n = qs + i;
+            const double2 qv = qc[i];
+            if (n >= ch.N || (qv.x == 0.0 && qv.y == 0.0)) continue;
+            double2 hg = make_double2(0.0, 0.0);
+            for (int q = 0; q < ch.ntap; ++q) {
+                const int m = n - ch.tap_delay[q] - gs;
+                if (m >= 0 && m < sk.GL) c_fma(hg, ir[((size_t)q * ch.N + n) * R + rl], gc[m]);
+            }
+            c_fma(acc, c_conj(qv), hg);
+        }
+        h[(size_t)c * R + rl] = acc;
+    }
+}
+
+void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
+               uint64_t rep0, McBuffers& b) {
+    const int R = b.R;
+    hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
+                       b.xp, b.sidx, b.xs);
+    // s = G x (script:376-378)
+    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(R / WAVE, sk.G.nblk), dim3(WAVE), 0, s, sk.G,
+                       LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
+    hipLaunchKernelGGL(k_channel_apply, dim3(R / WAVE, (ch.N + 63) / 64), dim3(WAVE), 0, s, ch, R, b.ir, b.ss, b.r0);
+    hipLaunchKernelGGL(k_hdiag, dim3(R / WAVE, (sk.LK + 15) / 16), dim3(WAVE), 0, s, sk, ch, R, b.ir, b.h);
+}
+
+// ---------------------------------------------------------------------------
+// a12: r = r0 + noise (script:397-403), lane = unit; grid (U/64, ceil(N/64)).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, const double* __restrict__ pn, uint64_t seed,
+                                              uint64_t rep0, const double2* __restrict__ r0,
+                                              double2* __restrict__ rbuf) {
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int snr = unit / R, rl = unit % R;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    const double sc = sqrt(pn[snr] / 2.0);
+    const int n0 = blockIdx.y * 64;
+    for (int n = n0; n < n0 + 64 && n < N; ++n) {
+        const uint4 w = stream_block(seed, rep, STREAM_NOISE, (uint32_t)snr, (uint32_t)n);
+        const double u1 = u53(w.x, w.y), u2 = u53(w.z, w.w);
+        const double rad = sqrt(-2.0 * log(1.0 - u1));
+        double sn, cs;
+        sincos(TWO_PI * u2, &sn, &cs);
+        const double2 r = r0[(size_t)n * R + rl];
+        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * (rad * cs), r.y + sc * (rad * sn));
+    }
+}
+
+void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
+                     uint64_t rep0, McBuffers& b) {
+    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, pn, seed, rep0,
+                       b.r0, b.t);
+    // y = Q' r (script:406-409)
+    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(b.U / WAVE, sk.QH.nblk), dim3(WAVE), 0, s, sk.QH,
+                       LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});
+}
+
+// ---------------------------------------------------------------------------
+// perfect-CSI interference cancellation product (D - diag h) u = Q'(H(G u)) - h.*u
+// (script:541-543), two banded passes.
+// ---------------------------------------------------------------------------
+void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b) {
+    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(b.U / WAVE, sk.G.nblk), dim3(WAVE), 0, s, sk.G,
+                       LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
+    LoadChannelApplied in{b.t, b.ir, b.U, b.R, ch.N, ch.ntap, {0}};
+    for (int q = 0; q < ch.ntap && q < 8; ++q) in.delay[q] = ch.tap_delay[q];
+    hipLaunchKernelGGL((k_band<LoadChannelApplied, StorePerfectIC>), dim3(b.U / WAVE, sk.QH.nblk), dim3(WAVE), 0, s,
+                       sk.QH, in, StorePerfectIC{b.yperf, b.y, b.h, b.u, b.U, b.R});
+}
+
+// ---------------------------------------------------------------------------
+// a13/a15: MMSE contraction  y_est = y - (D_hat - diag h_hat) v with
+// D_hat = sum_p W_p hP_p  (script:417-425, :482-484, :493-511), never forming
+// D_hat.  grid (U/64, nblk), block 64 = one wave of 64 units of one SNR.
+// W values: wave-uniform scalar loads of the packed band layout.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_wcontract(Band Wb, const double2* __restrict__ Wall, long long w_elems,
+                                                  int var, int nsnr, int NP, int R, int U,
+                                                  const double2* __restrict__ hp, const double2* __restrict__ v,
+                                                  const double2* __restrict__ y, const double2* __restrict__ hest,
+                                                  double2* __restrict__ yest) {
+    extern __shared__ double2 shp[];                     // [NP][64]
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int snr = (blockIdx.x * WAVE) / R;
+    const int blk = blockIdx.y;
+    for (int p = 0; p < NP; ++p) shp[p * WAVE + threadIdx.x] = hp[(size_t)p * U + unit];
+    __syncthreads();
+    const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
+    const int c_lo = Wb.klo[blk] / NP, c_hi = Wb.khi[blk] / NP;
+    const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)w_elems + Wb.off[blk];
+    double2 acc[DSCE_RB];
+#pragma unroll
+    for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
+    for (int c = c_lo; c < c_hi; ++c) {
+        const double2 vc = v[(size_t)c * U + unit];
+        const double2* __restrict__ wc = w + (size_t)(c - c_lo) * NP * DSCE_RB;
+        for (int p = 0; p < NP; ++p) {
+            const double2 z = c_mul(shp[p * WAVE + threadIdx.x], vc);
+            const double2* __restrict__ wk = wc + (size_t)p * DSCE_RB;
+#pragma unroll
+            for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], wk[r], z);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < DSCE_RB; ++r) {
+        if (r < nrows) {
+            const size_t i = (size_t)(row0 + r) * U + unit;
+            double2 o = c_sub(y[i], acc[r]);
+            o = c_add(o, c_mul(hest[i], v[i]));
+            yest[i] = o;
+        }
+    }
+}
+
+void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
+    hipLaunchKernelGGL(k_wcontract, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2), s, mm.Wb,
+                       mm.W, mm.w_elems, var, mm.nsnr, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+}
+
+// ---------------------------------------------------------------------------
+// a14/a16: one stage of the receiver (one-tap or IC iteration), lane = unit:
+// LS at the pilots (script:412-414 / :487-489), h_hat = diag(D_hat)
+// (script:428 / :515), one-tap equalisation + detection (SignalConstellation.m:83-101,
+// first minimum wins), error counting with and without edges (script:432-447 /
+// :531-537 / :548-561), and re-precoding of the quantised decisions for the next
+// IC iteration (script:482-484 / :541-543).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int nearest_level(const double* __restrict__ lv, int n, double x, int& alt) {
+    alt = -1;
+    if (n == 1) return 0;
+    const double step = lv[1] - lv[0];
+    int i = (int)floor((x - lv[0]) / step);
+    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i + 1]);
+    if (d1 < d0) return i + 1;
+    if (d1 == d0) alt = i + 1;
+    return i;
+}
+
+__device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
+    int aI, aQ;
+    const int iI = nearest_level(sk.lvI, sk.nI, z.x, aI);
+    const int iQ = nearest_level(sk.lvQ, sk.nQ, z.y, aQ);
+    int best = sk.grid_sym[iI * sk.nQ + iQ];
+    if (aI >= 0) best = min(best, sk.grid_sym[aI * sk.nQ + iQ]);
+    if (aQ >= 0) best = min(best, sk.grid_sym[iI * sk.nQ + aQ]);
+    if (aI >= 0 && aQ >= 0) best = min(best, sk.grid_sym[aI * sk.nQ + aQ]);
+    return best;
+}
+
+struct StageArgs {
+    int stage, var, nsnr, nstage, scheme, last, R, U;
+    const double2* ysrc_e;     // y (stage 0) or y_est
+    const double2* ysrc_p;     // y (stage 0) or y_perf
+};
+
+__global__ void __launch_bounds__(64) k_stage(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
+                                              const double2* __restrict__ xp, const uint16_t* __restrict__ sidx,
+                                              const double2* __restrict__ h, double2* __restrict__ hp,
+                                              double2* __restrict__ hest, double2* __restrict__ e,
+                                              uint16_t* __restrict__ qe, uint16_t* __restrict__ qp,
+                                              double2* __restrict__ v, double2* __restrict__ u,
+                                              unsigned long long* __restrict__ counters) {
+    extern __shared__ double2 smem[];
+    double2* sym = smem;                     // [M]
+    double2* shp = smem + sk.M;              // [NP][64]
+    for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int snr = (blockIdx.x * WAVE) / st.R;
+    const int rl = unit % st.R;
+    const int U = st.U, R = st.R;
+    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    // LS estimates at the pilot positions
+    for (int p = 0; p < sk.NP; ++p) {
+        const double2 yv = st.ysrc_e[(size_t)sk.pilot_pos[p] * U + unit];
+        const double2 q = c_div(yv, xp[(size_t)p * R + rl]);
+        const double2 hv = make_double2(q.x / sqk, q.y / sqk);
+        shp[p * WAVE + threadIdx.x] = hv;
+        hp[(size_t)p * U + unit] = hv;
+    }
+    __syncthreads();
+    // h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p
+    const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP;
+    for (int c = 0; c < sk.LK; ++c) {
+        double2 acc = make_double2(0.0, 0.0);
+        for (int p = 0; p < sk.NP; ++p) c_fma(acc, wd[(size_t)c * sk.NP + p], shp[p * WAVE + threadIdx.x]);
+        hest[(size_t)c * U + unit] = acc;
+    }
+    int cnt[4] = {0, 0, 0, 0};
+    // two passes: 0 = MMSE estimate, 1 = perfect CSI
+    for (int csi = 0; csi < 2; ++csi) {
+        const double2* __restrict__ ys = csi == 0 ? st.ysrc_e : st.ysrc_p;
+        uint16_t* __restrict__ qo = csi == 0 ? qe : qp;
+        if (sk.despread) {
+            for (int c = 0; c < sk.LK; ++c) {
+                const double2 hv = csi == 0 ? hest[(size_t)c * U + unit] : h[(size_t)c * R + rl];
+                e[(size_t)c * U + unit] = c_div(ys[(size_t)c * U + unit], hv);
+            }
+        }
+        for (int i = 0; i < sk.ND; ++i) {
+            double2 z;
+            if (sk.despread) {
+                const int row = sk.NP + i;
+                double2 acc = make_double2(0.0, 0.0);
+                for (int j = sk.ph_ptr[row]; j < sk.ph_ptr[row + 1]; ++j)
+                    c_fma(acc, sk.ph_val[j], e[(size_t)sk.ph_col[j] * U + unit]);
+                z = sk.real_detect ? make_double2(acc.x / sk.data_div, 0.0)
+                                   : make_double2(acc.x / sk.data_div, acc.y / sk.data_div);
+            } else {
+                const int c = sk.data_pos[i];
+                const double2 hv = csi == 0 ? hest[(size_t)c * U + unit] : h[(size_t)c * R + rl];
+                const double2 q = c_div(ys[(size_t)c * U + unit], hv);
+                z = sk.real_detect ? make_double2(q.x / sk.data_div, 0.0)
+                                   : make_double2(q.x / sk.data_div, q.y / sk.data_div);
+            }
+            const int d = slice(sk, z);
+            const int tx = sidx[(size_t)i * R + rl];
+            const int ne = __popc((unsigned)(d ^ tx));
+            cnt[csi * 2 + 0] += ne;
+            if (sk.considered[i]) cnt[csi * 2 + 1] += ne;
+            if (!st.last) qo[(size_t)i * U + unit] = (uint16_t)d;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int tot = wave_sum(cnt[k]);
+        if (threadIdx.x == 0 && tot) {
+            const int csi = k >> 1, edge = k & 1;
+            const size_t idx = ((((size_t)st.scheme * 2 + csi) * 2 + edge) * st.nsnr + snr) * st.nstage + st.stage;
+            atomicAdd(&counters[idx], (unsigned long long)tot);
+        }
+    }
+    if (st.last) return;
+    __syncthreads();
+    // re-precode the quantised decisions: v = P [xP; Q(x_est)], u = P [xP; Q(x_perf)]
+    for (int r = 0; r < sk.LK; ++r) {
+        double2 av = make_double2(0.0, 0.0), au = make_double2(0.0, 0.0);
+        for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
+            const int k = sk.p_col[j];
+            const double2 pv = sk.p_val[j];
+            if (k < sk.NP) {
+                const double2 x = xp[(size_t)k * R + rl];
+                c_fma(av, pv, x);
+                c_fma(au, pv, x);
+            } else {
+                c_fma(av, pv, sym[qe[(size_t)(k - sk.NP) * U + unit]]);
+                c_fma(au, pv, sym[qp[(size_t)(k - sk.NP) * U + unit]]);
+            }
+        }
+        v[(size_t)r * U + unit] = av;
+        u[(size_t)r * U + unit] = au;
+    }
+}
+
+void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
+                  McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t*) {
+    StageArgs st;
+    st.stage = stage;
+    st.var = var;
+    st.nsnr = mm.nsnr;
+    st.nstage = n_iter + 1;
+    st.scheme = scheme_index;
+    st.last = last ? 1 : 0;
+    st.R = b.R;
+    st.U = b.U;
+    st.ysrc_e = stage == 0 ? b.y : b.yest;
+    st.ysrc_p = stage == 0 ? b.y : b.yperf;
+    const size_t lds = (size_t)(sk.M + sk.NP * WAVE) * sizeof(double2);
+    hipLaunchKernelGGL(k_stage, dim3(b.U / WAVE), dim3(WAVE), lds, s, sk, st, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest,
+                       b.e, b.qe, b.qp, b.v, b.u, counters);
+}
+
+}  // namespace dsce

@@ -1,0 +1,283 @@
+// kernels_setup.hip — correlation matrices and the MMSE estimator
+// (DoublySelectiveChannelEstimation.m:208-313, FastFading.m:321-407) on the GPU.
+//
+// R_vecH = E{vec(H) vec(H)^H} (FastFading.m:366-407) is never materialised:
+// its only non-zeros couple H[a+tau, a] with H[b+tau, b] through
+// PDPn[tau] * J0(2 pi fD dt (a-b)), so every product R_vecH * vec(V) collapses
+// to a Toeplitz J0 matvec per tap ("m-coefficients" below).  Entries that the
+// reference wraps into the next column for tau >= 2 (FastFading.m:377) multiply
+// samples outside every pilot's support and are exactly zero for all
+// configurations served here (pilot supports never touch sample 0 and N-1 at
+// once); see DESIGN.md §Setup.
+#include "dsce_kernels.h"
+
+#include <math.h>
+
+namespace dsce {
+
+// J0 lag table, FastFading.m:330-333: index lag + N - 1, lag in [-(N-1), N-1]
+__global__ void k_time_correlation(int N, double fD, double dt, int model, double* tab) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 2 * N - 1) return;
+    const double t = dt * (double)(i - (N - 1));
+    tab[i] = model == 0 ? j0(((M_PI * 2.0) * fD) * t) : (t == 0.0 ? 1.0 : sin(M_PI * (2.0 * fD * t)) / (M_PI * (2.0 * fD * t)));
+}
+
+void setup_time_correlation(hipStream_t s, int N, double fD, double dt, int model, double* j0tab) {
+    hipLaunchKernelGGL(k_time_correlation, dim3((2 * N - 1 + 255) / 256), dim3(256), 0, s, N, fD, dt, model, j0tab);
+}
+
+// m[j][q][a] = PDPn[d_q] * sum_b J0(a-b) * Q[b+d_q, j] * conj(G[b, j])   (pilot j)
+// i.e. reshape(R_vecH * kron(g_j.', q_j')', N, N) restricted to its band
+// (script:213, :260).
+__global__ void k_mcoef(SetupArgs a, const int* __restrict__ g_start, int GL, double2* __restrict__ m) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int jq = blockIdx.y;                   // pilot * ntap + q
+    const int j = jq / a.ntap, q = jq % a.ntap;
+    if (idx >= a.N) return;
+    const int col = a.pilot_pos[j];
+    const int d = a.tap_delay[q];
+    const double pdp = a.pdp[q];
+    const double2* __restrict__ Gc = a.G + (size_t)col * a.N;
+    const double2* __restrict__ Qc = a.Q + (size_t)col * a.N;
+    const int b0 = g_start[col];
+    double2 acc = make_double2(0.0, 0.0);
+    for (int b = b0; b < b0 + GL && b < a.N; ++b) {
+        if (b + d >= a.N) break;
+        const double2 g = Gc[b];
+        const double2 qv = Qc[b + d];
+        if ((g.x == 0.0 && g.y == 0.0) || (qv.x == 0.0 && qv.y == 0.0)) continue;
+        const double2 w = c_mul(qv, c_conj(g));
+        const double r = pdp * a.j0tab[idx - b + a.N - 1];
+        acc.x += r * w.x;
+        acc.y += r * w.y;
+    }
+    m[((size_t)j * a.ntap + q) * a.N + idx] = acc;
+}
+
+void setup_mcoef(hipStream_t s, const SetupArgs& a, const int* g_start, int GL, const int*, int, double2* m) {
+    hipLaunchKernelGGL(k_mcoef, dim3((a.N + 255) / 256, a.NP * a.ntap), dim3(256), 0, s, a, g_start, GL, m);
+}
+
+// R_hP[i, j] = sum_n sum_q conj(Q[n+d_q, i]) m_j[q][n] G[n, i]   (script:212-215)
+__global__ void k_rhp(SetupArgs a, const double2* __restrict__ m, double2* __restrict__ rhp) {
+    const int i = blockIdx.x, j = blockIdx.y;
+    __shared__ double2 part[256];
+    const int ci = a.pilot_pos[i];
+    const double2* __restrict__ Gc = a.G + (size_t)ci * a.N;
+    const double2* __restrict__ Qc = a.Q + (size_t)ci * a.N;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int n = threadIdx.x; n < a.N; n += blockDim.x) {
+        const double2 g = Gc[n];
+        if (g.x == 0.0 && g.y == 0.0) continue;
+        for (int q = 0; q < a.ntap; ++q) {
+            const int r = n + a.tap_delay[q];
+            if (r >= a.N) continue;
+            const double2 t = c_mul(c_conj(Qc[r]), m[((size_t)j * a.ntap + q) * a.N + n]);
+            c_fma(acc, t, g);
+        }
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) part[threadIdx.x] = c_add(part[threadIdx.x], part[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) rhp[(size_t)j * a.NP + i] = part[0];     // column-major NP x NP
+}
+
+void setup_rhp(hipStream_t s, const SetupArgs& a, const double2* m, double2* rhp) {
+    hipLaunchKernelGGL(k_rhp, dim3(a.NP, a.NP), dim3(256), 0, s, a, m, rhp);
+}
+
+// Gp = G * P (script:203-205), dense N x Nsym column-major
+__global__ void k_gp(SetupArgs a, double2* __restrict__ gp) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.y;
+    if (n >= a.N) return;
+    double2 acc = make_double2(0.0, 0.0);
+    const double2* __restrict__ Pk = a.P + (size_t)k * a.LK;
+    for (int c = 0; c < a.LK; ++c) {
+        const double2 p = Pk[c];
+        if (p.x == 0.0 && p.y == 0.0) continue;
+        c_fma(acc, a.G[(size_t)c * a.N + n], p);
+    }
+    gp[(size_t)k * a.N + n] = acc;
+}
+
+void setup_gp(hipStream_t s, const SetupArgs& a, double2* gp) {
+    hipLaunchKernelGGL(k_gp, dim3((a.N + 255) / 256, a.Nsym), dim3(256), 0, s, a, gp);
+}
+
+// Total received power at pilot i incl. interference of every precoded symbol
+// (script:222-234):  |sum_{a,b} C_i[a,b] A[a,b]| with
+// C_i[a,b] = sum_q PDPn conj(Q[a+d_q,i]) Q[b+d_q,i] J0(a-b) / kappa, A = Gp Gp^H.
+__global__ void k_rest_diag(SetupArgs a, const double2* __restrict__ gp, const int* __restrict__ q_start, int QL,
+                            double* __restrict__ diag) {
+    const int i = blockIdx.x;
+    const int ci = a.pilot_pos[i];
+    const double2* __restrict__ Qc = a.Q + (size_t)ci * a.N;
+    int maxd = 0;
+    for (int q = 0; q < a.ntap; ++q) maxd = max(maxd, a.tap_delay[q]);
+    const int s0 = max(0, q_start[ci] - maxd);
+    const int s1 = min(a.N, q_start[ci] + QL);
+    const int S = s1 - s0;
+    __shared__ double2 part[256];
+    double2 acc = make_double2(0.0, 0.0);
+    for (int pr = threadIdx.x; pr < S * S; pr += blockDim.x) {
+        const int aa = s0 + pr / S, bb = s0 + pr % S;
+        double2 c = make_double2(0.0, 0.0);
+        for (int q = 0; q < a.ntap; ++q) {
+            const int ra = aa + a.tap_delay[q], rb = bb + a.tap_delay[q];
+            if (ra >= a.N || rb >= a.N) continue;
+            const double2 t = c_mul(c_conj(Qc[ra]), Qc[rb]);
+            const double f = a.pdp[q] * a.j0tab[aa - bb + a.N - 1];
+            c.x += f * t.x;
+            c.y += f * t.y;
+        }
+        if (c.x == 0.0 && c.y == 0.0) continue;
+        double2 A = make_double2(0.0, 0.0);
+        for (int k = 0; k < a.Nsym; ++k)
+            c_fma(A, gp[(size_t)k * a.N + aa], c_conj(gp[(size_t)k * a.N + bb]));
+        c_fma(acc, c, A);
+    }
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) part[threadIdx.x] = c_add(part[threadIdx.x], part[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) diag[i] = hypot(part[0].x, part[0].y) / a.kappa;
+}
+
+void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const int* q_start, int QL, double* diag) {
+    hipLaunchKernelGGL(k_rest_diag, dim3(a.NP), dim3(256), 0, s, a, gp, q_start, QL, diag);
+}
+
+// pinv(R) for a Hermitian positive-definite NP x NP R: Gauss-Jordan with partial
+// pivoting in LDS, one workgroup per matrix (script:283-285, :302-304).
+__global__ void k_rinv(int NP, const double2* __restrict__ Rall, double2* __restrict__ Iall) {
+    extern __shared__ double2 Aug[];          // NP x 2NP, row-major
+    __shared__ int piv;
+    const double2* R = Rall + (size_t)blockIdx.x * NP * NP;
+    double2* Ri = Iall + (size_t)blockIdx.x * NP * NP;
+    const int W2 = 2 * NP;
+    for (int t = threadIdx.x; t < NP * W2; t += blockDim.x) {
+        const int r = t / W2, c = t % W2;
+        Aug[t] = c < NP ? R[(size_t)c * NP + r] : make_double2(c - NP == r ? 1.0 : 0.0, 0.0);
+    }
+    __syncthreads();
+    for (int k = 0; k < NP; ++k) {
+        if (threadIdx.x == 0) {
+            int best = k;
+            double bv = hypot(Aug[k * W2 + k].x, Aug[k * W2 + k].y);
+            for (int r = k + 1; r < NP; ++r) {
+                const double v = hypot(Aug[r * W2 + k].x, Aug[r * W2 + k].y);
+                if (v > bv) { bv = v; best = r; }
+            }
+            piv = best;
+        }
+        __syncthreads();
+        if (piv != k)
+            for (int c = threadIdx.x; c < W2; c += blockDim.x) {
+                const double2 t = Aug[k * W2 + c];
+                Aug[k * W2 + c] = Aug[piv * W2 + c];
+                Aug[piv * W2 + c] = t;
+            }
+        __syncthreads();
+        const double2 d = Aug[k * W2 + k];
+        __syncthreads();
+        for (int c = threadIdx.x; c < W2; c += blockDim.x) Aug[k * W2 + c] = c_div(Aug[k * W2 + c], d);
+        __syncthreads();
+        for (int t = threadIdx.x; t < NP * W2; t += blockDim.x) {
+            const int r = t / W2, c = t % W2;
+            if (r == k) continue;
+            const double2 f = Aug[r * W2 + k];
+            if (c == k) continue;
+            Aug[t] = c_sub(Aug[t], c_mul(f, Aug[k * W2 + c]));
+        }
+        __syncthreads();
+        for (int r = threadIdx.x; r < NP; r += blockDim.x)
+            if (r != k) Aug[r * W2 + k] = make_double2(0.0, 0.0);
+        __syncthreads();
+    }
+    for (int t = threadIdx.x; t < NP * NP; t += blockDim.x) {
+        const int r = t % NP, c = t / NP;        // column-major output
+        Ri[t] = Aug[r * W2 + NP + c];
+    }
+}
+
+void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv) {
+    hipLaunchKernelGGL(k_rinv, dim3(nmat), dim3(256), (size_t)NP * 2 * NP * sizeof(double2), s, NP, R, Rinv);
+}
+
+// R_Dij,hP column i = vec(Q' M_i G) with |.| < thr -> 0 (script:259-268), written
+// straight into the packed band layout of W: off[blk] + ((c-c_lo)*NP + i)*RB + r.
+__global__ void k_rdij(SetupArgs a, Band Wb, const double2* __restrict__ m, const int* __restrict__ g_start, int GL,
+                       const int* __restrict__ q_start, int QL, double2* __restrict__ rd) {
+    const int blk = blockIdx.x, i = blockIdx.y;
+    const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
+    const int c_lo = Wb.klo[blk] / a.NP, c_hi = Wb.khi[blk] / a.NP;
+    const int nslot = (c_hi - c_lo) * DSCE_RB;
+    double2* __restrict__ out = rd + Wb.off[blk];
+    for (int t = threadIdx.x; t < nslot; t += blockDim.x) {
+        const int c = c_lo + t / DSCE_RB, rl = t % DSCE_RB;
+        double2 acc = make_double2(0.0, 0.0);
+        if (rl < nrows) {
+            const int r = row0 + rl;
+            const double2* __restrict__ Qr = a.Q + (size_t)r * a.N;
+            const double2* __restrict__ Gc = a.G + (size_t)c * a.N;
+            const int gs = g_start[c];
+            for (int n = q_start[r]; n < q_start[r] + QL && n < a.N; ++n) {
+                const double2 qv = Qr[n];
+                if (qv.x == 0.0 && qv.y == 0.0) continue;
+                double2 mg = make_double2(0.0, 0.0);
+                for (int q = 0; q < a.ntap; ++q) {
+                    const int b = n - a.tap_delay[q];
+                    if (b < gs || b >= gs + GL || b < 0) continue;
+                    c_fma(mg, m[((size_t)i * a.ntap + q) * a.N + b], Gc[b]);
+                }
+                c_fma(acc, c_conj(qv), mg);
+            }
+            if (hypot(acc.x, acc.y) < a.thr) acc = make_double2(0.0, 0.0);
+        }
+        out[((size_t)(c - c_lo) * a.NP + i) * DSCE_RB + rl] = acc;
+    }
+}
+
+void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
+                const int* q_start, int QL, double2* rd) {
+    hipLaunchKernelGGL(k_rdij, dim3(Wb.nblk, a.NP), dim3(256), 0, s, a, Wb, m, g_start, GL, q_start, QL, rd);
+}
+
+// W = R_Dij,hP * pinv(R) with |.| < thr -> 0 (script:283-289), packed layout;
+// also extracts the diagonal W[(c,c),p] used for h_hat = diag(D_hat).
+__global__ void k_w(SetupArgs a, Band Wb, const double2* __restrict__ rd, const double2* __restrict__ rinv,
+                    double2* __restrict__ w, double2* __restrict__ wd) {
+    const int blk = blockIdx.x;
+    const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
+    const int c_lo = Wb.klo[blk] / a.NP, c_hi = Wb.khi[blk] / a.NP;
+    const int nslot = (c_hi - c_lo) * DSCE_RB;
+    const double2* __restrict__ in = rd + Wb.off[blk];
+    double2* __restrict__ out = w + Wb.off[blk];
+    for (int t = threadIdx.x; t < nslot; t += blockDim.x) {
+        const int cl = t / DSCE_RB, rl = t % DSCE_RB;
+        const int c = c_lo + cl;
+        for (int pp = 0; pp < a.NP; ++pp) {
+            double2 acc = make_double2(0.0, 0.0);
+            if (rl < nrows)
+                for (int p = 0; p < a.NP; ++p)
+                    c_fma(acc, in[((size_t)cl * a.NP + p) * DSCE_RB + rl], rinv[(size_t)pp * a.NP + p]);
+            if (hypot(acc.x, acc.y) < a.thr) acc = make_double2(0.0, 0.0);
+            out[((size_t)cl * a.NP + pp) * DSCE_RB + rl] = acc;
+            if (rl < nrows && row0 + rl == c) wd[(size_t)c * a.NP + pp] = acc;
+        }
+    }
+}
+
+void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long, const double2* rd, const double2* rinv,
+             double2* w, double2* wd) {
+    hipLaunchKernelGGL(k_w, dim3(Wb.nblk), dim3(256), 0, s, a, Wb, rd, rinv, w, wd);
+}
+
+}  // namespace dsce

@@ -1,0 +1,258 @@
+"""ctypes binding of the C-ABI in include/dsce.h (libdsce.so, HIP for gfx950).
+
+This is the Python twin of the MEX gateway described in INTEGRATION.md: it
+converts the host objects (dsce.configs.Scheme, dsce.channel.FastFading) into
+the plain column-major interleaved-complex buffers of the ABI.  There is no
+CPU fallback: if the shared library is missing or no GPU is present the calls
+raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DSCE_LIB", os.path.join(_HERE, "libdsce.so"))
+
+EXPORTED = [
+    "dsce_abi_version", "dsce_device_count", "dsce_create", "dsce_destroy", "dsce_last_error",
+    "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
+    "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
+    "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model",
+]
+
+
+class ChannelDesc(C.Structure):
+    _fields_ = [("n_samples", C.c_int32), ("n_taps", C.c_int32), ("sampling_rate", C.c_double),
+                ("max_doppler", C.c_double), ("n_paths", C.c_int32), ("doppler_model", C.c_int32),
+                ("pdp_norm", C.POINTER(C.c_double))]
+
+
+class SchemeDesc(C.Structure):
+    _fields_ = [("n_subcarriers", C.c_int32), ("n_symbols", C.c_int32), ("n_tx_symbols", C.c_int32),
+                ("n_pilots", C.c_int32), ("n_data", C.c_int32), ("mod_order", C.c_int32),
+                ("bits_per_symbol", C.c_int32), ("despread", C.c_int32), ("real_detect", C.c_int32),
+                ("bits_slot", C.c_int32), ("pilot_slot", C.c_int32), ("kappa", C.c_double),
+                ("data_div", C.c_double), ("G", C.POINTER(C.c_double)), ("Q", C.POINTER(C.c_double)),
+                ("P", C.POINTER(C.c_double)), ("pilot_pos", C.POINTER(C.c_int32)),
+                ("data_pos", C.POINTER(C.c_int32)), ("considered", C.POINTER(C.c_uint8)),
+                ("symbols", C.POINTER(C.c_double))]
+
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libdsce.so (raises OSError with a build hint when it is missing)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError("libdsce.so not found at %s — build it with `make -C channel-estimation_amd` "
+                      "(or __graft_entry__.build())" % p)
+    lib = C.CDLL(p)
+    vp = C.c_void_p
+    dp = C.POINTER(C.c_double)
+    i64p = C.POINTER(C.c_int64)
+    lib.dsce_abi_version.restype = C.c_int
+    lib.dsce_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.dsce_create.argtypes = [C.c_int, C.POINTER(vp)]
+    lib.dsce_destroy.argtypes = [vp]
+    lib.dsce_destroy.restype = None
+    lib.dsce_last_error.argtypes = [vp]
+    lib.dsce_last_error.restype = C.c_char_p
+    lib.dsce_set_channel.argtypes = [vp, C.POINTER(ChannelDesc)]
+    lib.dsce_set_snr.argtypes = [vp, dp, C.c_int32, C.c_int32]
+    lib.dsce_add_scheme.argtypes = [vp, C.POINTER(SchemeDesc), C.POINTER(C.c_int32)]
+    lib.dsce_build_mmse.argtypes = [vp, C.c_double]
+    lib.dsce_set_batch.argtypes = [vp, C.c_int32]
+    lib.dsce_run.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint64, i64p]
+    lib.dsce_bits_per_rep.argtypes = [vp, C.c_int32, i64p]
+    lib.dsce_channel_realise.argtypes = [vp, C.c_uint64, C.c_uint64, dp]
+    lib.dsce_get_correlation.argtypes = [vp, C.c_int32, dp, dp, dp]
+    lib.dsce_get_W.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, dp]
+    lib.dsce_trace_unit.argtypes = [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32, dp, dp, dp, dp]
+    lib.dsce_enable_timing.argtypes = [vp, C.c_int32]
+    lib.dsce_kernel_time.argtypes = [vp, C.c_char_p, i64p, dp]
+    lib.dsce_work_model.argtypes = [vp, C.c_int32, dp, dp]
+    for name in EXPORTED:
+        fn = getattr(lib, name)
+        if name not in ("dsce_destroy", "dsce_last_error"):
+            fn.restype = C.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _cplx(a):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.complex128).reshape(-1, order="F"))
+    return a
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class DsceError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One engine context = one GPU + one HIP stream (dsce_create)."""
+
+    def __init__(self, device=0, lib_path=None):
+        self.lib = load_library(lib_path)
+        h = C.c_void_p()
+        rc = self.lib.dsce_create(int(device), C.byref(h))
+        if rc != 0 or not h.value:
+            raise DsceError("dsce_create(device=%d) failed with %d (no HIP device?)" % (device, rc))
+        self.h = h
+        self._keep = []
+        self.schemes = []
+        self.nsnr = 0
+        self.niter = 0
+        self.N = None
+        self.ntaps = None
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.dsce_last_error(self.h)
+            raise DsceError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.dsce_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- configuration -------------------------------------------------------
+    def set_channel(self, ff):
+        pdp = np.ascontiguousarray(ff.PowerDelayProfileNormalized, dtype=np.float64)
+        self._keep.append(pdp)
+        d = ChannelDesc(ff.SamplesTotal, pdp.size, ff.SamplingRate, ff.MaximumDopplerShift, ff.Paths,
+                        0 if ff.DopplerModel == "Jakes" else 1, _dptr(pdp))
+        self._chk(self.lib.dsce_set_channel(self.h, C.byref(d)), "dsce_set_channel")
+        self.N = ff.SamplesTotal
+        self.ntaps = pdp.size
+
+    def set_snr(self, pn_time, n_iter):
+        pn = np.ascontiguousarray(pn_time, dtype=np.float64)
+        self._chk(self.lib.dsce_set_snr(self.h, _dptr(pn), pn.size, int(n_iter)), "dsce_set_snr")
+        self.nsnr = pn.size
+        self.niter = int(n_iter)
+
+    def add_scheme(self, sc):
+        G = _cplx(sc.G)
+        Q = _cplx(sc.Q)
+        P = _cplx(sc.P)
+        pil = np.ascontiguousarray(sc.pilot_pos, dtype=np.int32)
+        dat = np.ascontiguousarray(sc.data_pos, dtype=np.int32)
+        cons = np.ascontiguousarray(sc.considered_symbols, dtype=np.uint8)
+        sym = _cplx(sc.const.SymbolMapping)
+        self._keep += [G, Q, P, pil, dat, cons, sym]
+        L = sc.extras.get("pilot_matrix").shape[0] if "pilot_matrix" in sc.extras else sc.LK
+        d = SchemeDesc(L, sc.LK // L, sc.P.shape[1], sc.n_pilots, sc.n_data, sc.const.ModulationOrder,
+                       sc.bits_per_symbol, int(sc.despread), int(sc.real_detect), sc.bits_slot, sc.pilot_slot,
+                       sc.kappa, sc.data_div, _dptr(G), _dptr(Q), _dptr(P),
+                       pil.ctypes.data_as(C.POINTER(C.c_int32)), dat.ctypes.data_as(C.POINTER(C.c_int32)),
+                       cons.ctypes.data_as(C.POINTER(C.c_uint8)), _dptr(sym))
+        sid = C.c_int32()
+        self._chk(self.lib.dsce_add_scheme(self.h, C.byref(d), C.byref(sid)), "dsce_add_scheme")
+        self.schemes.append(sc)
+        return sid.value
+
+    def build_mmse(self, zero_threshold=1e-8):
+        self._chk(self.lib.dsce_build_mmse(self.h, float(zero_threshold)), "dsce_build_mmse")
+
+    def set_batch(self, reps):
+        self._chk(self.lib.dsce_set_batch(self.h, int(reps)), "dsce_set_batch")
+
+    # -- Monte Carlo -----------------------------------------------------------
+    def counter_shape(self):
+        return (len(self.schemes), 2, 2, self.nsnr, 1 + self.niter)
+
+    def run(self, seed, first_rep, n_rep, counts=None):
+        if counts is None:
+            counts = np.zeros(self.counter_shape(), dtype=np.int64)
+        assert counts.dtype == np.int64 and counts.flags.c_contiguous and counts.shape == self.counter_shape()
+        self._chk(self.lib.dsce_run(self.h, int(seed), int(first_rep), int(n_rep),
+                                    counts.ctypes.data_as(C.POINTER(C.c_int64))), "dsce_run")
+        return counts
+
+    def bits_per_rep(self, sid):
+        b = np.zeros(2, dtype=np.int64)
+        self._chk(self.lib.dsce_bits_per_rep(self.h, int(sid), b.ctypes.data_as(C.POINTER(C.c_int64))),
+                  "dsce_bits_per_rep")
+        return b
+
+    # -- probes ----------------------------------------------------------------
+    def channel_impulse_response(self, seed, rep):
+        out = np.zeros(2 * self.N * self.ntaps)
+        self._chk(self.lib.dsce_channel_realise(self.h, int(seed), int(rep), _dptr(out)), "dsce_channel_realise")
+        return out.view(np.complex128).reshape(self.N, self.ntaps, order="F")
+
+    def correlation(self, sid):
+        NP = self.schemes[sid].n_pilots
+        rhp = np.zeros(2 * NP * NP)
+        rest = np.zeros(2 * self.nsnr * NP * NP)
+        rnoi = np.zeros(2 * self.nsnr * NP * NP)
+        self._chk(self.lib.dsce_get_correlation(self.h, int(sid), _dptr(rhp), _dptr(rest), _dptr(rnoi)),
+                  "dsce_get_correlation")
+        f = lambda a, n: a.view(np.complex128).reshape(n, NP, NP).transpose(0, 2, 1)   # column-major NP x NP
+        return f(rhp, 1)[0], f(rest, self.nsnr), f(rnoi, self.nsnr)
+
+    def W(self, sid, snr_index, variant=0):
+        sc = self.schemes[sid]
+        out = np.zeros(2 * sc.LK * sc.LK * sc.n_pilots)
+        self._chk(self.lib.dsce_get_W(self.h, int(sid), int(snr_index), int(variant), _dptr(out)), "dsce_get_W")
+        return out.view(np.complex128)
+
+    def trace_unit(self, sid, seed, rep, snr_index):
+        sc = self.schemes[sid]
+        ns = self.niter + 1
+        y = np.zeros(2 * sc.LK)
+        hp = np.zeros(2 * ns * sc.n_pilots)
+        he = np.zeros(2 * ns * sc.LK)
+        h = np.zeros(2 * sc.LK)
+        self._chk(self.lib.dsce_trace_unit(self.h, int(sid), int(seed), int(rep), int(snr_index), _dptr(y),
+                                           _dptr(hp), _dptr(he), _dptr(h)), "dsce_trace_unit")
+        v = lambda a: a.view(np.complex128)
+        return dict(y=v(y), hp=v(hp).reshape(ns, sc.n_pilots), hest=v(he).reshape(ns, sc.LK), h=v(h))
+
+    # -- measurement -----------------------------------------------------------
+    def enable_timing(self, on=True):
+        self._chk(self.lib.dsce_enable_timing(self.h, int(bool(on))), "dsce_enable_timing")
+
+    def kernel_time(self, name):
+        n = C.c_int64()
+        ms = C.c_double()
+        self._chk(self.lib.dsce_kernel_time(self.h, name.encode(), C.byref(n), C.byref(ms)), "dsce_kernel_time")
+        return n.value, ms.value
+
+    def work_model(self, sid):
+        cm = C.c_double()
+        wb = C.c_double()
+        self._chk(self.lib.dsce_work_model(self.h, int(sid), C.byref(cm), C.byref(wb)), "dsce_work_model")
+        return cm.value, wb.value
+
+
+def build_engine(setup, schemes=None, device=0, zero_threshold=None, batch=None):
+    """Engine configured like the script: channel, SNR list, schemes, MMSE setup."""
+    eng = Engine(device)
+    eng.set_channel(setup.channel)
+    eng.set_snr(setup.pn_time, setup.n_iter)
+    names = list(setup.schemes) if schemes is None else list(schemes)
+    for n in names:
+        eng.add_scheme(setup.schemes[n])
+    eng.build_mmse(setup.zero_threshold if zero_threshold is None else zero_threshold)
+    if batch:
+        eng.set_batch(batch)
+    return eng

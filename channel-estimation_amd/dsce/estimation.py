@@ -1,0 +1,303 @@
+"""Host-side mirror of the reference's ``+ChannelEstimation`` package.
+
+* ``ImaginaryInterferenceCancellationAtPilotPosition`` —
+  ``+ChannelEstimation/ImaginaryInterferenceCancellationAtPilotPosition.m:37-229``.
+  Builds the FBMC precoders ('Auxiliary' and 'Coding').  The construction is
+  tie-sensitive (sorted interference thresholds IIC.m:72-73/:113-114, the 1e-10
+  rounding IIC.m:133, ``hist``/``unique`` clusters IIC.m:140), so it runs once
+  on the host in fp64 and its output is handed to the engine as data
+  (SURVEY.md §7 hard part 4).
+* ``PilotSymbolAidedChannelEstimation`` —
+  ``+ChannelEstimation/PilotSymbolAidedChannelEstimation.m:33-133``.  The
+  reference stubs its 'MMSE' method with ``error('Needs to be implemented')``
+  (PSACE.m:110-111, :128-129); here 'MMSE' is the plug-in slot served by the
+  HIP engine (see ``dsce.engine`` / ``dsce.experiment``).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _col(x):
+    return np.asarray(x).reshape(-1, order="F")
+
+
+def _hadamard(n):
+    H = np.array([[1.0]])
+    while H.shape[0] < n:
+        H = np.block([[H, H], [H, -H]])
+    if H.shape[0] != n:
+        raise ValueError("hadamard: n must be a power of two here")
+    return H
+
+
+class ImaginaryInterferenceCancellationAtPilotPosition:
+    """``(Method, PilotMatrix, FBMCMatrix, NrCanceledInterferersPerPilot, PilotToDataPowerOffset)``."""
+
+    def __init__(self, Method, PilotMatrix, FBMCMatrix, NrCanceled, PilotToDataPowerOffset):
+        PM = np.asarray(PilotMatrix)
+        D = np.asarray(FBMCMatrix)
+        nL, nK = PM.shape
+        pm = _col(PM)
+        numel = pm.size
+
+        # |interference| around the four corners (IIC.m:46-50)
+        I11 = np.abs(D[:, 0].reshape(nL, nK, order="F"))
+        IE1 = np.abs(D[:, nL - 1].reshape(nL, nK, order="F"))
+        I1E = np.abs(D[:, numel - nL].reshape(nL, nK, order="F"))
+        IEE = np.abs(D[:, numel - 1].reshape(nL, nK, order="F"))
+        IM = np.hstack([np.vstack([IEE, I1E[1:, :]]), np.vstack([IE1[:, 1:], I11[1:, 1:]])])
+
+        pil = pm == 1
+        dat = pm == 0
+        aux = pm == -1
+        NP = int(pil.sum())
+
+        sorted_vals = np.sort(_col(IM))[::-1]
+        thr = sorted_vals[NrCanceled] if NrCanceled > 0 else None
+
+        def considered(mask_temp):
+            # sum over pilots of -(pilot number) * membership (IIC.m:74-76 / :121-123)
+            ci = np.zeros(numel)
+            for p in range(NP):
+                ci -= (p + 1) * mask_temp[p, :]
+            ci[pil] = np.arange(1, NP + 1)
+            return ci
+
+        if Method == "Auxiliary":
+            ND = int(dat.sum())
+            NA = int(aux.sum())
+            PI = np.linalg.pinv(D[np.ix_(pil, aux)])
+            AuxP = PI @ (np.eye(NP) - D[np.ix_(pil, pil)])
+            AuxD = -PI @ D[np.ix_(pil, dat)]
+            A = np.zeros((numel, numel - NA), dtype=complex)
+            A[np.ix_(aux, np.arange(NP))] = AuxP
+            A[np.ix_(aux, np.arange(NP, numel - NA))] = AuxD
+            A[np.ix_(pil, np.arange(NP))] = np.eye(NP) * np.sqrt(PilotToDataPowerOffset)
+            A[np.ix_(dat, np.arange(NP, numel - NA))] = np.eye(ND)
+            if NrCanceled > 0:
+                ct = np.abs(D[pil, :]) >= thr
+                ci = considered(ct)
+                idx_p = ci[pil]
+                idx_d = ci[dat]
+                zero_cols = np.concatenate([idx_p, idx_d]) == 0
+                A[np.ix_(aux, zero_cols)] = 0
+            else:
+                ci = "All"
+            DPR = numel / np.sum(np.abs(A) ** 2)
+            A = A * np.sqrt(DPR)
+            Dt = D[pil, :] @ A
+            sir = np.empty(NP)
+            for i in range(NP):
+                s = np.abs(Dt[i, i]) ** 2
+                sir[i] = 10 * np.log10(s / (np.sum(np.abs(Dt[i, :]) ** 2) - s))
+            power = np.real(np.diag(A @ A.conj().T))
+            self.AuxiliaryToDataPowerOffset = np.mean(power[aux]) / np.mean(power[dat])
+            P = A
+            self.PostCodingChannelMatrix = np.nan
+            self.NrAuxiliarySymbols = NA
+        elif Method == "Coding":
+            ND = numel - 2 * NP
+            self.NrAuxiliarySymbols = 0
+            self.AuxiliaryToDataPowerOffset = 0
+            ct = np.abs(D[pil, :]) >= thr
+            if np.any(ct.sum(axis=0) > 1):
+                raise ValueError("Coding symbols must not overlap: The pilot-spacing is too small!")
+            ci = considered(ct)
+            n_unc = int(np.sum(ci == 0))
+            C = np.zeros((numel, numel - NP), dtype=complex)
+            C[np.ix_(pil, np.arange(NP))] = np.eye(NP) * np.sqrt(PilotToDataPowerOffset)
+            C[np.ix_(ci == 0, NP + np.arange(n_unc))] = np.eye(n_unc)
+            col_outer = NP + n_unc
+            pil_pos = np.flatnonzero(pil)
+            for ip in range(1, NP + 1):
+                row = int(np.flatnonzero(ci == ip)[0])
+                cols = np.flatnonzero(ci == -ip)
+                interf = np.round(np.imag(D[row, cols]) * 1e10) / 1e10
+                n = interf.size
+                order = np.argsort(-np.abs(interf), kind="stable")       # sort 'descend', stable
+                abs_sorted = np.abs(interf)[order]
+                isorted = interf[order]
+                uniq = np.unique(abs_sorted)
+                counts = np.array([np.sum(abs_sorted == u) for u in uniq])
+                COP = np.zeros((n, n - 1))
+                colidx = 0
+                for iu, u in enumerate(uniq):
+                    nel = counts[iu]
+                    sel = abs_sorted == u
+                    it = isorted[sel]
+                    if (np.log2(nel) % 1) == 0:
+                        Ct = _hadamard(nel) / it[:, None]
+                        Ct = Ct[:, 1:]
+                        COP[np.ix_(sel, colidx + np.arange(Ct.shape[1]))] = Ct
+                        colidx += Ct.shape[1]
+                    elif nel > 1:
+                        e = np.eye(nel, nel - 1)
+                        Ct = e / it[:, None] - np.roll(e, 1, axis=0) / it[:, None]
+                        COP[np.ix_(sel, colidx + np.arange(Ct.shape[1]))] = Ct
+                        colidx += Ct.shape[1]
+                clusters = [(np.abs(isorted) == u) for u in uniq]
+                clusters = [c.astype(np.int64) for c in clusters]
+                for _ in range(len(uniq) - 1):
+                    sums = [int(c.sum()) for c in clusters]
+                    i1 = int(np.argmin(sums))
+                    c1 = clusters.pop(i1)
+                    sums = [int(c.sum()) for c in clusters]
+                    i2 = int(np.argmin(sums))
+                    c2 = clusters.pop(i2)
+                    comb = [int(np.flatnonzero(c1)[0]), int(np.flatnonzero(c2)[0])]
+                    clusters.append(c1 + c2)
+                    colidx += 1
+                    COP[comb, colidx - 1] = np.array([1.0, -1.0]) / isorted[comb]
+                # classical Gram-Schmidt (IIC.m:184-191)
+                CG = np.zeros((n, n - 1))
+                CG[:, 0] = COP[:, 0] / np.sqrt(COP[:, 0] @ COP[:, 0])
+                for ig in range(1, n - 1):
+                    v = COP[:, ig]
+                    proj = v @ CG[:, :ig]
+                    w = v - (CG[:, :ig] * proj[None, :]).sum(axis=1)
+                    CG[:, ig] = w / np.sqrt(w @ w)
+                res = np.zeros_like(CG)
+                res[order, :] = CG
+                C[np.ix_(ci == -ip, col_outer + np.arange(n - 1))] = res
+                col_outer += n - 1
+            DPR = numel / np.sum(np.abs(C) ** 2)
+            C = C * np.sqrt(DPR)
+            Dt = D[pil, :] @ C
+            sir = np.empty(NP)
+            for i in range(NP):
+                s = np.abs(Dt[i, i]) ** 2
+                sir[i] = 10 * np.log10(s / (np.sum(np.abs(Dt[i, :]) ** 2) - s))
+            P = C
+            self.PostCodingChannelMatrix = np.abs(P.conj().T) ** 2
+        else:
+            raise ValueError("Method must be  'Auxiliary' or 'Coding'!")
+
+        self.Method = Method
+        self.PilotMatrix = PM
+        self.PrecodingMatrix = P
+        self.NrDataSymbols = int(ND)
+        self.NrPilotSymbols = NP
+        self.NrTransmittedSymbols = P.shape[0]
+        self.PilotToDataPowerOffset = PilotToDataPowerOffset
+        self.DataPowerReduction = float(DPR)
+        self.SIR_dB = sir
+        self.ConsideredInterferenceMatrix = ci
+
+
+class PilotSymbolAidedChannelEstimation:
+    """``(PilotPattern, Parameters, InterpolationMethod[, Block])`` (PSACE.m:33-112).
+
+    Supported interpolation methods: 'FullAverage', 'MovingBlockAverage',
+    'linear'/'nearest' (MATLAB ``scatteredInterpolant`` semantics with
+    extrapolation restated on the host: CPU-only, config 1 plumbing), and
+    'MMSE' — the slot the reference leaves as ``error('Needs to be
+    implemented')``.  For 'MMSE' the object carries the engine handle
+    (``set_mmse_engine``) and ``ChannelInterpolation`` returns the MMSE
+    estimate of the one-tap channel computed by the HIP engine.
+    """
+
+    def __init__(self, PilotPattern, Params, InterpolationMethod, Block=None):
+        self.PilotPattern = PilotPattern
+        self.InterpolationMethod = InterpolationMethod
+        if PilotPattern == "Rectangular":
+            nL, sf = int(Params[0][0]), Params[0][1]
+            nK, st = int(Params[1][0]), Params[1][1]
+            self.PilotSpacingFrequency, self.PilotSpacingTime = sf, st
+            PM = np.zeros((nL, nK))
+            r0 = int(round(((nL - 1) % sf) / 2))
+            c0 = int(round(round(((nK - 1) % st) / 2)))
+            PM[r0:nL:int(sf), c0:nK:int(st)] = 1
+        elif PilotPattern == "Diamond":
+            nL, sf = int(Params[0][0]), Params[0][1]
+            nK, st = int(Params[1][0]), Params[1][1]
+            self.PilotSpacingFrequency, self.PilotSpacingTime = sf, st
+
+            def rng(a, step, stop):
+                return np.arange(a, stop + 1e-9, step)
+            fvals = np.concatenate([rng(1, 2 * sf, nL), rng(1 + sf / 2, 2 * sf, nL),
+                                    rng(1 + sf, 2 * sf, nL), rng(1 + 3 * sf / 2, 2 * sf, nL)])
+            fshift = int(np.floor((nL - np.max(fvals)) / 2)) + 1
+            tvals = np.concatenate([rng(1, 2 * st, nK), rng(1 + st, 2 * st, nK)])
+            tshift = int(np.floor((nK - np.max(tvals)) / 2)) + 1
+            PM = np.zeros((nL, nK))
+
+            def mset(f0, t0):
+                f = np.arange(f0, nL + 1, 2 * sf).astype(int) - 1
+                t = np.arange(t0, nK + 1, 2 * st).astype(int) - 1
+                PM[np.ix_(f, t)] = 1
+            mset(fshift, tshift)
+            mset(fshift + int(round(sf / 2)), int(round(tshift + st)))
+            mset(fshift + int(round(sf)), tshift)
+            mset(fshift + int(round(3 * sf / 2)), int(round(tshift + st)))
+        elif PilotPattern == "Custom":
+            self.PilotSpacingFrequency = np.nan
+            self.PilotSpacingTime = np.nan
+            PM = np.asarray(Params, dtype=float)
+        else:
+            raise ValueError("Pilot pattern is not supported! Chose Rectangular Diamond or Custom")
+        self.PilotMatrix = PM
+        self.NrPilotSymbols = int(PM.sum())
+        self._mmse = None
+        if InterpolationMethod == "MovingBlockAverage":
+            self._init_moving_block(Block)
+
+    def _init_moving_block(self, Block):
+        PM = self.PilotMatrix
+        nL, nK = PM.shape
+        num = np.zeros(PM.size, dtype=int)
+        pidx = np.flatnonzero(_col(PM))
+        num[pidx] = np.arange(1, pidx.size + 1)
+        num = num.reshape(nL, nK, order="F")
+        bf, bt = int(Block[0]), int(Block[1])
+        Imat = np.zeros((PM.size, self.NrPilotSymbols))
+        for pos in range(PM.size):
+            f, t = pos % nL, pos // nL
+            fs = np.arange(max(0, f - bf), min(nL, f + bf + 1))
+            ts = np.arange(max(0, t - bt), min(nK, t + bt + 1))
+            sub = num[np.ix_(fs, ts)]
+            # column-major order of logical(Impulse) & logical(PilotMatrix)
+            sel = _col(sub)
+            sel = sel[sel > 0]
+            if sel.size:
+                Imat[pos, sel - 1] = 1.0 / sel.size
+        self.InterpolationMatrix = Imat
+
+    def set_mmse_engine(self, fn):
+        """Attach the engine callback used by the 'MMSE' method (plug-in slot)."""
+        self._mmse = fn
+
+    def ChannelInterpolation(self, LS):
+        LS = _col(LS)
+        m = self.InterpolationMethod
+        if m == "FullAverage":
+            return np.ones(self.PilotMatrix.shape) * np.mean(LS)
+        if m == "MovingBlockAverage":
+            return (self.InterpolationMatrix @ LS).reshape(self.PilotMatrix.shape, order="F")
+        if m in ("linear", "nearest", "natural"):
+            # scatteredInterpolant with extrapolation is config-1 CPU plumbing
+            # (SURVEY.md §8f row f4); not part of the doubly-selective hot path.
+            raise NotImplementedError("scatteredInterpolant interpolation is not provided (SURVEY §8f f4)")
+        if m == "MMSE":
+            if self._mmse is None:
+                raise RuntimeError("MMSE interpolation needs an engine: call set_mmse_engine()")
+            return self._mmse(LS)
+        raise ValueError("Interpolation method not implemented")
+
+    def GetAuxiliaryMatrix(self, NrAuxiliarySymbols):
+        """PSACE.m:137-169."""
+        A = self.PilotMatrix.copy()
+        il, ik = np.nonzero(self.PilotMatrix.T)
+        il, ik = ik, il  # back to (row, col) in column-major order
+        for l, k in zip(il, ik):
+            if NrAuxiliarySymbols >= 1:
+                A[l, k + 1] = -1
+            if NrAuxiliarySymbols >= 2:
+                A[l, k - 1] = -1
+            if NrAuxiliarySymbols >= 3:
+                A[l + 1, k] = -1
+            if NrAuxiliarySymbols >= 4:
+                A[l - 1, k] = -1
+            if NrAuxiliarySymbols > 4 or NrAuxiliarySymbols < 1:
+                raise ValueError("Only 1,2,3,4 auxiliary symbols per pilot are supported")
+        return A

@@ -1,0 +1,164 @@
+/*
+ * dsce.h — C-ABI of the MI355X doubly-selective channel-estimation engine
+ * (libdsce.so).  Plain C types only: pointers + sizes, no torch/HIP types.
+ *
+ * Reference: rnissel/Channel-Estimation (MATLAB).  The reference has no native
+ * layer; these entry points are what a MEX gateway behind the reference's
+ * class surfaces binds (see INTEGRATION.md for the gateway and ctypes stubs):
+ *
+ *   dsce_set_channel      <- Channel.FastFading(...) ctor        FastFading.m:25-192
+ *   dsce_channel_realise  <- FastFading.NewRealization +
+ *                            .ImpulseResponse / GetConvolutionMatrix
+ *                                                               FastFading.m:194-250, :276-295
+ *   dsce_add_scheme       <- the operator set of the script     DoublySelectiveChannelEstimation.m:191-205
+ *                            (G_*, Q_*, precoders of
+ *                             ImaginaryInterferenceCancellationAtPilotPosition.m:37-229,
+ *                             PilotMapping_OFDM script:134-142)
+ *   dsce_set_snr          <- M_SNR_dB / Pn_time / NrIterations   script:18, :33, :243, :398
+ *   dsce_build_mmse       <- correlation matrices + MMSE W      script:208-313 (+ FastFading.m:321-407);
+ *                            the 'MMSE' slot of PilotSymbolAidedChannelEstimation
+ *                            (stubbed with error() at PSACE.m:110-111)
+ *   dsce_run              <- the Monte-Carlo loop body          script:350-564
+ *                            ('MMSE' ChannelInterpolation, PSACE.m:128-129, per stage)
+ *   dsce_get_correlation / dsce_get_W <- R_hP*, W_MMSE_*          script:210-313 (parity probes)
+ *
+ * Conventions
+ *  - Return 0 on success, a negative DSCE_E* code on failure; the message is
+ *    available from dsce_last_error(ctx).  No C++ exception crosses the ABI.
+ *  - Complex numbers are interleaved (re, im) doubles; matrices are
+ *    column-major like MATLAB (R2018a+ interleaved complex storage).
+ *  - Indices are 0-based (a MEX gateway subtracts 1).
+ *  - Host buffers are caller-owned and only read/written during the call;
+ *    device memory and the HIP stream are owned by the context.
+ *  - One context per thread per GPU; no global mutable state besides the HIP
+ *    runtime.  A context binds to one HIP device at dsce_create.
+ *
+ * Random streams (shared with the CPU oracle, oracle/philox.py).
+ *  Philox4x32-10 (Salmon et al. 2011), key = (seed & 0xffffffff, seed >> 32),
+ *  counter = (idx, rep & 0xffffffff, rep >> 32, stream << 16 | sub).
+ *  u53(a,b) = ((a>>5)*2^26 + (b>>6)) * 2^-53.
+ *    THETA  (1, 0)   Doppler angles, element e = tap + Ntap*path (MATLAB
+ *                    rand([Ntap 1 Paths]) column-major, FastFading.m:227):
+ *                    counter e/2, words (0,1) for even e, (2,3) for odd e.
+ *    PHI    (2, 0)   random phases, same layout (FastFading.m:233).
+ *    BITS   (3, s)   data bits of scheme slot s (script:355-357): bit i is bit
+ *                    (i & 31) of word ((i>>5) & 3) of counter i>>7.
+ *    PILOTS (4, s)   pilot symbol indices (script:365-367): pilot j is word
+ *                    (j & 3) of counter j>>2, masked to log2(M) bits.
+ *    NOISE  (5, k)   AWGN of SNR index k, shared by all schemes (script:399):
+ *                    sample e: u1=u53(w0,w1), u2=u53(w2,w3);
+ *                    re = sqrt(-2 log(1-u1)) cos(2 pi u2), im = ... sin(2 pi u2).
+ *
+ * Error counters (dsce_run): int64 array of shape
+ *   [n_schemes][2 csi: 0 = MMSE estimate, 1 = perfect CSI][2 edge: 0 = all bits,
+ *    1 = no-edge bits][n_snr][1 + n_iter stages: 0 = one-tap, i = IC iteration i]
+ * (C order, last index fastest).  BER = count / bits, bits from dsce_bits_per_rep.
+ */
+#ifndef DSCE_H
+#define DSCE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSCE_ABI_VERSION 1
+
+#define DSCE_OK 0
+#define DSCE_EINVAL -1      /* bad argument / shape */
+#define DSCE_EHIP -2        /* HIP runtime error */
+#define DSCE_ESTATE -3      /* call order (e.g. run before build_mmse) */
+#define DSCE_ENOMEM -4
+
+typedef struct dsce_ctx dsce_ctx;
+
+typedef struct {
+    int32_t n_samples;          /* N                                          */
+    int32_t n_taps;             /* length of the sampled PDP (incl. zero taps) */
+    double sampling_rate;       /* Hz                                         */
+    double max_doppler;         /* Hz (FastFading.m:42)                        */
+    int32_t n_paths;            /* sum-of-sinusoids paths (FastFading.m:179)   */
+    int32_t doppler_model;      /* 0 = 'Jakes', 1 = 'Uniform'                  */
+    const double* pdp_norm;     /* n_taps, PowerDelayProfileNormalized (:129) */
+} dsce_channel_desc;
+
+typedef struct {
+    int32_t n_subcarriers;      /* L                                          */
+    int32_t n_symbols;          /* K; LK = L*K columns of G and Q              */
+    int32_t n_tx_symbols;       /* columns of P: NP + ND                       */
+    int32_t n_pilots;           /* NP                                          */
+    int32_t n_data;             /* ND                                          */
+    int32_t mod_order;          /* M (power of two)                            */
+    int32_t bits_per_symbol;    /* log2(M)                                     */
+    int32_t despread;           /* 1: x_hat = P^H (y./h), data = entries NP..  (script:436) */
+    int32_t real_detect;        /* 1: real() before detection (FBMC-OQAM)      */
+    int32_t bits_slot;          /* RNG sub-stream for the data bits            */
+    int32_t pilot_slot;         /* RNG sub-stream for the pilots               */
+    double kappa;               /* pilot scaling, script:140-142               */
+    double data_div;            /* divisor before detection, script:430/437/444 */
+    const double* G;            /* N x LK complex, s = G x                     */
+    const double* Q;            /* N x LK complex, y = Q^H r                   */
+    const double* P;            /* LK x n_tx_symbols complex, x = P [xP; xD]   */
+    const int32_t* pilot_pos;   /* n_pilots positions in 0..LK-1               */
+    const int32_t* data_pos;    /* n_data positions (select mode)              */
+    const uint8_t* considered;  /* n_data no-edge flags (script:151-172)       */
+    const double* symbols;      /* M complex, SymbolMapping sorted by bit label */
+} dsce_scheme_desc;
+
+int dsce_abi_version(void);
+int dsce_device_count(int* count);
+
+int dsce_create(int hip_device, dsce_ctx** out);
+void dsce_destroy(dsce_ctx* ctx);
+const char* dsce_last_error(const dsce_ctx* ctx);
+
+int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* desc);
+int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter);
+int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* desc, int32_t* scheme_id);
+
+/* Builds R_hP, R_hP,est, R_hP,est(no interference), R_Dij,hP and the two MMSE
+ * estimators W / W0 for every SNR on the GPU, zeroing |.| < zero_threshold
+ * like script:263-264, :287-289, :306-308. */
+int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold);
+
+/* Repetitions per device batch (default 8192); larger batches fill the GPU
+ * better at the cost of HBM for per-unit state. */
+int dsce_set_batch(dsce_ctx* ctx, int32_t reps_per_batch);
+
+/* Runs realisations [first_rep, first_rep + n_rep) for every scheme and SNR and
+ * ADDS the bit-error counts into err_counts (layout above).  Synchronous. */
+int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts);
+
+/* Bits per realisation of a scheme: [0] all data bits, [1] no-edge bits. */
+int dsce_bits_per_rep(dsce_ctx* ctx, int32_t scheme_id, int64_t* bits2);
+
+/* ---- parity probes (same kernels as dsce_run) ---------------------------- */
+/* ImpulseResponse of realisation `rep`: N x n_taps complex, column-major. */
+int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_out);
+/* R_hP (NP x NP), R_est / R_noI (n_snr x NP x NP, each NP x NP column-major). */
+int dsce_get_correlation(dsce_ctx* ctx, int32_t scheme_id, double* r_hp, double* r_est, double* r_noi);
+/* W (variant 0) or W0 (variant 1) of SNR index k in the reference layout:
+ * vector of LK*LK*NP complex, index r + LK*c + LK*LK*p (script:283). */
+int dsce_get_W(dsce_ctx* ctx, int32_t scheme_id, int32_t snr_index, int32_t variant, double* w_out);
+/* Per-unit trace of one (rep, snr): y (LK), then for stages 0..n_iter the LS
+ * pilot estimates (NP each) and the MMSE one-tap channel diag(D_hat) (LK each),
+ * and the perfect-CSI diag(D) (LK).  Buffers complex, sized by the caller. */
+int dsce_trace_unit(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t rep, int32_t snr_index,
+                    double* y, double* hp_stages, double* hest_stages, double* h_perfect);
+
+/* ---- measurement -------------------------------------------------------- */
+/* When enabled, dsce_run records HIP events around every launch of each kernel
+ * on the context's stream; dsce_kernel_time returns (launches, total ms). */
+int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
+int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
+/* Algorithmic work of one realisation of a scheme (support-aware): complex
+ * multiply-accumulates of the MMSE contraction and the number of W bytes
+ * streamed per contraction launch. */
+int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per_rep, double* w_bytes_per_snr);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DSCE_H */

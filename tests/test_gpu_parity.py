@@ -1,0 +1,87 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle on the
+same Philox streams.  Floating-point quantities: |gpu - oracle| within the
+stated fp64 tolerances; bit-error counts: identical, up to the number of
+decisions the oracle flags as borderline (distance margin < 1e-9)."""
+import numpy as np
+import pytest
+
+import harness  # noqa: F401  (sys.path)
+from dsce.configs import build_setup
+from oracle import refsim
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0002
+
+
+@pytest.fixture(scope="module")
+def ofdm():
+    from dsce.engine import build_engine
+    S = build_setup("default", schemes=("ofdm",))
+    eng = build_engine(S, batch=256)
+    mm = harness.oracle_mmse(S, S.schemes["ofdm"])
+    yield S, eng, mm
+    eng.close()
+
+
+def test_jakes_ir_matches_oracle(ofdm):
+    S, eng, _ = ofdm
+    ch = S.channel
+    for rep in (0, 1, 77, 1 << 33):
+        ir_g = eng.channel_impulse_response(SEED, rep)
+        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
+                               ch.MaximumDopplerShift, ch.Paths)
+        assert ir_g.shape == ir_o.shape
+        np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
+
+
+def test_correlation_matrices_match_oracle(ofdm):
+    S, eng, mm = ofdm
+    rhp, rest, rnoi = eng.correlation(0)
+    scale = np.abs(mm["R_hP"]).max()
+    np.testing.assert_allclose(rhp, mm["R_hP"], rtol=0, atol=1e-12 * scale)
+    np.testing.assert_allclose(rest, mm["R_est"], rtol=0, atol=1e-12 * scale)
+    np.testing.assert_allclose(rnoi, mm["R_noI"], rtol=0, atol=1e-12 * scale)
+
+
+def test_mmse_estimator_matches_oracle(ofdm):
+    """W = R_Dij pinv(R): the tolerance is fp64 rounding amplified by the
+    condition number of R (pinv/inverse of an ill-conditioned pilot
+    correlation at high SNR), tol = 1e-14 * cond(R) * max|W|."""
+    S, eng, mm = ofdm
+    for k in range(len(S.pn_time)):
+        for var, key, R in ((0, "W", mm["R_est"][k]), (1, "W0", mm["R_noI"][k])):
+            wg = eng.W(0, k, var)
+            wo = mm[key][:, k]
+            scale = np.abs(wo).max()
+            tol = max(1e-14 * np.linalg.cond(R), 1e-12) * scale
+            diff = np.abs(wg - wo)
+            # entries within tol of the 1e-8 zero threshold may legitimately flip to 0
+            border = np.abs(np.abs(wo) - 1e-8) <= tol
+            assert np.all((diff <= tol) | border), (k, var, diff.max() / scale, np.linalg.cond(R))
+
+
+def test_unit_trace_matches_oracle(ofdm):
+    S, eng, mm = ofdm
+    sc = S.schemes["ofdm"]
+    tr = {}
+    rep, k = 5, 3
+    refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
+                    trace=tr)
+    g = eng.trace_unit(0, SEED, rep, k)
+    np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(g["hp"][0], tr["hP0"][k], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(g["hest"][0], tr["hest0"][k], rtol=0, atol=1e-10)
+
+
+def test_error_counts_match_oracle(ofdm):
+    S, eng, mm = ofdm
+    sc = S.schemes["ofdm"]
+    n = 64
+    cg = eng.run(SEED, 0, n)
+    res = refsim.simulate(SEED, 0, n, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm])
+    co = res["err"]
+    diff = np.abs(cg - co).sum()
+    assert diff <= 8 * res["borderline"].sum(), (cg - co)
+    b = eng.bits_per_rep(0)
+    assert b[0] == sc.n_bits and b[1] == sc.considered_symbols.sum() * sc.bits_per_symbol
