@@ -509,6 +509,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.u = dalloc<double2>(c, LK * U, L);
     b.t = dalloc<double2>(c, N * U, L);
     b.e = dalloc<double2>(c, LK * U, L);
+    b.e2 = dalloc<double2>(c, LK * U, L);
     b.qe = dalloc<uint16_t>(c, ND * U, L);
     b.qp = dalloc<uint16_t>(c, ND * U, L);
 }

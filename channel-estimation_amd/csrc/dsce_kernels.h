@@ -27,7 +27,8 @@ struct McBuffers {
     double2* v;       // [LK][U]   P [xP; Q(x_est)]
     double2* u;       // [LK][U]   P [xP; Q(x_perfect)]
     double2* t;       // [N][U]    scratch: r / G u
-    double2* e;       // [LK][U]   scratch: y ./ h (despreading)
+    double2* e;       // [LK][U]   y_est ./ h_hat (one-tap quotient, MMSE)
+    double2* e2;      // [LK][U]   y_perf ./ h     (one-tap quotient, perfect CSI)
     uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
 };

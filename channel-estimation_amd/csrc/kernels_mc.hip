@@ -32,47 +32,80 @@ __device__ __forceinline__ int wave_sum(int v) {
 
 // ---------------------------------------------------------------------------
 // a2: Jakes / Uniform sum-of-sinusoids impulse response, FastFading.m:222-238.
-// grid (ceil(N/256), R, ntap), block 256: the 2 x Paths random parameters of
-// one (realisation, tap) are drawn once into LDS, every lane owns one sample n.
-// Output IR[tap][n][rep] (only non-zero-power taps).
+// IR[n, tap] = sqrt(PDPn) / sqrt(Paths) * sum_p exp(j 2 pi (phi_p + fD_p n dt)).
+// Block 256 = 4 waves = 4 realisations of one tap; each wave draws its
+// realisation's 2 x Paths random numbers (Philox, THETA/PHI streams) into LDS
+// together with the per-path rotation w_p = exp(j 2 pi fD_p dt).  A lane owns
+// JCH consecutive samples: one exact sincos per path at the chunk start, then
+// JCH-1 complex rotations (|error| ~ JCH * 1e-16, far inside the 1e-12
+// parity tolerance).  grid (ceil(nchunk/64), R/4, ntap).
+// Output IR[tap][n][rep] (only the non-zero-power taps).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+static constexpr int JCH_MAX = 16;
+__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R, int jch,
                                                double2* __restrict__ ir) {
     extern __shared__ double sm[];
-    double* ds = sm;
-    double* ph = sm + ch.paths;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int P = ch.paths;
+    double* ds = sm + (size_t)wv * 4 * P;
+    double* ph = ds + P;
+    double* wr = ph + P;
+    double* wi = wr + P;
     const int tap = blockIdx.z;
-    const int rl = blockIdx.y;
+    const int rl = blockIdx.y * 4 + wv;
     const uint64_t rep = rep0 + (uint64_t)rl;
-    for (int p = threadIdx.x; p < ch.paths; p += blockDim.x) {
+    for (int p = lane; p < P; p += WAVE) {
         const uint32_t e = (uint32_t)(tap + ch.ntap * p);       // rand([Ntap 1 Paths]) column-major
         const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, e >> 1);
         const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, e >> 1);
         const double th = (e & 1) ? u53(wt.z, wt.w) : u53(wt.x, wt.y);
         const double phi = (e & 1) ? u53(wp.z, wp.w) : u53(wp.x, wp.y);
-        ds[p] = (ch.model == 0) ? cos((th * 2.0) * M_PI) * ch.fD : (2.0 * (th - 0.5)) * ch.fD;
+        const double d = (ch.model == 0) ? cos((th * 2.0) * M_PI) * ch.fD : (2.0 * (th - 0.5)) * ch.fD;
+        double sn, cs;
+        sincos(TWO_PI * (d * ch.dt), &sn, &cs);
+        ds[p] = d;
         ph[p] = phi;
+        wr[p] = cs;
+        wi[p] = sn;
     }
     __syncthreads();
-    const int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= ch.N) return;
-    const double t = (double)n * ch.dt;
-    double sr = 0.0, si = 0.0;
-    for (int p = 0; p < ch.paths; ++p) {
-        const double x = ph[p] + ds[p] * t;                        // no contraction (-ffp-contract=off)
-        double s, c;
-        sincos(TWO_PI * x, &s, &c);
-        sr += c;
-        si += s;
+    const int n0 = (blockIdx.x * WAVE + lane) * jch;
+    if (n0 >= ch.N) return;
+    const double t0 = (double)n0 * ch.dt;
+    double2 acc[JCH_MAX];
+#pragma unroll
+    for (int i = 0; i < JCH_MAX; ++i) acc[i] = make_double2(0.0, 0.0);
+    for (int p = 0; p < P; ++p) {
+        double sn, cs;
+        sincos(TWO_PI * (ph[p] + ds[p] * t0), &sn, &cs);
+        double2 z = make_double2(cs, sn);
+        const double2 w = make_double2(wr[p], wi[p]);
+#pragma unroll
+        for (int i = 0; i < JCH_MAX; ++i) {
+            if (i < jch) {
+                acc[i].x += z.x;
+                acc[i].y += z.y;
+                z = c_mul(z, w);
+            }
+        }
     }
-    const double sp = sqrt((double)ch.paths);
+    const double sp = sqrt((double)P);
     const double g = ch.sqrt_pdp[tap];
-    ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (sr / sp), g * (si / sp));
+#pragma unroll
+    for (int i = 0; i < JCH_MAX; ++i) {
+        const int n = n0 + i;
+        if (i < jch && n < ch.N)
+            ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
+    }
 }
 
 void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
-    dim3 grid((ch.N + 255) / 256, R, ch.ntap);
-    hipLaunchKernelGGL(k_jakes, grid, dim3(256), 2 * ch.paths * sizeof(double), s, ch, seed, rep0, R, ir);
+    int jch = (ch.N + WAVE - 1) / WAVE;
+    if (jch > JCH_MAX) jch = JCH_MAX;
+    const int nchunk = (ch.N + jch - 1) / jch;
+    dim3 grid((nchunk + WAVE - 1) / WAVE, R / 4, ch.ntap);
+    hipLaunchKernelGGL(k_jakes, grid, dim3(256), (size_t)4 * 4 * ch.paths * sizeof(double), s, ch, seed, rep0, R, jch,
+                       ir);
 }
 
 // ---------------------------------------------------------------------------
@@ -365,64 +398,69 @@ struct StageArgs {
     const double2* ysrc_p;     // y (stage 0) or y_perf
 };
 
-__global__ void __launch_bounds__(64) k_stage(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
-                                              const double2* __restrict__ xp, const uint16_t* __restrict__ sidx,
-                                              const double2* __restrict__ h, double2* __restrict__ hp,
-                                              double2* __restrict__ hest, double2* __restrict__ e,
-                                              uint16_t* __restrict__ qe, uint16_t* __restrict__ qp,
-                                              double2* __restrict__ v, double2* __restrict__ u,
-                                              unsigned long long* __restrict__ counters) {
-    extern __shared__ double2 smem[];
-    double2* sym = smem;                     // [M]
-    double2* shp = smem + sk.M;              // [NP][64]
-    for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
+// (1) LS pilot estimates, h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p and the
+// one-tap quotients y./h_hat (MMSE) and y./h (perfect CSI) for a block of 24
+// rows; grid (U/64, ceil(LK/24)).
+__global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
+                                                const double2* __restrict__ xp, const double2* __restrict__ h,
+                                                double2* __restrict__ hp, double2* __restrict__ hest,
+                                                double2* __restrict__ e_est, double2* __restrict__ e_perf) {
+    extern __shared__ double2 shp[];                     // [NP][64], each lane its own column
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int snr = (blockIdx.x * WAVE) / st.R;
     const int rl = unit % st.R;
     const int U = st.U, R = st.R;
     const double sqk = 1.0 / sk.inv_sqrt_kappa;
-    // LS estimates at the pilot positions
     for (int p = 0; p < sk.NP; ++p) {
         const double2 yv = st.ysrc_e[(size_t)sk.pilot_pos[p] * U + unit];
         const double2 q = c_div(yv, xp[(size_t)p * R + rl]);
         const double2 hv = make_double2(q.x / sqk, q.y / sqk);
         shp[p * WAVE + threadIdx.x] = hv;
-        hp[(size_t)p * U + unit] = hv;
+        if (blockIdx.y == 0) hp[(size_t)p * U + unit] = hv;
     }
-    __syncthreads();
-    // h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p
     const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP;
-    for (int c = 0; c < sk.LK; ++c) {
+    const int r0 = blockIdx.y * DSCE_RB;
+    const int r1 = min(sk.LK, r0 + DSCE_RB);
+    for (int c = r0; c < r1; ++c) {
         double2 acc = make_double2(0.0, 0.0);
         for (int p = 0; p < sk.NP; ++p) c_fma(acc, wd[(size_t)c * sk.NP + p], shp[p * WAVE + threadIdx.x]);
-        hest[(size_t)c * U + unit] = acc;
+        const size_t i = (size_t)c * U + unit;
+        hest[i] = acc;
+        e_est[i] = c_div(st.ysrc_e[i], acc);
+        e_perf[i] = c_div(st.ysrc_p[i], h[(size_t)c * R + rl]);
     }
+}
+
+// (2) data-symbol decisions and bit-error counts, grid (U/64, ceil(ND/32)).
+static constexpr int DET_CHUNK = 32;
+__global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const uint16_t* __restrict__ sidx,
+                                               const double2* __restrict__ e_est, const double2* __restrict__ e_perf,
+                                               uint16_t* __restrict__ qe, uint16_t* __restrict__ qp,
+                                               unsigned long long* __restrict__ counters) {
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int snr = (blockIdx.x * WAVE) / st.R;
+    const int rl = unit % st.R;
+    const int U = st.U, R = st.R;
+    const int i0 = blockIdx.y * DET_CHUNK;
+    const int i1 = min(sk.ND, i0 + DET_CHUNK);
     int cnt[4] = {0, 0, 0, 0};
-    // two passes: 0 = MMSE estimate, 1 = perfect CSI
     for (int csi = 0; csi < 2; ++csi) {
-        const double2* __restrict__ ys = csi == 0 ? st.ysrc_e : st.ysrc_p;
+        const double2* __restrict__ e = csi == 0 ? e_est : e_perf;
         uint16_t* __restrict__ qo = csi == 0 ? qe : qp;
-        if (sk.despread) {
-            for (int c = 0; c < sk.LK; ++c) {
-                const double2 hv = csi == 0 ? hest[(size_t)c * U + unit] : h[(size_t)c * R + rl];
-                e[(size_t)c * U + unit] = c_div(ys[(size_t)c * U + unit], hv);
-            }
-        }
-        for (int i = 0; i < sk.ND; ++i) {
+        for (int i = i0; i < i1; ++i) {
             double2 z;
-            if (sk.despread) {
+            if (sk.despread) {                                  // x = P' (y ./ h), script:436 / :520
                 const int row = sk.NP + i;
                 double2 acc = make_double2(0.0, 0.0);
                 for (int j = sk.ph_ptr[row]; j < sk.ph_ptr[row + 1]; ++j)
                     c_fma(acc, sk.ph_val[j], e[(size_t)sk.ph_col[j] * U + unit]);
-                z = sk.real_detect ? make_double2(acc.x / sk.data_div, 0.0)
-                                   : make_double2(acc.x / sk.data_div, acc.y / sk.data_div);
-            } else {
-                const int c = sk.data_pos[i];
-                const double2 hv = csi == 0 ? hest[(size_t)c * U + unit] : h[(size_t)c * R + rl];
-                const double2 q = c_div(ys[(size_t)c * U + unit], hv);
-                z = sk.real_detect ? make_double2(q.x / sk.data_div, 0.0)
-                                   : make_double2(q.x / sk.data_div, q.y / sk.data_div);
+                z = acc;
+                z = sk.real_detect ? make_double2(z.x / sk.data_div, 0.0)
+                                   : make_double2(z.x / sk.data_div, z.y / sk.data_div);
+            } else {                                            // x(data positions) ./ sqrt(DPR)
+                z = e[(size_t)sk.data_pos[i] * U + unit];
+                z = sk.real_detect ? make_double2(z.x / sk.data_div, 0.0)
+                                   : make_double2(z.x / sk.data_div, z.y / sk.data_div);
             }
             const int d = slice(sk, z);
             const int tx = sidx[(size_t)i * R + rl];
@@ -441,10 +479,23 @@ __global__ void __launch_bounds__(64) k_stage(SchemeK sk, StageArgs st, const do
             atomicAdd(&counters[idx], (unsigned long long)tot);
         }
     }
-    if (st.last) return;
+}
+
+// (3) re-precoding of the quantised decisions for the next IC iteration:
+// v = P [xP; Q(x_est)], u = P [xP; Q(x_perf)] (script:482-484, :541-543);
+// grid (U/64, ceil(LK/24)).
+__global__ void __launch_bounds__(64) k_precode(SchemeK sk, StageArgs st, const double2* __restrict__ xp,
+                                                const uint16_t* __restrict__ qe, const uint16_t* __restrict__ qp,
+                                                double2* __restrict__ v, double2* __restrict__ u) {
+    __shared__ double2 sym[256];
+    for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
     __syncthreads();
-    // re-precode the quantised decisions: v = P [xP; Q(x_est)], u = P [xP; Q(x_perf)]
-    for (int r = 0; r < sk.LK; ++r) {
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int rl = unit % st.R;
+    const int U = st.U, R = st.R;
+    const int r0 = blockIdx.y * DSCE_RB;
+    const int r1 = min(sk.LK, r0 + DSCE_RB);
+    for (int r = r0; r < r1; ++r) {
         double2 av = make_double2(0.0, 0.0), au = make_double2(0.0, 0.0);
         for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
             const int k = sk.p_col[j];
@@ -476,9 +527,13 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     st.U = b.U;
     st.ysrc_e = stage == 0 ? b.y : b.yest;
     st.ysrc_p = stage == 0 ? b.y : b.yperf;
-    const size_t lds = (size_t)(sk.M + sk.NP * WAVE) * sizeof(double2);
-    hipLaunchKernelGGL(k_stage, dim3(b.U / WAVE), dim3(WAVE), lds, s, sk, st, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest,
-                       b.e, b.qe, b.qp, b.v, b.u, counters);
+    const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
+    hipLaunchKernelGGL(k_ls_hest, dim3(b.U / WAVE, rblk), dim3(WAVE), (size_t)sk.NP * WAVE * sizeof(double2), s, sk,
+                       st, mm.Wd, b.xp, b.h, b.hp, b.hest, b.e, b.e2);
+    hipLaunchKernelGGL(k_detect, dim3(b.U / WAVE, (sk.ND + DET_CHUNK - 1) / DET_CHUNK), dim3(WAVE), 0, s, sk, st,
+                       b.sidx, b.e, b.e2, b.qe, b.qp, counters);
+    if (!last)
+        hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v, b.u);
 }
 
 }  // namespace dsce
