@@ -31,27 +31,33 @@ static inline double2 cx(const double* p, size_t i) { return make_double2(p[2 * 
 static inline bool nz(double2 v) { return v.x != 0.0 || v.y != 0.0; }
 
 struct HostBand {
+    int rb = DSCE_RB;
     std::vector<int> row0, nrows, klo, khi;
     std::vector<long long> off;
     std::vector<double2> vals;
     long long elems = 0;
 };
 
-// rows [0, nrow) grouped in blocks of DSCE_RB; range(row) -> [lo, hi)
+// rows [0, nrow) grouped in blocks of at most rb rows; range(row) -> [lo, hi).
+// split_disjoint: a block also ends where the next row's range does not overlap
+// the block's union (block-diagonal operators such as the OFDM estimator).
 template <class RangeFn>
-static HostBand band_geometry(int nrow, RangeFn range, int kscale) {
+static HostBand band_geometry(int nrow, RangeFn range, int kscale, int rb = DSCE_RB, bool split_disjoint = false) {
     HostBand b;
+    b.rb = rb;
     long long off = 0;
-    for (int r0 = 0; r0 < nrow; r0 += DSCE_RB) {
-        const int nr = std::min(DSCE_RB, nrow - r0);
-        int lo = 1 << 30, hi = -1;
-        for (int r = r0; r < r0 + nr; ++r) {
+    int r0 = 0;
+    while (r0 < nrow) {
+        int lo = 1 << 30, hi = -1, nr = 0;
+        for (int r = r0; r < nrow && nr < rb; ++r) {
             int a, c;
             range(r, a, c);
+            if (split_disjoint && nr > 0 && c > a && hi >= 0 && (a >= hi || c <= lo)) break;
             if (c > a) {
                 lo = std::min(lo, a);
                 hi = std::max(hi, c);
             }
+            ++nr;
         }
         if (hi < 0) { lo = 0; hi = 0; }
         b.row0.push_back(r0);
@@ -59,7 +65,8 @@ static HostBand band_geometry(int nrow, RangeFn range, int kscale) {
         b.klo.push_back(lo * kscale);
         b.khi.push_back(hi * kscale);
         b.off.push_back(off);
-        off += (long long)(hi - lo) * kscale * DSCE_RB;
+        off += (long long)(hi - lo) * kscale * rb;
+        r0 += nr;
     }
     b.elems = off;
     return b;
@@ -186,6 +193,7 @@ void collect_timing(dsce_ctx* c) {
 Band upload_band(dsce_ctx* c, const HostBand& h, bool with_vals) {
     Band b{};
     b.nblk = (int)h.row0.size();
+    b.rb = h.rb;
     b.row0 = dupload(c, h.row0);
     b.nrows = dupload(c, h.nrows);
     b.klo = dupload(c, h.klo);
@@ -276,7 +284,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
             }
             if (b < 0) { a = 0; b = 0; }
         },
-        NP);
+        NP, DSCE_WRB, true);
     s.w_elems = s.wband.elems;
     s.w_struct = 0;
     for (size_t blk = 0; blk < s.wband.row0.size(); ++blk)
@@ -854,7 +862,7 @@ int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out)
         for (int rl = 0; rl < b.nrows[blk]; ++rl)
             for (int cc = clo; cc < chi; ++cc)
                 for (size_t p = 0; p < NP; ++p) {
-                    const double2 v = packed[b.off[blk] + ((size_t)(cc - clo) * NP + p) * DSCE_RB + rl];
+                    const double2 v = packed[b.off[blk] + ((size_t)(cc - clo) * NP + p) * b.rb + rl];
                     const size_t o = (size_t)(b.row0[blk] + rl) + LK * cc + LK * LK * p;
                     w_out[2 * o] = v.x;
                     w_out[2 * o + 1] = v.y;

@@ -11,7 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define DSCE_RB 24          // rows per band block (MMSE contraction / banded matvec tile)
+#define DSCE_RB 24          // rows per block of the G / Q^H bands (banded matvec tile)
+#define DSCE_WRB 32         // rows per block of the MMSE estimator W (two 16-row MFMA tiles)
 #define DSCE_MAX_NP 64
 #define DSCE_MAX_TAPS 64
 
@@ -82,6 +83,7 @@ __host__ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
 // ---------------------------------------------------------------------------
 struct Band {
     int nblk;
+    int rb;                       // row stride of the packed values (rows per block, padded)
     const int* row0;
     const int* nrows;
     const int* klo;

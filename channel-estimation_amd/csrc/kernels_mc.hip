@@ -15,6 +15,8 @@
 #include "dsce_kernels.h"
 
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 namespace dsce {
 
@@ -313,16 +315,117 @@ void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McB
 }
 
 // ---------------------------------------------------------------------------
-// a13/a15: MMSE contraction  y_est = y - (D_hat - diag h_hat) v with
+// a13/a15: MMSE contraction  y_est = y - (D_hat - diag h_hat) v  with
 // D_hat = sum_p W_p hP_p  (script:417-425, :482-484, :493-511), never forming
-// D_hat.  grid (U/64, nblk), block 64 = one wave of 64 units of one SNR.
-// W values: wave-uniform scalar loads of the packed band layout.
+// D_hat:  acc[r][u] = sum_{c in band(r)} sum_p W[r, (c,p)] * (hP[p][u] v[c][u]).
+// This is a GEMM  [rows x K] * [K x units]  with K = (column, pilot) and the
+// right operand Z = hP (x) v generated on the fly; W is shared by all units of
+// one SNR point.
+//
+// k_wcontract_mfma: v_mfma_f64_16x16x4_f64.  A = W (16 rows x 4 k, one f64 per
+// lane: row = lane&15, k = lane>>4), B = Z (4 k x 16 units: k = lane>>4,
+// unit = lane&15), D: row = (lane>>4) + 4*reg, unit = lane&15
+// (cdna_hip_programming.md §3 f64 layout; probed by tools/mfma_f64_layout.hip).
+// Complex product with 4 real MFMAs: Re += Wr Zr + (-Wi) Zi, Im += Wr Zi + Wi Zr.
+// Wave tile = 32 rows (2 row tiles, one W band block) x 64 units (4 unit
+// tiles) -> 32 MFMAs per 4-deep k step.  Block = 4 waves = 256 units.
+// grid (U/256, nblk).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_wcontract(Band Wb, const double2* __restrict__ Wall, long long w_elems,
-                                                  int var, int nsnr, int NP, int R, int U,
-                                                  const double2* __restrict__ hp, const double2* __restrict__ v,
-                                                  const double2* __restrict__ y, const double2* __restrict__ hest,
-                                                  double2* __restrict__ yest) {
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+// one complex 16x16x4 tile: (re, im) += W (16 rows x 4 k) * Z (4 k x 16 units)
+#define CTILE(RE, IM, W, Z)                 \
+    RE = MFMA64((W).x, (Z).x, RE);          \
+    RE = MFMA64(-(W).y, (Z).y, RE);         \
+    IM = MFMA64((W).x, (Z).y, IM);          \
+    IM = MFMA64((W).y, (Z).x, IM)
+
+// Wave tile: 32 rows x 32 units (2 x 2 complex tiles, 64 accumulator AGPRs ->
+// 2-3 waves per SIMD).  Block = 4 waves = 128 units.  grid (U/128, nblk).
+__global__ void __launch_bounds__(256) k_wcontract_mfma(Band Wb, const double2* __restrict__ Wall, long long w_elems,
+                                                        int var, int nsnr, int NP, int R, int U,
+                                                        const double2* __restrict__ hp,
+                                                        const double2* __restrict__ v,
+                                                        const double2* __restrict__ y,
+                                                        const double2* __restrict__ hest,
+                                                        double2* __restrict__ yest) {
+    extern __shared__ double2 shp[];                     // [4 waves][NP][32]
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int ubase = blockIdx.x * 128 + wv * 32;
+    const int snr = ubase / R;
+    const int blk = blockIdx.y;
+    double2* sh = shp + (size_t)wv * NP * 32;
+    if (l < 32)
+        for (int p = 0; p < NP; ++p) sh[p * 32 + l] = hp[(size_t)p * U + ubase + l];
+    __syncthreads();
+    const int rb = Wb.rb;
+    const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
+    const int c_lo = Wb.klo[blk] / NP, c_hi = Wb.khi[blk] / NP;
+    const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)w_elems + Wb.off[blk];
+    const int kk = l >> 4, j = l & 15;
+    d4 r00 = {0, 0, 0, 0}, i00 = r00, r01 = r00, i01 = r00, r10 = r00, i10 = r00, r11 = r00, i11 = r00;
+    const int nq = NP >> 2;
+    const int nstep = (c_hi - c_lo) * nq;                 // k steps of 4 (column c, pilots 4q..4q+3); even
+    const double2* __restrict__ vb = v + ubase + j;
+    const double2* __restrict__ wb = w + (size_t)kk * rb + j;
+    // step st: column c = c_lo + st / nq, pilots 4 (st % nq) + kk
+#define LOADSTEP(ST, W0, W1, V0, V1)                                              \
+    {                                                                            \
+        const int c_ = (ST) / nq;                                                \
+        const double2* wk_ = wb + ((size_t)c_ * NP + 4 * ((ST) - c_ * nq)) * rb; \
+        W0 = wk_[0];                                                             \
+        W1 = wk_[16];                                                            \
+        const double2* vv_ = vb + (size_t)(c_lo + c_) * U;                       \
+        V0 = vv_[0];                                                             \
+        V1 = vv_[16];                                                            \
+    }
+#define MMASTEP(ST, W0, W1, V0, V1)                                   \
+    {                                                                 \
+        const int p_ = 4 * ((ST) % nq) + kk;                          \
+        const double2 z0 = c_mul(sh[p_ * 32 + j], V0);                \
+        const double2 z1 = c_mul(sh[p_ * 32 + 16 + j], V1);           \
+        CTILE(r00, i00, W0, z0);                                      \
+        CTILE(r01, i01, W0, z1);                                      \
+        CTILE(r10, i10, W1, z0);                                      \
+        CTILE(r11, i11, W1, z1);                                      \
+    }
+    double2 a0, a1, av0, av1, b0, b1, bv0, bv1;
+    if (nstep > 0) LOADSTEP(0, a0, a1, av0, av1);
+    for (int st = 0; st < nstep; st += 2) {
+        LOADSTEP(st + 1, b0, b1, bv0, bv1);
+        MMASTEP(st, a0, a1, av0, av1);
+        const int sn = min(st + 2, nstep - 1);
+        LOADSTEP(sn, a0, a1, av0, av1);
+        MMASTEP(st + 1, b0, b1, bv0, bv1);
+    }
+#undef LOADSTEP
+#undef MMASTEP
+    // D layout: row = 16*it + kk + 4*reg, unit = 16*jt + j
+#define STORE(ACCR, ACCI, IT, JT)                                                       \
+    _Pragma("unroll") for (int reg = 0; reg < 4; ++reg) {                               \
+        const int row = 16 * (IT) + kk + 4 * reg;                                       \
+        if (row < nrows) {                                                              \
+            const size_t i_ = (size_t)(row0 + row) * U + ubase + 16 * (JT) + j;         \
+            double2 o = c_sub(y[i_], make_double2(ACCR[reg], ACCI[reg]));               \
+            o = c_add(o, c_mul(hest[i_], v[i_]));                                       \
+            yest[i_] = o;                                                               \
+        }                                                                               \
+    }
+    STORE(r00, i00, 0, 0)
+    STORE(r01, i01, 0, 1)
+    STORE(r10, i10, 1, 0)
+    STORE(r11, i11, 1, 1)
+#undef STORE
+}
+
+// VALU reference variant (one unit per lane, W rows wave-uniform via scalar
+// loads); kept for in-process A/B (DSCE_WCONTRACT=valu) and NP % 4 != 0.
+__global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* __restrict__ Wall, long long w_elems,
+                                                       int var, int nsnr, int NP, int R, int U,
+                                                       const double2* __restrict__ hp, const double2* __restrict__ v,
+                                                       const double2* __restrict__ y, const double2* __restrict__ hest,
+                                                       double2* __restrict__ yest) {
     extern __shared__ double2 shp[];                     // [NP][64]
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int snr = (blockIdx.x * WAVE) / R;
@@ -332,21 +435,21 @@ __global__ void __launch_bounds__(64) k_wcontract(Band Wb, const double2* __rest
     const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
     const int c_lo = Wb.klo[blk] / NP, c_hi = Wb.khi[blk] / NP;
     const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)w_elems + Wb.off[blk];
-    double2 acc[DSCE_RB];
+    double2 acc[DSCE_WRB];
 #pragma unroll
-    for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
+    for (int r = 0; r < DSCE_WRB; ++r) acc[r] = make_double2(0.0, 0.0);
     for (int c = c_lo; c < c_hi; ++c) {
         const double2 vc = v[(size_t)c * U + unit];
-        const double2* __restrict__ wc = w + (size_t)(c - c_lo) * NP * DSCE_RB;
+        const double2* __restrict__ wc = w + (size_t)(c - c_lo) * NP * DSCE_WRB;
         for (int p = 0; p < NP; ++p) {
             const double2 z = c_mul(shp[p * WAVE + threadIdx.x], vc);
-            const double2* __restrict__ wk = wc + (size_t)p * DSCE_RB;
+            const double2* __restrict__ wk = wc + (size_t)p * DSCE_WRB;
 #pragma unroll
-            for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], wk[r], z);
+            for (int r = 0; r < DSCE_WRB; ++r) c_fma(acc[r], wk[r], z);
         }
     }
 #pragma unroll
-    for (int r = 0; r < DSCE_RB; ++r) {
+    for (int r = 0; r < DSCE_WRB; ++r) {
         if (r < nrows) {
             const size_t i = (size_t)(row0 + r) * U + unit;
             double2 o = c_sub(y[i], acc[r]);
@@ -357,8 +460,18 @@ __global__ void __launch_bounds__(64) k_wcontract(Band Wb, const double2* __rest
 }
 
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
-    hipLaunchKernelGGL(k_wcontract, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2), s, mm.Wb,
-                       mm.W, mm.w_elems, var, mm.nsnr, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+    // DSCE_WCONTRACT = mfma (default) | valu — read per launch for in-process A/B.
+    const char* mode = getenv("DSCE_WCONTRACT");
+    bool valu = (sk.NP % 8) != 0 || mm.Wb.rb != 32 || (b.U % 128) != 0 || (b.R % 32) != 0;
+    if (mode && mode[0] == 'v') valu = true;
+    if (valu) {
+        hipLaunchKernelGGL(k_wcontract_valu, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2),
+                           s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+    } else {
+        hipLaunchKernelGGL(k_wcontract_mfma, dim3(b.U / 128, mm.Wb.nblk), dim3(256),
+                           (size_t)4 * sk.NP * 32 * sizeof(double2), s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, sk.NP,
+                           b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+    }
 }
 
 // ---------------------------------------------------------------------------

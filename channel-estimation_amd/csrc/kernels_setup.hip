@@ -218,10 +218,11 @@ __global__ void k_rdij(SetupArgs a, Band Wb, const double2* __restrict__ m, cons
     const int blk = blockIdx.x, i = blockIdx.y;
     const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
     const int c_lo = Wb.klo[blk] / a.NP, c_hi = Wb.khi[blk] / a.NP;
-    const int nslot = (c_hi - c_lo) * DSCE_RB;
+    const int rb = Wb.rb;
+    const int nslot = (c_hi - c_lo) * rb;
     double2* __restrict__ out = rd + Wb.off[blk];
     for (int t = threadIdx.x; t < nslot; t += blockDim.x) {
-        const int c = c_lo + t / DSCE_RB, rl = t % DSCE_RB;
+        const int c = c_lo + t / rb, rl = t % rb;
         double2 acc = make_double2(0.0, 0.0);
         if (rl < nrows) {
             const int r = row0 + rl;
@@ -241,7 +242,7 @@ __global__ void k_rdij(SetupArgs a, Band Wb, const double2* __restrict__ m, cons
             }
             if (hypot(acc.x, acc.y) < a.thr) acc = make_double2(0.0, 0.0);
         }
-        out[((size_t)(c - c_lo) * a.NP + i) * DSCE_RB + rl] = acc;
+        out[((size_t)(c - c_lo) * a.NP + i) * rb + rl] = acc;
     }
 }
 
@@ -257,19 +258,20 @@ __global__ void k_w(SetupArgs a, Band Wb, const double2* __restrict__ rd, const 
     const int blk = blockIdx.x;
     const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
     const int c_lo = Wb.klo[blk] / a.NP, c_hi = Wb.khi[blk] / a.NP;
-    const int nslot = (c_hi - c_lo) * DSCE_RB;
+    const int rb = Wb.rb;
+    const int nslot = (c_hi - c_lo) * rb;
     const double2* __restrict__ in = rd + Wb.off[blk];
     double2* __restrict__ out = w + Wb.off[blk];
     for (int t = threadIdx.x; t < nslot; t += blockDim.x) {
-        const int cl = t / DSCE_RB, rl = t % DSCE_RB;
+        const int cl = t / rb, rl = t % rb;
         const int c = c_lo + cl;
         for (int pp = 0; pp < a.NP; ++pp) {
             double2 acc = make_double2(0.0, 0.0);
             if (rl < nrows)
                 for (int p = 0; p < a.NP; ++p)
-                    c_fma(acc, in[((size_t)cl * a.NP + p) * DSCE_RB + rl], rinv[(size_t)pp * a.NP + p]);
+                    c_fma(acc, in[((size_t)cl * a.NP + p) * rb + rl], rinv[(size_t)pp * a.NP + p]);
             if (hypot(acc.x, acc.y) < a.thr) acc = make_double2(0.0, 0.0);
-            out[((size_t)cl * a.NP + pp) * DSCE_RB + rl] = acc;
+            out[((size_t)cl * a.NP + pp) * rb + rl] = acc;
             if (rl < nrows && row0 + rl == c) wd[(size_t)c * a.NP + pp] = acc;
         }
     }

@@ -266,6 +266,8 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                     trace.setdefault("y", []).append(y)
                     trace.setdefault("hP0", []).append(hP)
                     trace.setdefault("hest0", []).append(hest)
+                    trace.setdefault("hp_stages", []).append([hP])
+                    trace.setdefault("hest_stages", []).append([hest])
                 Dt = Dest
                 ht = hest
                 for it in range(1, n_iter + 1):
@@ -290,6 +292,8 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                     if trace is not None:
                         trace.setdefault("yic", []).append(yic)
                         trace.setdefault("ypc", []).append(ypc)
+                        trace["hp_stages"][-1].append(hPt)
+                        trace["hest_stages"][-1].append(ht)
     return dict(err=err, borderline=border, nbits=nbits)
 
 

@@ -70,8 +70,14 @@ def test_unit_trace_matches_oracle(ofdm):
                     trace=tr)
     g = eng.trace_unit(0, SEED, rep, k)
     np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
-    np.testing.assert_allclose(g["hp"][0], tr["hP0"][k], rtol=0, atol=1e-10)
-    np.testing.assert_allclose(g["hest"][0], tr["hest0"][k], rtol=0, atol=1e-10)
+    np.testing.assert_allclose(g["h"], np.diag(sc.Q.conj().T @ (np.asarray(
+        refsim.conv_matrix(tr["ir"][0], S.channel.PowerDelayProfile, S.N).todense()) @ sc.G)), rtol=0, atol=1e-10)
+    # every stage: LS pilot estimates and diag(D_hat) after the MMSE contraction
+    # (stage s >= 1 depends on y_est of the k_wcontract kernel).  Decisions
+    # are identical here, so the trajectories agree to fp64 rounding.
+    for st in range(S.n_iter + 1):
+        np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
 
 
 def test_error_counts_match_oracle(ofdm):

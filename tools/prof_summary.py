@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output into profiles/.
+
+usage: prof_summary.py ROUND_TAG STATS_DIR FETCH_DIR WRITE_DIR [KERNEL_SUBSTR]
+
+* copies <STATS_DIR>/**/*_kernel_stats.csv to profiles/<tag>_kernel_stats.csv
+* averages FETCH_SIZE / WRITE_SIZE (KB) per launch of the kernel and writes
+  profiles/<tag>_pmc_wcontract.json with the HBM bytes per launch, using the
+  gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE counts half of the
+  bytes of a wide (16 B/lane) coalesced streaming read, so
+  hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def one(pattern):
+    f = sorted(glob.glob(pattern, recursive=True))
+    if not f:
+        raise SystemExit("no file matches %s" % pattern)
+    return f[-1]
+
+
+def counter_mean(d, counter, kern):
+    vals = []
+    for r in csv.DictReader(open(one(os.path.join(d, "**", "*_counter_collection.csv")))):
+        if kern in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals.append(float(r["Counter_Value"]))
+    return (sum(vals) / len(vals) if vals else None), len(vals)
+
+
+def main():
+    tag, sdir, fdir, wdir = sys.argv[1:5]
+    kern = sys.argv[5] if len(sys.argv) > 5 else "k_wcontract"
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(one(os.path.join(sdir, "**", "*_kernel_stats.csv")), os.path.join(out, tag + "_kernel_stats.csv"))
+    avg_ns = None
+    for r in csv.DictReader(open(one(os.path.join(sdir, "**", "*_kernel_stats.csv")))):
+        if kern in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+    fetch, nf = counter_mean(fdir, "FETCH_SIZE", kern)
+    write, nw = counter_mean(wdir, "WRITE_SIZE", kern)
+    res = {"kernel": kern, "avg_duration_ns_rocprof": avg_ns, "fetch_size_kb_per_launch": fetch,
+           "write_size_kb_per_launch": write, "launches_sampled": [nf, nw],
+           "hbm_bytes_per_launch": (2 * fetch + write) * 1024 if fetch is not None and write is not None else None,
+           "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE reports half of "
+                         "wide coalesced reads, MI355X_MICROARCH.md §HBM)"}
+    with open(os.path.join(out, tag + "_pmc_wcontract.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

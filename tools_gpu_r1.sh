@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-1 GPU session: smoke, bench, rocprofv3 kernel stats + PMC HBM counters
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke_fail; exit 1; }
+timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench_fail; exit 1; }
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_stats" -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > gpurun_out/bench_prof.log 2>&1 || { echo prof_fail; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_fetch" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/bench_fetch.log 2>&1 || { echo fetch_fail; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_write" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/bench_write.log 2>&1 || { echo write_fail; exit 1; }
+echo all_ok
