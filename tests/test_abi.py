@@ -1,0 +1,66 @@
+"""CPU: the C-ABI shared library loads and exports exactly the entry points
+declared in include/dsce.h; the ctypes structures match the C layout.  No
+compute calls (no GPU in this container)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+import harness
+
+HDR = os.path.join(harness.ROOT, "include", "dsce.h")
+LIB = os.path.join(harness.PKG, "dsce", "libdsce.so")
+
+
+def declared():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dsce_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_and_binding_agree():
+    from dsce import engine
+    assert sorted(engine.EXPORTED) == declared()
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(LIB):
+        pytest.skip("libdsce.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    syms = set(re.findall(r"\bT (dsce_\w+)", out))
+    missing = [s for s in declared() if s not in syms]
+    assert not missing, missing
+    from dsce import engine
+    lib = engine.load_library()
+    assert lib.dsce_abi_version() == 1
+
+
+def test_struct_layout_matches_c(tmp_path):
+    import ctypes
+
+    from dsce import engine
+    src = tmp_path / "l.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dsce.h"\nint main(){printf("%zu %zu %zu %zu %zu\\n",'
+                   'sizeof(dsce_channel_desc), sizeof(dsce_scheme_desc), offsetof(dsce_scheme_desc, kappa),'
+                   'offsetof(dsce_scheme_desc, G), offsetof(dsce_scheme_desc, symbols));return 0;}\n')
+    exe = tmp_path / "l"
+    subprocess.run(["gcc", "-I", os.path.dirname(HDR), str(src), "-o", str(exe)], check=True)
+    c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    py = [ctypes.sizeof(engine.ChannelDesc), ctypes.sizeof(engine.SchemeDesc), engine.SchemeDesc.kappa.offset,
+          engine.SchemeDesc.G.offset, engine.SchemeDesc.symbols.offset]
+    assert c == py
+
+
+def test_no_cpu_fallback_without_gpu():
+    """The product path fails loudly when no HIP device is usable."""
+    if not os.path.exists(LIB):
+        pytest.skip("libdsce.so not built")
+    from dsce import engine
+    n = engine.load_library()
+    import ctypes
+    cnt = ctypes.c_int(0)
+    n.dsce_device_count(ctypes.byref(cnt))
+    if cnt.value > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(engine.DsceError):
+        engine.Engine(0)

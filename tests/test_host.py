@@ -1,0 +1,90 @@
+"""CPU: host-side mirror of the reference's setup classes (dsce.modulation /
+estimation / configs) against the structural statements of the reference."""
+import numpy as np
+import pytest
+
+import harness  # noqa: F401
+from dsce.channel import quantise_pdp
+from dsce.configs import build_setup
+from dsce.modulation import FBMC, OFDM, SignalConstellation
+
+
+def test_vehicular_a_pdp_on_sample_grid():
+    """FastFading.m:77-80/:111-129 at SR = 360 kHz."""
+    _, n = quantise_pdp("VehicularA", 360e3)
+    np.testing.assert_allclose(n, [0.979813, 0.020187], atol=1e-6)
+    assert n.sum() == pytest.approx(1.0)
+    _, n5 = quantise_pdp("VehicularA", 720e3)
+    assert n5.size == 3 and np.all(n5 > 0)
+
+
+@pytest.mark.parametrize("name,N,LKf,LKo,NP", [("default", 540, 720, 336, 16), ("c5", 1080, 1440, 672, 32)])
+def test_derived_sizes(name, N, LKf, LKo, NP):
+    """SURVEY.md appendix A1."""
+    S = build_setup(name, schemes=("ofdm",))
+    assert S.N == N
+    sc = S.schemes["ofdm"]
+    assert sc.LK == LKo and sc.n_pilots == NP and sc.n_data == LKo - NP
+    fb = FBMC(S.L, 30, 15e3, S.SR, 0, False, "Hermite-OQAM", 8, 0, True)
+    assert fb.Nr.SamplesTotal == N and fb.Nr.Subcarriers * fb.Nr.MCSymbols == LKf
+
+
+def test_paper_config_sizes():
+    fb = FBMC(24, 60, 15e3, 15e3 * 14 * 14, 0, False, "Hermite-OQAM", 8, 0, True)
+    assert fb.Nr.SamplesTotal == 7350 and fb.Implementation.TimeSpacing == 98
+
+
+def test_tx_rx_matrices_reproduce_modulation():
+    """G x == Modulation(x), Q' r == Demodulation(r) (FBMC.m:319-320, :344-345;
+    OFDM.m:185-186, :206-207)."""
+    rng = np.random.default_rng(1)
+    for mod in (FBMC(24, 30, 15e3, 360e3, 0, False, "Hermite-OQAM", 8, 0, True),
+                OFDM(24, 14, 15e3, 360e3, 0, False, 1 / 15e3 / 14, 88 / 360e3)):
+        L, K = mod.Nr.Subcarriers, mod.Nr.MCSymbols
+        x = rng.standard_normal((L, K)) + 1j * rng.standard_normal((L, K))
+        G = mod.GetTXMatrix()
+        np.testing.assert_allclose(G @ x.reshape(-1, order="F"), mod.Modulation(x), atol=1e-12)
+        r = rng.standard_normal(mod.Nr.SamplesTotal) + 1j * rng.standard_normal(mod.Nr.SamplesTotal)
+        np.testing.assert_allclose(mod.GetRXMatrix() @ r, mod.Demodulation(r).reshape(-1, order="F"), atol=1e-11)
+
+
+def test_fbmc_oqam_transmission_matrix():
+    """Real part of D = Q'G is the identity, the rest is imaginary interference
+    (FBMC.m:1-14, :371-377); GetFBMCMatrix == Demod(Mod(.)) (FBMC.m:356-357)."""
+    fb = FBMC(24, 30, 15e3, 360e3, 0, False, "Hermite-OQAM", 8, 0, True)
+    D = fb.GetRXMatrix() @ fb.GetTXMatrix()
+    np.testing.assert_allclose(D.real, np.eye(D.shape[0]), atol=1e-6)
+    Df = fb.GetFBMCMatrix()
+    for col in (0, 100, 359, 719):
+        e = np.zeros(720)
+        e[col] = 1
+        np.testing.assert_allclose(Df[:, col], fb.Demodulation(fb.Modulation(e)).reshape(-1, order="F"), atol=1e-10)
+
+
+@pytest.mark.parametrize("M,kind", [(4, "QAM"), (16, "QAM"), (256, "QAM"), (16, "PAM"), (4, "PAM")])
+def test_constellation_gray_and_order(M, kind):
+    c = SignalConstellation(M, kind)
+    lab = (c.BitMapping.astype(int) << np.arange(c.BitsPerSymbol)).sum(axis=1)
+    assert np.array_equal(lab, np.arange(M))                      # sorted by bi2de (SignalConstellation.m:64-66)
+    assert np.mean(np.abs(c.SymbolMapping) ** 2) == pytest.approx(1.0)
+    d = np.abs(c.SymbolMapping[:, None] - c.SymbolMapping[None, :])
+    dmin = d[d > 0].min()
+    for i in range(M):                                            # Gray: nearest neighbours differ in one bit
+        for k in np.flatnonzero(np.abs(d[i] - dmin) < 1e-12):
+            assert bin(i ^ k).count("1") == 1
+    bits = np.random.default_rng(0).integers(0, 2, c.BitsPerSymbol * 50).astype(np.uint8)
+    assert np.array_equal(c.Symbol2Bit(c.Bit2Symbol(bits)), bits)
+
+
+def test_precoders_cancel_pilot_interference():
+    """IIC.m:92-96 / :203-207: high SIR at the pilots, DPR normalisation."""
+    S = build_setup("default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"))
+    aux = S.schemes["fbmc_aux"].extras["iic"]
+    cod = S.schemes["fbmc_cod"].extras["iic"]
+    assert aux.SIR_dB.min() > 30 and cod.SIR_dB.min() > 20
+    for iic in (aux, cod):
+        P = iic.PrecodingMatrix
+        assert np.sum(np.abs(P) ** 2) == pytest.approx(P.shape[0])     # numel / DPR scaling
+    assert aux.NrDataSymbols == 640 and cod.NrDataSymbols == 688 and aux.NrAuxiliarySymbols == 64
+    o = S.schemes["ofdm"]
+    assert o.kappa == pytest.approx(2 * o.dpr) and o.dpr == pytest.approx(336 / (16 * 2 + 320))

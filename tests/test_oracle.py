@@ -1,0 +1,139 @@
+"""CPU: the oracle pinned against every known answer available offline
+(Random123 KATs, the reference's own closed-form BEP, structural invariants
+stated in the reference) and against its committed regression vectors."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import harness  # noqa: F401
+from oracle import philox, refsim
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_philox_known_answers():
+    for v in json.load(open(os.path.join(GOLD, "philox_kat.json"))):
+        out = philox.philox4x32_10(*[np.uint32(c) for c in v["ctr"]], *v["key"])
+        assert [int(x) for x in out] == v["out"]
+
+
+def test_stream_layout():
+    # bits: bit i = bit (i&31) of word ((i>>5)&3) of counter i>>7
+    b = philox.bits(7, 3, 2, 300)
+    w = philox._block(7, 3, philox.STREAM_BITS, 2, np.arange(3, dtype=np.uint32))
+    words = np.stack(w, axis=1).reshape(-1)
+    for i in (0, 31, 32, 127, 128, 299):
+        assert b[i] == (int(words[i >> 5]) >> (i & 31)) & 1
+    u = philox.uniforms(7, 3, philox.STREAM_THETA, 0, 5)
+    assert np.all((u >= 0) & (u < 1))
+    assert not np.array_equal(philox.uniforms(7, 4, 1, 0, 8), philox.uniforms(7, 3, 1, 0, 8))
+    re, im = philox.complex_normals(9, 1, 0, 200000)
+    assert abs(re.mean()) < 0.01 and abs(im.std() - 1) < 0.01 and abs(np.mean(re * im)) < 0.01
+    idx = philox.indices(1, 2, 0, 4000, 16)
+    assert idx.min() == 0 and idx.max() == 15
+
+
+def test_theory_bep_closed_form_4qam():
+    """Theory/BitErrorProbabilityDoublyFlatRayleigh.m vs the reference's own
+    closed form for 4-QAM (SimpleVersion_DoublyFlat.m:179)."""
+    from dsce.modulation import SignalConstellation
+    g = json.load(open(os.path.join(GOLD, "theory_4qam.json")))
+    q = SignalConstellation(4, "QAM")
+    got = refsim.bit_error_probability_doubly_flat_rayleigh(g["snr_db"], q.SymbolMapping, q.BitMapping)
+    np.testing.assert_allclose(got, g["bep"], rtol=1e-10, atol=1e-15)   # 0.5 - x cancellation at high SNR
+
+
+def test_theory_bep_256qam_lower_bound_of_figure5():
+    """The grey 'doubly-flat theory' line of png/Figure5.png is ~0.0129 at 32 dB."""
+    from dsce.modulation import SignalConstellation
+    q = SignalConstellation(256, "QAM")
+    b = refsim.bit_error_probability_doubly_flat_rayleigh([32.0], q.SymbolMapping, q.BitMapping)[0]
+    assert abs(b - 0.0129) < 0.0004
+
+
+def test_jakes_statistics():
+    """Sum of sinusoids: E|h_tau|^2 = PDPn[tau], E{h(n) h*(n+k)} ~ J0(2 pi fD k dt)."""
+    from dsce.configs import build_setup
+    S = build_setup("default", schemes=())
+    ch = S.channel
+    irs = np.stack([refsim.jakes_ir(3, r, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
+                                    ch.MaximumDopplerShift, ch.Paths) for r in range(300)])
+    p = np.mean(np.abs(irs) ** 2, axis=(0, 1))
+    np.testing.assert_allclose(p, ch.PowerDelayProfileNormalized, rtol=0.12)
+    lag = 200
+    c = np.mean(irs[:, :-lag, 0] * np.conj(irs[:, lag:, 0])) / ch.PowerDelayProfileNormalized[0]
+    tc = refsim.time_correlation(S.N, ch.dt, ch.MaximumDopplerShift)[S.N - 1 + lag]
+    assert abs(c.real - tc) < 0.12
+
+
+def test_convolution_matrix_structure():
+    """GetConvolutionMatrix: H[n, n - tau] = IR[n, tau], zero elsewhere."""
+    N = 40
+    pdp = np.array([0.5, 0.0, 0.3, 0.2])
+    ir = (np.arange(N)[:, None] + 1j * np.arange(4)[None, :]) * (pdp > 0)
+    H = refsim.conv_matrix(ir, pdp, N).toarray()
+    ref = np.zeros((N, N), dtype=complex)
+    for tau in np.flatnonzero(pdp):
+        for n in range(tau, N):
+            ref[n, n - tau] = ir[n, tau]
+    np.testing.assert_array_equal(H, ref)
+
+
+def test_correlation_matrix_literal_structure():
+    """R_vecH[vec(H[a+tau,a]), vec(H[b+tau,b])] = PDPn[tau] J0(a-b), including the
+    column wrap of FastFading.m:377 for tau >= 2 (entries with a+tau >= N land in
+    row a+tau-N of column a+1 and survive the crop at N^2)."""
+    N = 12
+    pdp = np.array([0.6, 0.3, 0.1])
+    tc = refsim.time_correlation(N, 1 / 720e3, 1158.18)
+    R = refsim.correlation_matrix(N, pdp, tc).toarray()
+    f = lambda a, t: a * (N + 1) + t
+    for t in range(3):
+        for a in range(N):
+            for b in range(N):
+                if f(a, t) < N * N and f(b, t) < N * N:
+                    assert R[f(a, t), f(b, t)] == pytest.approx(pdp[t] * tc[N - 1 + a - b], abs=1e-15)
+    assert R[f(N - 2, 2), f(N - 2, 2)] != 0          # the wrapped entry (row 0, column N-1)
+    assert np.count_nonzero(R) == sum(min(N, (N * N - t + N) // (N + 1)) ** 2 for t in range(3))
+
+
+@pytest.fixture(scope="module")
+def c2():
+    from dsce.configs import build_setup
+    S = build_setup("default", schemes=("ofdm",))
+    return S, harness.oracle_mmse(S, S.schemes["ofdm"])
+
+
+def test_correlation_invariants(c2):
+    S, mm = c2
+    R = mm["R_hP"]
+    np.testing.assert_allclose(R, R.conj().T, atol=1e-14)
+    assert np.linalg.eigvalsh(R).min() > -1e-12
+    for k in range(len(S.pn_time)):
+        assert np.all(np.real(np.diag(mm["R_est"][k])) >= np.real(np.diag(R)) - 1e-12)
+    w = mm["W"]
+    nz = np.abs(w[w != 0])
+    assert nz.min() >= 1e-8                               # script:287-289 threshold
+    # block-diagonal OFDM estimator: only same-symbol (r, c) pairs survive
+    LK = S.schemes["ofdm"].LK
+    W3 = w[:, 0].reshape(LK, LK, -1, order="F")
+    r, c = np.nonzero(np.abs(W3).sum(axis=2))
+    assert np.all(r // 24 == c // 24)
+
+
+def test_oracle_regression_vectors(c2):
+    S, mm = c2
+    g = json.load(open(os.path.join(GOLD, "oracle_c2_small.json")))
+    sc = S.schemes["ofdm"]
+    tr = {}
+    res = refsim.simulate(g["seed"], 0, 2, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
+                          [mm], trace=tr)
+    ir = tr["ir"][0]
+    for n, v in g["ir_rep0_samples"].items():
+        n = int(n)
+        np.testing.assert_allclose([ir[n, 0].real, ir[n, 0].imag, ir[n, 1].real, ir[n, 1].imag], v, atol=1e-13)
+    np.testing.assert_allclose([[z.real, z.imag] for z in np.diag(mm["R_hP"])], g["rhp_diag"], atol=1e-13)
+    assert res["err"].tolist() == g["err"]
+    assert res["nbits"].tolist() == g["nbits"]
