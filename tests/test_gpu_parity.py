@@ -91,3 +91,75 @@ def test_error_counts_match_oracle(ofdm):
     assert diff <= 8 * res["borderline"].sum(), (cg - co)
     b = eng.bits_per_rep(0)
     assert b[0] == sc.n_bits and b[1] == sc.considered_symbols.sum() * sc.bits_per_symbol
+
+
+# ---------------------------------------------------------------------------
+# C3 / C4: FBMC-OQAM with auxiliary-symbol and data-spreading precoders
+# (two SNR points keep the literal oracle's run time in check)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module", params=["fbmc_aux", "fbmc_cod"])
+def fbmc(request):
+    from dsce.engine import build_engine
+    S = build_setup("default", schemes=(request.param,), snr_db=[15.0, 35.0])
+    eng = build_engine(S, batch=256)
+    mm = harness.oracle_mmse(S, S.schemes[request.param])
+    yield request.param, S, eng, mm
+    eng.close()
+
+
+def test_fbmc_estimator_and_trace(fbmc):
+    name, S, eng, mm = fbmc
+    sc = S.schemes[name]
+    for k in range(2):
+        for var, key, R in ((0, "W", mm["R_est"][k]), (1, "W0", mm["R_noI"][k])):
+            wg = eng.W(0, k, var)
+            wo = mm[key][:, k]
+            scale = np.abs(wo).max()
+            tol = max(1e-14 * np.linalg.cond(R), 1e-12) * scale
+            border = np.abs(np.abs(wo) - 1e-8) <= tol
+            assert np.all((np.abs(wg - wo) <= tol) | border), (name, k, var)
+    tr = {}
+    refsim.simulate(SEED, 9, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
+                    trace=tr)
+    for k in range(2):
+        g = eng.trace_unit(0, SEED, 9, k)
+        np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
+        for st in range(S.n_iter + 1):
+            np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
+            np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
+
+
+def test_fbmc_error_counts(fbmc):
+    name, S, eng, mm = fbmc
+    sc = S.schemes[name]
+    cg = eng.run(SEED, 64, 64)
+    res = refsim.simulate(SEED, 64, 64, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
+                          [mm])
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
+
+
+def test_three_schemes_share_channel_and_noise():
+    """script:350-403: one channel draw and one noise draw per (rep, SNR) feed
+    all three schemes; a joint engine equals three single-scheme engines."""
+    from dsce.engine import build_engine
+    S = build_setup("default", snr_db=[25.0])
+    joint = build_engine(S, batch=128)
+    cj = joint.run(SEED, 0, 128)
+    joint.close()
+    for i, name in enumerate(S.schemes):
+        e = build_engine(S, schemes=(name,), batch=128)
+        np.testing.assert_array_equal(e.run(SEED, 0, 128)[0], cj[i])
+        e.close()
+
+
+def test_counts_are_additive_and_batch_invariant(ofdm):
+    """Size-independent properties at any scale: [0,2B) = [0,B) + [B,2B), and the
+    device batch size does not change a single count."""
+    S, eng, _ = ofdm
+    a = eng.run(SEED, 0, 512)
+    b = eng.run(SEED, 0, 256) + eng.run(SEED, 256, 256)
+    np.testing.assert_array_equal(a, b)
+    eng.set_batch(64)
+    c = eng.run(SEED, 0, 512)
+    eng.set_batch(256)
+    np.testing.assert_array_equal(a, c)
