@@ -886,6 +886,34 @@ int dsce_trace_unit(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, int3
     API_END
 }
 
+int dsce_mmse_onetap(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, const double* hp_ls, int32_t n,
+                     double* h_out) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!s.mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    if (k < 0 || k >= ctx->nsnr || var < 0 || var > 1 || n <= 0 || !hp_ls || !h_out)
+        throw ApiError(DSCE_EINVAL, "bad dsce_mmse_onetap arguments");
+    const int NP = s.d.n_pilots, LK = s.LK;
+    double2* dh = nullptr;
+    double2* dp = nullptr;
+    DSCE_HIP_CHECK(hipMalloc(&dp, (size_t)NP * n * sizeof(double2)));
+    try {
+        DSCE_HIP_CHECK(hipMalloc(&dh, (size_t)LK * n * sizeof(double2)));
+        DSCE_HIP_CHECK(hipMemcpyAsync(dp, hp_ls, (size_t)NP * n * sizeof(double2), hipMemcpyHostToDevice, ctx->stream));
+        launch_mmse_onetap(ctx->stream, LK, NP, s.Wd + ((size_t)var * ctx->nsnr + k) * LK * NP, dp, n, dh);
+        DSCE_HIP_CHECK(hipMemcpyAsync(h_out, dh, (size_t)LK * n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+        DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+        (void)hipFree(dp);
+        if (dh) (void)hipFree(dh);
+        throw;
+    }
+    DSCE_HIP_CHECK(hipFree(dp));
+    DSCE_HIP_CHECK(hipFree(dh));
+    API_END
+}
+
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable) {
     API_BEGIN
     check_ctx(ctx);

@@ -51,6 +51,7 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
                   McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t* dummy);
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
 void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b);
+void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)
 struct SetupArgs {

@@ -649,4 +649,20 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
         hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v, b.u);
 }
 
+// MMSE one-tap channel h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p for n LS
+// vectors (PSACE 'MMSE' slot, script:417-428); hp NP x n, h LK x n (column-major).
+__global__ void k_mmse_onetap(int LK, int NP, const double2* __restrict__ wd, const double2* __restrict__ hp, int n,
+                              double2* __restrict__ h) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int u = blockIdx.y;
+    if (c >= LK || u >= n) return;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int p = 0; p < NP; ++p) c_fma(acc, wd[(size_t)c * NP + p], hp[(size_t)u * NP + p]);
+    h[(size_t)u * LK + c] = acc;
+}
+
+void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h) {
+    hipLaunchKernelGGL(k_mmse_onetap, dim3((LK + 63) / 64, n), dim3(64), 0, s, LK, NP, wd, hp, n, h);
+}
+
 }  // namespace dsce

@@ -20,7 +20,7 @@ EXPORTED = [
     "dsce_abi_version", "dsce_device_count", "dsce_create", "dsce_destroy", "dsce_last_error",
     "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
     "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
-    "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model",
+    "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap",
 ]
 
 
@@ -78,6 +78,7 @@ def load_library(path=None):
     lib.dsce_enable_timing.argtypes = [vp, C.c_int32]
     lib.dsce_kernel_time.argtypes = [vp, C.c_char_p, i64p, dp]
     lib.dsce_work_model.argtypes = [vp, C.c_int32, dp, dp]
+    lib.dsce_mmse_onetap.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, dp, C.c_int32, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -226,6 +227,20 @@ class Engine:
                                            _dptr(hp), _dptr(he), _dptr(h)), "dsce_trace_unit")
         v = lambda a: a.view(np.complex128)
         return dict(y=v(y), hp=v(hp).reshape(ns, sc.n_pilots), hest=v(he).reshape(ns, sc.LK), h=v(h))
+
+    def mmse_onetap(self, sid, snr_index, hp_ls, variant=0):
+        """h_hat = diag(sum_p W_p hP_p) for LS vectors hp_ls (NP,) or (NP, n)."""
+        sc = self.schemes[sid]
+        hp = np.asarray(hp_ls, dtype=np.complex128)
+        one = hp.ndim == 1
+        hp = np.ascontiguousarray(hp.reshape(sc.n_pilots, -1).T)      # n x NP rows = column-major NP x n
+        n = hp.shape[0]
+        out = np.zeros(2 * sc.LK * n)
+        self._chk(self.lib.dsce_mmse_onetap(self.h, int(sid), int(snr_index), int(variant),
+                                            hp.ctypes.data_as(C.POINTER(C.c_double)), n, _dptr(out)),
+                  "dsce_mmse_onetap")
+        h = out.view(np.complex128).reshape(n, sc.LK).T
+        return h[:, 0] if one else h
 
     # -- measurement -----------------------------------------------------------
     def enable_timing(self, on=True):

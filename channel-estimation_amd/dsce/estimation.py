@@ -263,8 +263,14 @@ class PilotSymbolAidedChannelEstimation:
                 Imat[pos, sel - 1] = 1.0 / sel.size
         self.InterpolationMatrix = Imat
 
-    def set_mmse_engine(self, fn):
-        """Attach the engine callback used by the 'MMSE' method (plug-in slot)."""
+    def set_mmse_engine(self, engine, scheme_id, snr_index, variant=0):
+        """Bind the 'MMSE' method to a built HIP engine (dsce.engine.Engine after
+        build_mmse): ChannelInterpolation(LS) then returns the L x K MMSE
+        one-tap channel diag(sum_p W_p hP_p) of script:417-428."""
+        shape = self.PilotMatrix.shape
+
+        def fn(ls):
+            return engine.mmse_onetap(scheme_id, snr_index, ls, variant).reshape(shape, order="F")
         self._mmse = fn
 
     def ChannelInterpolation(self, LS):

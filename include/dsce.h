@@ -20,6 +20,9 @@
  *                            (stubbed with error() at PSACE.m:110-111)
  *   dsce_run              <- the Monte-Carlo loop body          script:350-564
  *                            ('MMSE' ChannelInterpolation, PSACE.m:128-129, per stage)
+ *   dsce_mmse_onetap      <- PilotSymbolAidedChannelEstimation.ChannelInterpolation,
+ *                            method 'MMSE' (PSACE.m:128-129 stub): h_hat = diag(sum_p W_p hP_p),
+ *                            script:417-428
  *   dsce_get_correlation / dsce_get_W <- R_hP*, W_MMSE_*          script:210-313 (parity probes)
  *
  * Conventions
@@ -132,6 +135,12 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
 
 /* Bits per realisation of a scheme: [0] all data bits, [1] no-edge bits. */
 int dsce_bits_per_rep(dsce_ctx* ctx, int32_t scheme_id, int64_t* bits2);
+
+/* MMSE one-tap channel for n_units LS pilot-estimate vectors (the 'MMSE' slot of
+ * PilotSymbolAidedChannelEstimation): hp_ls is NP x n_units complex
+ * (column-major), h_out LK x n_units complex; variant 0 = W, 1 = W0. */
+int dsce_mmse_onetap(dsce_ctx* ctx, int32_t scheme_id, int32_t snr_index, int32_t variant, const double* hp_ls,
+                     int32_t n_units, double* h_out);
 
 /* ---- parity probes (same kernels as dsce_run) ---------------------------- */
 /* ImpulseResponse of realisation `rep`: N x n_taps complex, column-major. */

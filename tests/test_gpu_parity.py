@@ -163,3 +163,21 @@ def test_counts_are_additive_and_batch_invariant(ofdm):
     c = eng.run(SEED, 0, 512)
     eng.set_batch(256)
     np.testing.assert_array_equal(a, c)
+
+
+def test_psace_mmse_plugin(ofdm):
+    """The 'MMSE' method of PilotSymbolAidedChannelEstimation (a stub in the
+    reference, PSACE.m:110-111/:128-129) served by the engine equals
+    diag(sum_p W_p hP_p) of script:417-428."""
+    from dsce.estimation import PilotSymbolAidedChannelEstimation
+    S, eng, mm = ofdm
+    sc = S.schemes["ofdm"]
+    pm = sc.extras["pilot_matrix"]
+    est = PilotSymbolAidedChannelEstimation("Custom", pm, "MMSE")
+    est.set_mmse_engine(eng, 0, 3)
+    rng = np.random.default_rng(4)
+    ls = rng.standard_normal(16) + 1j * rng.standard_normal(16)
+    got = est.ChannelInterpolation(ls)
+    W3 = mm["W"][:, 3].reshape(sc.LK, sc.LK, 16, order="F")
+    ref = np.diag((W3 * ls[None, None, :]).sum(axis=2))
+    np.testing.assert_allclose(got.reshape(-1, order="F"), ref, rtol=0, atol=1e-11 * np.abs(ref).max())
