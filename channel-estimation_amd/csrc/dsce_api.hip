@@ -3,6 +3,7 @@
 // the setup pipeline (script:208-313) and the batched Monte-Carlo loop
 // (script:350-564).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -84,7 +85,7 @@ struct Scheme {
     std::vector<uint8_t> considered;
     std::vector<double2> symbols;
     SchemeK k{};
-    HostBand gband, qband, wband;
+    HostBand gband, qband, wband, wband_struct;   // wband: trimmed after build_mmse
     Band Wb{};
     long long w_elems = 0, w_struct = 0;
     double2* W = nullptr;
@@ -144,6 +145,15 @@ T* dupload(dsce_ctx* c, const std::vector<T>& v) {
     T* p = dalloc<T>(c, v.size());
     if (!v.empty()) DSCE_HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return p;
+}
+
+void free_alloc(dsce_ctx* c, void* p) {
+    for (auto it = c->allocs.begin(); it != c->allocs.end(); ++it)
+        if (*it == p) {
+            DSCE_HIP_CHECK(hipFree(*it));
+            c->allocs.erase(it);
+            return;
+        }
 }
 
 hipEvent_t get_event(dsce_ctx* c) {
@@ -359,12 +369,69 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.g_start = dupload(c, gs);
     k.g_col = dupload(c, gcol);
     k.GL = s.GL;
+    s.wband_struct = s.wband;
     s.Wb = upload_band(c, s.wband, false);
     // bits per realisation
     s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;
     int64_t ce = 0;
     for (auto v : s.considered) ce += v ? 1 : 0;
     s.bits_noedge = ce * s.d.bits_per_symbol;
+}
+
+// ---------------------------------------------------------------------------
+// Trim every W block to the column range that holds a non-zero entry in some
+// (variant, SNR) slice after the 1e-8 threshold, and repack.  The contraction
+// only skips exact zeros, so results are bit-identical; at C3/C4 the thresholded
+// estimator spans |dk| <= 7 symbols instead of the structural 15.
+// ---------------------------------------------------------------------------
+void trim_w_band(dsce_ctx* c, Scheme& s, std::vector<void*>& tmp) {
+    const char* env = getenv("DSCE_WTRIM");      // "0": keep the structural band (A/B, tests)
+    if (env && env[0] == '0') return;
+    hipStream_t st = c->stream;
+    const int NP = s.d.n_pilots, nsl = 2 * c->nsnr, nblk = (int)s.wband.row0.size();
+    int* dlohi;
+    DSCE_HIP_CHECK(hipMalloc(&dlohi, 2 * nblk * sizeof(int)));
+    tmp.push_back(dlohi);
+    std::vector<int> lohi(2 * nblk);
+    for (int b = 0; b < nblk; ++b) {
+        lohi[2 * b] = 1 << 30;
+        lohi[2 * b + 1] = -1;
+    }
+    DSCE_HIP_CHECK(hipMemcpy(dlohi, lohi.data(), lohi.size() * sizeof(int), hipMemcpyHostToDevice));
+    setup_w_extent(st, s.Wb, NP, s.W, s.w_elems, nsl, dlohi);
+    DSCE_HIP_CHECK(hipMemcpyAsync(lohi.data(), dlohi, lohi.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+    DSCE_HIP_CHECK(hipStreamSynchronize(st));
+    HostBand nb = s.wband;
+    nb.vals.clear();
+    long long off = 0;
+    for (int b = 0; b < nblk; ++b) {
+        const int clo = s.wband.klo[b] / NP;
+        int lo = lohi[2 * b], hi = lohi[2 * b + 1];
+        if (hi < lo) { lo = 0; hi = -1; }
+        nb.klo[b] = (clo + lo) * NP;
+        nb.khi[b] = (clo + hi + 1) * NP;
+        nb.off[b] = off;
+        off += (long long)(hi - lo + 1) * NP * nb.rb;
+    }
+    nb.elems = off;
+    if (off == s.w_elems) return;
+    double2* W2 = dalloc<double2>(c, (size_t)nsl * std::max<long long>(off, 1));
+    for (int sl = 0; sl < nsl; ++sl)
+        for (int b = 0; b < nblk; ++b) {
+            const long long n = (long long)(nb.khi[b] - nb.klo[b]) * nb.rb;
+            if (n == 0) continue;
+            const long long src = s.wband.off[b] + (long long)(nb.klo[b] - s.wband.klo[b]) * nb.rb;
+            DSCE_HIP_CHECK(hipMemcpyAsync(W2 + (size_t)sl * off + nb.off[b], s.W + (size_t)sl * s.w_elems + src,
+                                          n * sizeof(double2), hipMemcpyDeviceToDevice, st));
+        }
+    DSCE_HIP_CHECK(hipStreamSynchronize(st));
+    free_alloc(c, s.W);          // release the untrimmed estimator and switch geometry
+    s.W = W2;
+    s.wband = nb;
+    s.w_elems = off;
+    s.w_struct = 0;
+    for (int b = 0; b < nblk; ++b) s.w_struct += (long long)nb.nrows[b] * (nb.khi[b] - nb.klo[b]);
+    s.Wb = upload_band(c, nb, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -380,6 +447,14 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         tmp.push_back(p);
         return p;
     };
+    if (s.W) {                     // rebuild (e.g. new SNR list): back to the structural band
+        free_alloc(c, s.W);
+        free_alloc(c, s.Wd);
+        s.W = s.Wd = nullptr;
+        s.wband = s.wband_struct;
+        s.w_elems = s.wband.elems;
+        s.Wb = upload_band(c, s.wband, false);
+    }
     try {
         double2* dG = (double2*)talloc(s.G.size() * sizeof(double2));
         double2* dQ = (double2*)talloc(s.Q.size() * sizeof(double2));
@@ -460,10 +535,8 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         double2* rd = (double2*)talloc((size_t)s.w_elems * sizeof(double2));
         Band Wb = s.Wb;
         setup_rdij(st, a, Wb, m, s.k.g_start, s.GL, s.k.q_start, s.QL, rd);
-        if (!s.W) {
-            s.W = dalloc<double2>(c, (size_t)2 * nsnr * s.w_elems);
-            s.Wd = dalloc<double2>(c, (size_t)2 * nsnr * LK * NP);
-        }
+        s.W = dalloc<double2>(c, (size_t)2 * nsnr * s.w_elems);
+        s.Wd = dalloc<double2>(c, (size_t)2 * nsnr * LK * NP);
         for (int var = 0; var < 2; ++var)
             for (int k = 0; k < nsnr; ++k) {
                 const size_t vi = (size_t)var * nsnr + k;
@@ -471,6 +544,7 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
             }
         DSCE_HIP_CHECK(hipStreamSynchronize(st));
         DSCE_HIP_CHECK(hipGetLastError());
+        trim_w_band(c, s, tmp);
     } catch (...) {
         for (void* p : tmp) (void)hipFree(p);
         throw;

@@ -77,6 +77,7 @@ void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const
 void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv);
 void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
                 const int* q_start, int QL, double2* rd /* packed, w_elems */);
+void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);
 void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
              const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);
 

@@ -283,3 +283,34 @@ void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long, const
 }
 
 }  // namespace dsce
+
+namespace dsce {
+
+// Non-zero column extent of every W block over all (variant, SNR) slices, after
+// the 1e-8 threshold: lohi[2*blk] = min c_local, lohi[2*blk+1] = max c_local.
+// The contraction skips exact zeros only, so trimming is bit-exact.
+__global__ void k_w_extent(Band Wb, int NP, const double2* __restrict__ w, long long w_elems, int* __restrict__ lohi) {
+    const int blk = blockIdx.x;
+    const double2* __restrict__ ws = w + (size_t)blockIdx.y * w_elems + Wb.off[blk];
+    const int ncol = (Wb.khi[blk] - Wb.klo[blk]) / NP;
+    const long long n = (long long)ncol * NP * Wb.rb;
+    int lo = 1 << 30, hi = -1;
+    for (long long t = threadIdx.x; t < n; t += blockDim.x) {
+        const double2 v = ws[t];
+        if (v.x != 0.0 || v.y != 0.0) {
+            const int c = (int)(t / ((long long)NP * Wb.rb));
+            lo = min(lo, c);
+            hi = max(hi, c);
+        }
+    }
+    if (hi >= 0) {
+        atomicMin(&lohi[2 * blk], lo);
+        atomicMax(&lohi[2 * blk + 1], hi);
+    }
+}
+
+void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi) {
+    hipLaunchKernelGGL(k_w_extent, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, lohi);
+}
+
+}  // namespace dsce

@@ -181,3 +181,20 @@ def test_psace_mmse_plugin(ofdm):
     W3 = mm["W"][:, 3].reshape(sc.LK, sc.LK, 16, order="F")
     ref = np.diag((W3 * ls[None, None, :]).sum(axis=2))
     np.testing.assert_allclose(got.reshape(-1, order="F"), ref, rtol=0, atol=1e-11 * np.abs(ref).max())
+
+
+def test_w_band_trim_is_bit_exact(monkeypatch):
+    """Trimming W to its non-zero column extent (after the 1e-8 threshold) skips
+    exact zeros only: counts are bit-identical and the contracted work shrinks."""
+    from dsce.engine import build_engine
+    S = build_setup("default", schemes=("fbmc_aux",), snr_db=[20.0, 40.0])
+    monkeypatch.setenv("DSCE_WTRIM", "0")
+    full = build_engine(S, batch=128)
+    monkeypatch.setenv("DSCE_WTRIM", "1")
+    trim = build_engine(S, batch=128)
+    np.testing.assert_array_equal(full.run(SEED, 0, 128), trim.run(SEED, 0, 128))
+    for k in range(2):
+        np.testing.assert_array_equal(full.W(0, k, 0), trim.W(0, k, 0))
+    assert trim.work_model(0)[0] < 0.7 * full.work_model(0)[0]
+    full.close()
+    trim.close()
