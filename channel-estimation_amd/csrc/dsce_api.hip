@@ -371,6 +371,34 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.GL = s.GL;
     s.wband_struct = s.wband;
     s.Wb = upload_band(c, s.wband, false);
+    // fused-stage maps (select mode): data index per row, data range per DSCE_SRB-row block
+    {
+        std::vector<int> row_data(LK, -1);
+        if (!s.d.despread)
+            for (int i = 0; i < s.d.n_data; ++i) row_data[s.data_pos[i]] = i;
+        const int nb = (LK + DSCE_SRB - 1) / DSCE_SRB;
+        std::vector<int> i0(nb, 0), i1(nb, 0);
+        bool local = !s.d.despread;
+        for (int b = 0; b < nb; ++b) {
+            int lo = 1 << 30, hi = -1;
+            for (int r = b * DSCE_SRB; r < std::min(LK, (b + 1) * DSCE_SRB); ++r)
+                if (row_data[r] >= 0) { lo = std::min(lo, row_data[r]); hi = std::max(hi, row_data[r]); }
+            if (hi < 0) { lo = 0; hi = -1; }
+            i0[b] = lo;
+            i1[b] = hi + 1;
+            for (int i = lo; i <= hi; ++i)       // data indices of a block must sit in the block
+                if (s.data_pos[i] / DSCE_SRB != b) local = false;
+            for (int r = b * DSCE_SRB; r < std::min(LK, (b + 1) * DSCE_SRB) && local; ++r)
+                for (int j = pptr[r]; j < pptr[r + 1]; ++j) {
+                    const int kc = pcol[j] - NP;
+                    if (kc >= 0 && (kc < lo || kc > hi)) { local = false; break; }
+                }
+        }
+        s.k.row_data = dupload(c, row_data);
+        s.k.blk_i0 = dupload(c, i0);
+        s.k.blk_i1 = dupload(c, i1);
+        s.k.p_blocklocal = local ? 1 : 0;
+    }
     // bits per realisation
     s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;
     int64_t ce = 0;

@@ -627,6 +627,112 @@ __global__ void __launch_bounds__(64) k_precode(SchemeK sk, StageArgs st, const 
     }
 }
 
+// Fused stage for select-mode schemes (OFDM, FBMC auxiliary): LS, diag(D_hat),
+// one-tap quotients, detection + error counts of the data symbols of a 24-row
+// block and, when P is block-local (OFDM), the re-precoding of that block —
+// one pass, no quotient / decision round trip through HBM.  The LS pilot
+// estimates are consumed as they are formed (p-outer loop, 24 diag(D_hat)
+// accumulators in registers), so LDS only holds the constellation (shared by
+// the block's 4 waves) and the block's decisions for the precoder.
+// grid (U/(64*BW), ceil(LK/12)), block 64*BW (12-row blocks keep the 12
+// diag(D_hat) accumulators + detection state under 128 VGPRs).
+template <int BW>
+__global__ void __launch_bounds__(64 * BW) k_stage_sel(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
+                                                       const double2* __restrict__ xp,
+                                                       const uint16_t* __restrict__ sidx,
+                                                       const double2* __restrict__ h, double2* __restrict__ hp,
+                                                       double2* __restrict__ hest, uint16_t* __restrict__ qe,
+                                                       uint16_t* __restrict__ qp, double2* __restrict__ v,
+                                                       double2* __restrict__ u,
+                                                       unsigned long long* __restrict__ counters, int fuse_precode) {
+    extern __shared__ double2 smem[];
+    double2* sym = smem;                                                  // [M]
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint16_t* qloc = (uint16_t*)(smem + sk.M) + (size_t)wv * 2 * DSCE_SRB * WAVE;   // [wave][2][24][64]
+    for (int i = threadIdx.x; i < sk.M; i += 64 * BW) sym[i] = sk.symbols[i];
+    __syncthreads();
+    const int unit = blockIdx.x * (64 * BW) + threadIdx.x;
+    const int snr = (blockIdx.x * (64 * BW) + wv * 64) / st.R;
+    const int rl = unit % st.R;
+    const int U = st.U, R = st.R;
+    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    const int r0 = blockIdx.y * DSCE_SRB;
+    const int nr = min(sk.LK - r0, DSCE_SRB);
+    const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP +
+                                     (size_t)r0 * sk.NP;
+    double2 hv[DSCE_SRB];
+#pragma unroll
+    for (int r = 0; r < DSCE_SRB; ++r) hv[r] = make_double2(0.0, 0.0);
+    for (int p = 0; p < sk.NP; ++p) {
+        const double2 yv = st.ysrc_e[(size_t)sk.pilot_pos[p] * U + unit];
+        const double2 q = c_div(yv, xp[(size_t)p * R + rl]);
+        const double2 hpv = make_double2(q.x / sqk, q.y / sqk);      // LS estimate, script:412-414
+        if (blockIdx.y == 0) hp[(size_t)p * U + unit] = hpv;
+#pragma unroll
+        for (int r = 0; r < DSCE_SRB; ++r)
+            if (r < nr) c_fma(hv[r], wd[(size_t)r * sk.NP + p], hpv);
+    }
+    int cnt[4] = {0, 0, 0, 0};
+    const double dd = sk.data_div;
+#pragma unroll
+    for (int r = 0; r < DSCE_SRB; ++r) {
+        if (r >= nr) continue;
+        const size_t ix = (size_t)(r0 + r) * U + unit;
+        hest[ix] = hv[r];
+        const int i = sk.row_data[r0 + r];
+        if (i < 0) continue;
+        const double2 ze = c_div(st.ysrc_e[ix], hv[r]);
+        const double2 zp = c_div(st.ysrc_p[ix], h[(size_t)(r0 + r) * R + rl]);
+        const int de = slice(sk, sk.real_detect ? make_double2(ze.x / dd, 0.0) : make_double2(ze.x / dd, ze.y / dd));
+        const int dp = slice(sk, sk.real_detect ? make_double2(zp.x / dd, 0.0) : make_double2(zp.x / dd, zp.y / dd));
+        const int tx = sidx[(size_t)i * R + rl];
+        const int ne = __popc((unsigned)(de ^ tx)), np_ = __popc((unsigned)(dp ^ tx));
+        cnt[0] += ne;
+        cnt[2] += np_;
+        if (sk.considered[i]) {
+            cnt[1] += ne;
+            cnt[3] += np_;
+        }
+        if (!st.last) {
+            if (fuse_precode) {
+                qloc[r * WAVE + lane] = (uint16_t)de;
+                qloc[(DSCE_SRB + r) * WAVE + lane] = (uint16_t)dp;
+            } else {
+                qe[(size_t)i * U + unit] = (uint16_t)de;
+                qp[(size_t)i * U + unit] = (uint16_t)dp;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int tot = wave_sum(cnt[k]);
+        if (lane == 0 && tot) {
+            const int csi = k >> 1, edge = k & 1;
+            const size_t idx = ((((size_t)st.scheme * 2 + csi) * 2 + edge) * st.nsnr + snr) * st.nstage + st.stage;
+            atomicAdd(&counters[idx], (unsigned long long)tot);
+        }
+    }
+    if (st.last || !fuse_precode) return;
+    for (int r = r0; r < r0 + nr; ++r) {
+        double2 av = make_double2(0.0, 0.0), au = make_double2(0.0, 0.0);
+        for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
+            const int k = sk.p_col[j];
+            const double2 pv = sk.p_val[j];
+            if (k < sk.NP) {
+                const double2 x = xp[(size_t)k * R + rl];
+                c_fma(av, pv, x);
+                c_fma(au, pv, x);
+            } else {
+                const int row = sk.data_pos[k - sk.NP] - r0;
+                c_fma(av, pv, sym[qloc[row * WAVE + lane]]);
+                c_fma(au, pv, sym[qloc[(DSCE_SRB + row) * WAVE + lane]]);
+            }
+        }
+        v[(size_t)r * U + unit] = av;
+        u[(size_t)r * U + unit] = au;
+    }
+}
+
 void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
                   McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t*) {
     StageArgs st;
@@ -641,6 +747,26 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     st.ysrc_e = stage == 0 ? b.y : b.yest;
     st.ysrc_p = stage == 0 ? b.y : b.yperf;
     const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
+    // DSCE_STAGE=fused selects the one-pass stage for select-mode schemes; the
+    // 3-kernel split is the default (measured faster: the fused pass is
+    // latency-bound at 4 waves/SIMD).
+    const char* mode = getenv("DSCE_STAGE");
+    const bool fused = mode && mode[0] == 'f';
+    if (!sk.despread && fused) {
+        const bool b4 = (b.U % 256) == 0;
+        const int sblk = (sk.LK + DSCE_SRB - 1) / DSCE_SRB;
+        const size_t lds = (size_t)sk.M * sizeof(double2) + (b4 ? 4 : 1) * 2 * DSCE_SRB * WAVE * sizeof(uint16_t);
+        if (b4)
+            hipLaunchKernelGGL(k_stage_sel<4>, dim3(b.U / 256, sblk), dim3(256), lds, s, sk, st, mm.Wd, b.xp, b.sidx,
+                               b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters, sk.p_blocklocal);
+        else
+            hipLaunchKernelGGL(k_stage_sel<1>, dim3(b.U / WAVE, sblk), dim3(WAVE), lds, s, sk, st, mm.Wd, b.xp,
+                               b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters, sk.p_blocklocal);
+        if (!last && !sk.p_blocklocal)
+            hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v,
+                               b.u);
+        return;
+    }
     hipLaunchKernelGGL(k_ls_hest, dim3(b.U / WAVE, rblk), dim3(WAVE), (size_t)sk.NP * WAVE * sizeof(double2), s, sk,
                        st, mm.Wd, b.xp, b.h, b.hp, b.hest, b.e, b.e2);
     hipLaunchKernelGGL(k_detect, dim3(b.U / WAVE, (sk.ND + DET_CHUNK - 1) / DET_CHUNK), dim3(WAVE), 0, s, sk, st,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-1 GPU session: smoke, bench, rocprofv3 kernel stats + PMC HBM counters
+# GPU session: smoke, bench, rocprofv3 kernel stats + PMC HBM counters (run via gpurun from the repo root)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
