@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def one(pattern):
-    f = sorted(glob.glob(pattern, recursive=True))
+    f = sorted(glob.glob(pattern, recursive=True), key=os.path.getmtime)
     if not f:
         raise SystemExit("no file matches %s" % pattern)
     return f[-1]
