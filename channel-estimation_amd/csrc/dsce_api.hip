@@ -371,33 +371,26 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.GL = s.GL;
     s.wband_struct = s.wband;
     s.Wb = upload_band(c, s.wband, false);
-    // fused-stage maps (select mode): data index per row, data range per DSCE_SRB-row block
+    // fused-stage maps (select mode): data index per row; row-local precoder
     {
-        std::vector<int> row_data(LK, -1);
+        std::vector<int> row_data(LK, -1), row_pcol(LK, -1);
+        std::vector<double2> row_pval(LK, make_double2(0.0, 0.0));
         if (!s.d.despread)
             for (int i = 0; i < s.d.n_data; ++i) row_data[s.data_pos[i]] = i;
-        const int nb = (LK + DSCE_SRB - 1) / DSCE_SRB;
-        std::vector<int> i0(nb, 0), i1(nb, 0);
-        bool local = !s.d.despread;
-        for (int b = 0; b < nb; ++b) {
-            int lo = 1 << 30, hi = -1;
-            for (int r = b * DSCE_SRB; r < std::min(LK, (b + 1) * DSCE_SRB); ++r)
-                if (row_data[r] >= 0) { lo = std::min(lo, row_data[r]); hi = std::max(hi, row_data[r]); }
-            if (hi < 0) { lo = 0; hi = -1; }
-            i0[b] = lo;
-            i1[b] = hi + 1;
-            for (int i = lo; i <= hi; ++i)       // data indices of a block must sit in the block
-                if (s.data_pos[i] / DSCE_SRB != b) local = false;
-            for (int r = b * DSCE_SRB; r < std::min(LK, (b + 1) * DSCE_SRB) && local; ++r)
-                for (int j = pptr[r]; j < pptr[r + 1]; ++j) {
-                    const int kc = pcol[j] - NP;
-                    if (kc >= 0 && (kc < lo || kc > hi)) { local = false; break; }
-                }
+        bool diag = !s.d.despread;
+        for (int r = 0; r < LK && diag; ++r) {
+            if (pptr[r + 1] - pptr[r] > 1) diag = false;
+            else if (pptr[r + 1] == pptr[r] + 1) {
+                const int kc = pcol[pptr[r]];
+                if (kc >= NP && s.data_pos[kc - NP] != r) diag = false;
+                row_pcol[r] = kc;
+                row_pval[r] = pval[pptr[r]];
+            }
         }
         s.k.row_data = dupload(c, row_data);
-        s.k.blk_i0 = dupload(c, i0);
-        s.k.blk_i1 = dupload(c, i1);
-        s.k.p_blocklocal = local ? 1 : 0;
+        s.k.row_pcol = dupload(c, row_pcol);
+        s.k.row_pval = dupload(c, row_pval);
+        s.k.p_diag = diag ? 1 : 0;
     }
     // bits per realisation
     s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;
@@ -584,6 +577,15 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
 // ---------------------------------------------------------------------------
 // Monte-Carlo batches
 // ---------------------------------------------------------------------------
+// SNR points processed together by the receiver kernels (DSCE_SNR_CHUNK, default
+// all): smaller chunks shrink the per-unit working set of a stage.
+int snr_chunk(dsce_ctx* c) {
+    const char* e = getenv("DSCE_SNR_CHUNK");
+    int k = e ? atoi(e) : 0;
+    if (k <= 0 || k > c->nsnr) k = c->nsnr;
+    return k;
+}
+
 void ensure_buffers(dsce_ctx* c, int R) {
     size_t N = 0, LK = 0, NP = 0, ND = 0;
     for (auto& s : c->schemes) {
@@ -592,12 +594,12 @@ void ensure_buffers(dsce_ctx* c, int R) {
         NP = std::max<size_t>(NP, s->d.n_pilots);
         ND = std::max<size_t>(ND, s->d.n_data);
     }
-    const size_t key[6] = {(size_t)R, N, LK, NP, ND, (size_t)c->nsnr};
+    const size_t key[6] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c)};
     if (memcmp(key, c->buf_key, sizeof(key)) == 0) return;
     for (void* p : c->buf_allocs) (void)hipFree(p);
     c->buf_allocs.clear();
     memcpy(c->buf_key, key, sizeof(key));
-    const size_t U = (size_t)R * c->nsnr;
+    const size_t U = (size_t)R * snr_chunk(c);
     McBuffers& b = c->buf;
     auto* L = &c->buf_allocs;
     b.R = R;
@@ -642,12 +644,12 @@ int var_of_stage(int stage, int niter) { return (stage == 0 || stage <= niter / 
 void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, const Trace* tr) {
     McBuffers& b = c->buf;
     b.R = R;
-    b.U = R * c->nsnr;
     {
         Timed t(c, "k_jakes");
         launch_jakes(c->stream, c->ch, seed, rep0, R, b.ir);
     }
     (void)valid;
+    const int chunk = snr_chunk(c);
     for (size_t si = 0; si < c->schemes.size(); ++si) {
         Scheme& s = *c->schemes[si];
         MmseK mm{};
@@ -656,39 +658,43 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.w_elems = s.w_elems;
         mm.nsnr = c->nsnr;
         mm.Wb = s.Wb;
-        const bool tracing = tr && tr->scheme == (int)si;
-        const int tunit = tracing ? tr->snr * R + tr->lane : 0;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
         }
-        {
-            Timed t(c, "rx_front");
-            launch_rx_front(c->stream, s.k, c->ch, c->d_pn, seed, rep0, b);
-        }
-        if (tracing) {
-            copy_col(c, tr->y, b.y, s.LK, b.U, tunit);
-            copy_col(c, tr->h, b.h, s.LK, R, tr->lane);
-        }
-        for (int it = 0; it <= c->niter; ++it) {
-            if (it > 0) {
-                {
-                    Timed t(c, "k_wcontract");
-                    launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
-                }
-                {
-                    Timed t(c, "perfect_ic");
-                    launch_perfect_ic(c->stream, s.k, c->ch, b);
-                }
-            }
+        for (int s0 = 0; s0 < c->nsnr; s0 += chunk) {
+            b.snr0 = s0;
+            b.U = R * std::min(chunk, c->nsnr - s0);
+            const bool tracing = tr && tr->scheme == (int)si && tr->snr >= s0 && tr->snr < s0 + chunk;
+            const int tunit = tracing ? (tr->snr - s0) * R + tr->lane : 0;
             {
-                Timed t(c, "k_stage");
-                launch_stage(c->stream, s.k, mm, it, var_of_stage(it, c->niter), c->niter, it == c->niter, b,
-                             c->d_counters, (int)si, nullptr);
+                Timed t(c, "rx_front");
+                launch_rx_front(c->stream, s.k, c->ch, c->d_pn, seed, rep0, b);
             }
             if (tracing) {
-                copy_col(c, tr->hp + (size_t)2 * it * s.d.n_pilots, b.hp, s.d.n_pilots, b.U, tunit);
-                copy_col(c, tr->hest + (size_t)2 * it * s.LK, b.hest, s.LK, b.U, tunit);
+                copy_col(c, tr->y, b.y, s.LK, b.U, tunit);
+                copy_col(c, tr->h, b.h, s.LK, R, tr->lane);
+            }
+            for (int it = 0; it <= c->niter; ++it) {
+                if (it > 0) {
+                    {
+                        Timed t(c, "k_wcontract");
+                        launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
+                    }
+                    {
+                        Timed t(c, "perfect_ic");
+                        launch_perfect_ic(c->stream, s.k, c->ch, b);
+                    }
+                }
+                {
+                    Timed t(c, "k_stage");
+                    launch_stage(c->stream, s.k, mm, it, var_of_stage(it, c->niter), c->niter, it == c->niter, b,
+                                 c->d_counters, (int)si, tracing);
+                }
+                if (tracing) {
+                    copy_col(c, tr->hp + (size_t)2 * it * s.d.n_pilots, b.hp, s.d.n_pilots, b.U, tunit);
+                    copy_col(c, tr->hest + (size_t)2 * it * s.LK, b.hest, s.LK, b.U, tunit);
+                }
             }
         }
     }
@@ -970,6 +976,16 @@ int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out)
                     w_out[2 * o + 1] = v.y;
                 }
     }
+    // the packed band holds D_hat's off-diagonal part; the diagonal is in Wd
+    std::vector<double2> wd(LK * NP);
+    DSCE_HIP_CHECK(hipMemcpy(wd.data(), s.Wd + ((size_t)var * ctx->nsnr + k) * LK * NP, wd.size() * sizeof(double2),
+                             hipMemcpyDeviceToHost));
+    for (size_t c = 0; c < LK; ++c)
+        for (size_t p = 0; p < NP; ++p) {
+            const size_t o = c + LK * c + LK * LK * p;
+            w_out[2 * o] = wd[c * NP + p].x;
+            w_out[2 * o + 1] = wd[c * NP + p].y;
+        }
     API_END
 }
 

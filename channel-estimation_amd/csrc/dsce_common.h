@@ -12,7 +12,6 @@
 #include <stdint.h>
 
 #define DSCE_RB 24          // rows per block of the G / Q^H bands (banded matvec tile)
-#define DSCE_SRB 12         // rows per block of the fused receiver stage
 #define DSCE_WRB 32         // rows per block of the MMSE estimator W (two 16-row MFMA tiles)
 #define DSCE_MAX_NP 64
 #define DSCE_MAX_TAPS 64
@@ -125,12 +124,13 @@ struct SchemeK {
     const double2* g_col;         // LK x GL
     int GL;
     // fused receiver stage (select-mode detection): per LK row the data-symbol
-    // index detected there (-1: pilot / auxiliary), per DSCE_SRB-row block the data
-    // index range, and whether P's rows in a block only read that block's data
+    // index detected there (-1: pilot / auxiliary); when P has at most one entry
+    // per row and every data entry sits on its own row (p_diag, e.g. OFDM), the
+    // entry's column (-1: none) and value, so re-precoding is row-local
     const int* row_data;          // LK
-    const int* blk_i0;            // ceil(LK/DSCE_SRB)
-    const int* blk_i1;
-    int p_blocklocal;
+    const int* row_pcol;          // LK
+    const double2* row_pval;      // LK
+    int p_diag;
 };
 
 struct ChannelK {

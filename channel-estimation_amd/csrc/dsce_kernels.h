@@ -8,7 +8,8 @@ namespace dsce {
 struct McBuffers {
     int R;            // repetitions per batch (multiple of 64)
     int nsnr;
-    int U;            // units = nsnr * R, unit = snr * R + rep
+    int U;            // units of the current SNR chunk = nchunk * R, unit = (snr - snr0) * R + rep
+    int snr0;         // first SNR index of the chunk being processed
     // per repetition (channel shared by all schemes)
     double2* ir;      // [ntap][N][R]
     // per repetition and scheme
@@ -48,7 +49,7 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
                      uint64_t rep0, McBuffers& b);
 void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t* dummy);
+                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace);
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
 void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);

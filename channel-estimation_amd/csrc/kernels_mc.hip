@@ -273,11 +273,11 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 // ---------------------------------------------------------------------------
 // a12: r = r0 + noise (script:397-403), lane = unit; grid (U/64, ceil(N/64)).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, const double* __restrict__ pn, uint64_t seed,
+__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, const double* __restrict__ pn, uint64_t seed,
                                               uint64_t rep0, const double2* __restrict__ r0,
                                               double2* __restrict__ rbuf) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
-    const int snr = unit / R, rl = unit % R;
+    const int snr = snr0 + unit / R, rl = unit % R;
     const uint64_t rep = rep0 + (uint64_t)rl;
     const double sc = sqrt(pn[snr] / 2.0);
     const int n0 = blockIdx.y * 64;
@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, const double*
 
 void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
                      uint64_t rep0, McBuffers& b) {
-    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, pn, seed, rep0,
+    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)
     hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(b.U / WAVE, sk.QH.nblk), dim3(WAVE), 0, s, sk.QH,
@@ -344,16 +344,15 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // Wave tile: 32 rows x 32 units (2 x 2 complex tiles, 64 accumulator AGPRs ->
 // 2-3 waves per SIMD).  Block = 4 waves = 128 units.  grid (U/128, nblk).
 __global__ void __launch_bounds__(256) k_wcontract_mfma(Band Wb, const double2* __restrict__ Wall, long long w_elems,
-                                                        int var, int nsnr, int NP, int R, int U,
+                                                        int var, int nsnr, int snr0, int NP, int R, int U,
                                                         const double2* __restrict__ hp,
                                                         const double2* __restrict__ v,
                                                         const double2* __restrict__ y,
-                                                        const double2* __restrict__ hest,
                                                         double2* __restrict__ yest) {
     extern __shared__ double2 shp[];                     // [4 waves][NP][32]
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int ubase = blockIdx.x * 128 + wv * 32;
-    const int snr = ubase / R;
+    const int snr = snr0 + ubase / R;
     const int blk = blockIdx.y;
     double2* sh = shp + (size_t)wv * NP * 32;
     if (l < 32)
@@ -407,9 +406,7 @@ __global__ void __launch_bounds__(256) k_wcontract_mfma(Band Wb, const double2* 
         const int row = 16 * (IT) + kk + 4 * reg;                                       \
         if (row < nrows) {                                                              \
             const size_t i_ = (size_t)(row0 + row) * U + ubase + 16 * (JT) + j;         \
-            double2 o = c_sub(y[i_], make_double2(ACCR[reg], ACCI[reg]));               \
-            o = c_add(o, c_mul(hest[i_], v[i_]));                                       \
-            yest[i_] = o;                                                               \
+            yest[i_] = c_sub(y[i_], make_double2(ACCR[reg], ACCI[reg]));                \
         }                                                                               \
     }
     STORE(r00, i00, 0, 0)
@@ -422,13 +419,12 @@ __global__ void __launch_bounds__(256) k_wcontract_mfma(Band Wb, const double2* 
 // VALU reference variant (one unit per lane, W rows wave-uniform via scalar
 // loads); kept for in-process A/B (DSCE_WCONTRACT=valu) and NP % 4 != 0.
 __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* __restrict__ Wall, long long w_elems,
-                                                       int var, int nsnr, int NP, int R, int U,
+                                                       int var, int nsnr, int snr0, int NP, int R, int U,
                                                        const double2* __restrict__ hp, const double2* __restrict__ v,
-                                                       const double2* __restrict__ y, const double2* __restrict__ hest,
-                                                       double2* __restrict__ yest) {
+                                                       const double2* __restrict__ y, double2* __restrict__ yest) {
     extern __shared__ double2 shp[];                     // [NP][64]
     const int unit = blockIdx.x * WAVE + threadIdx.x;
-    const int snr = (blockIdx.x * WAVE) / R;
+    const int snr = snr0 + (blockIdx.x * WAVE) / R;
     const int blk = blockIdx.y;
     for (int p = 0; p < NP; ++p) shp[p * WAVE + threadIdx.x] = hp[(size_t)p * U + unit];
     __syncthreads();
@@ -452,9 +448,7 @@ __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* _
     for (int r = 0; r < DSCE_WRB; ++r) {
         if (r < nrows) {
             const size_t i = (size_t)(row0 + r) * U + unit;
-            double2 o = c_sub(y[i], acc[r]);
-            o = c_add(o, c_mul(hest[i], v[i]));
-            yest[i] = o;
+            yest[i] = c_sub(y[i], acc[r]);
         }
     }
 }
@@ -466,11 +460,11 @@ void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
     if (mode && mode[0] == 'v') valu = true;
     if (valu) {
         hipLaunchKernelGGL(k_wcontract_valu, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2),
-                           s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+                           s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
     } else {
         hipLaunchKernelGGL(k_wcontract_mfma, dim3(b.U / 128, mm.Wb.nblk), dim3(256),
-                           (size_t)4 * sk.NP * 32 * sizeof(double2), s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, sk.NP,
-                           b.R, b.U, b.hp, b.v, b.y, b.hest, b.yest);
+                           (size_t)4 * sk.NP * 32 * sizeof(double2), s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0,
+                           sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
     }
 }
 
@@ -505,8 +499,52 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
     return best;
 }
 
+// Slicer tables staged in LDS (levels and the level-grid -> symbol map are
+// gathered per lane; from global memory these gathers were the stage's latency
+// chain).  The cell index comes from a multiply by 1/step: an index off by one
+// can only occur when x sits (to rounding) on a level, where both candidate
+// pairs resolve to that level; ties (mid-points) keep the first-minimum rule.
+struct SlicerLds {
+    double lvI[16], lvQ[16];
+    int grid[256];
+};
+
+__device__ __forceinline__ void slicer_load(SlicerLds& t, const SchemeK& sk, int tid, int nthreads) {
+    for (int i = tid; i < sk.nI; i += nthreads) t.lvI[i] = sk.lvI[i];
+    for (int i = tid; i < sk.nQ; i += nthreads) t.lvQ[i] = sk.lvQ[i];
+    for (int i = tid; i < sk.nI * sk.nQ; i += nthreads) t.grid[i] = sk.grid_sym[i];
+}
+
+__device__ __forceinline__ int nearest_level_fast(const double* lv, int n, double x, double istep, int& alt) {
+    alt = -1;
+    if (n == 1) return 0;
+    int i = (int)floor((x - lv[0]) * istep);
+    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i + 1]);
+    if (d1 < d0) return i + 1;
+    if (d1 == d0) alt = i + 1;
+    return i;
+}
+
+__device__ __forceinline__ int slice_fast(const SlicerLds& t, int nI, int nQ, double2 z, double sI, double sQ) {
+    int aI, aQ;
+    const int iI = nearest_level_fast(t.lvI, nI, z.x, sI, aI);
+    const int iQ = nearest_level_fast(t.lvQ, nQ, z.y, sQ, aQ);
+    int best = t.grid[iI * nQ + iQ];
+    if (aI >= 0) best = min(best, t.grid[aI * nQ + iQ]);
+    if (aQ >= 0) best = min(best, t.grid[iI * nQ + aQ]);
+    if (aI >= 0 && aQ >= 0) best = min(best, t.grid[aI * nQ + aQ]);
+    return best;
+}
+
+// a / b with one division (rounding-level differences to c_div)
+__device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
+    const double id = 1.0 / (b.x * b.x + b.y * b.y);
+    return make_double2((a.x * b.x + a.y * b.y) * id, (a.y * b.x - a.x * b.y) * id);
+}
+
 struct StageArgs {
-    int stage, var, nsnr, nstage, scheme, last, R, U;
+    int stage, var, nsnr, nstage, scheme, last, trace, R, U, snr0, xcd_order;
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
 };
@@ -520,7 +558,7 @@ __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const 
                                                 double2* __restrict__ e_est, double2* __restrict__ e_perf) {
     extern __shared__ double2 shp[];                     // [NP][64], each lane its own column
     const int unit = blockIdx.x * WAVE + threadIdx.x;
-    const int snr = (blockIdx.x * WAVE) / st.R;
+    const int snr = st.snr0 + (blockIdx.x * WAVE) / st.R;
     const int rl = unit % st.R;
     const int U = st.U, R = st.R;
     const double sqk = 1.0 / sk.inv_sqrt_kappa;
@@ -550,8 +588,14 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
                                                const double2* __restrict__ e_est, const double2* __restrict__ e_perf,
                                                uint16_t* __restrict__ qe, uint16_t* __restrict__ qp,
                                                unsigned long long* __restrict__ counters) {
+    __shared__ SlicerLds slt;
+    const bool lds_slicer = sk.nI <= 16 && sk.nQ <= 16;
+    if (lds_slicer) slicer_load(slt, sk, threadIdx.x, WAVE);
+    __syncthreads();
+    const double sI = 1.0 / (sk.nI > 1 ? sk.lvI[1] - sk.lvI[0] : 1.0);
+    const double sQ = 1.0 / (sk.nQ > 1 ? sk.lvQ[1] - sk.lvQ[0] : 1.0);
     const int unit = blockIdx.x * WAVE + threadIdx.x;
-    const int snr = (blockIdx.x * WAVE) / st.R;
+    const int snr = st.snr0 + (blockIdx.x * WAVE) / st.R;
     const int rl = unit % st.R;
     const int U = st.U, R = st.R;
     const int i0 = blockIdx.y * DET_CHUNK;
@@ -575,7 +619,7 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
                 z = sk.real_detect ? make_double2(z.x / sk.data_div, 0.0)
                                    : make_double2(z.x / sk.data_div, z.y / sk.data_div);
             }
-            const int d = slice(sk, z);
+            const int d = lds_slicer ? slice_fast(slt, sk.nI, sk.nQ, z, sI, sQ) : slice(sk, z);
             const int tx = sidx[(size_t)i * R + rl];
             const int ne = __popc((unsigned)(d ^ tx));
             cnt[csi * 2 + 0] += ne;
@@ -627,80 +671,119 @@ __global__ void __launch_bounds__(64) k_precode(SchemeK sk, StageArgs st, const 
     }
 }
 
-// Fused stage for select-mode schemes (OFDM, FBMC auxiliary): LS, diag(D_hat),
-// one-tap quotients, detection + error counts of the data symbols of a 24-row
-// block and, when P is block-local (OFDM), the re-precoding of that block —
-// one pass, no quotient / decision round trip through HBM.  The LS pilot
-// estimates are consumed as they are formed (p-outer loop, 24 diag(D_hat)
-// accumulators in registers), so LDS only holds the constellation (shared by
-// the block's 4 waves) and the block's decisions for the precoder.
-// grid (U/(64*BW), ceil(LK/12)), block 64*BW (12-row blocks keep the 12
-// diag(D_hat) accumulators + detection state under 128 VGPRs).
-template <int BW>
-__global__ void __launch_bounds__(64 * BW) k_stage_sel(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
-                                                       const double2* __restrict__ xp,
-                                                       const uint16_t* __restrict__ sidx,
-                                                       const double2* __restrict__ h, double2* __restrict__ hp,
-                                                       double2* __restrict__ hest, uint16_t* __restrict__ qe,
-                                                       uint16_t* __restrict__ qp, double2* __restrict__ v,
-                                                       double2* __restrict__ u,
-                                                       unsigned long long* __restrict__ counters, int fuse_precode) {
-    extern __shared__ double2 smem[];
-    double2* sym = smem;                                                  // [M]
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint16_t* qloc = (uint16_t*)(smem + sk.M) + (size_t)wv * 2 * DSCE_SRB * WAVE;   // [wave][2][24][64]
-    for (int i = threadIdx.x; i < sk.M; i += 64 * BW) sym[i] = sk.symbols[i];
+// LS pilot estimates alone (script:412-414 / :487-489), lane = unit; grid U/64.
+__global__ void __launch_bounds__(64) k_ls(SchemeK sk, StageArgs st, const double2* __restrict__ xp,
+                                           double2* __restrict__ hp) {
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int rl = unit % st.R;
+    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    for (int p = 0; p < sk.NP; ++p) {
+        const double2 q = c_div(st.ysrc_e[(size_t)sk.pilot_pos[p] * st.U + unit], xp[(size_t)p * st.R + rl]);
+        hp[(size_t)p * st.U + unit] = make_double2(q.x / sqk, q.y / sqk);
+    }
+}
+
+// Fused stage for select-mode schemes (OFDM, FBMC auxiliary), one pass over a
+// block of RB rows: diag(D_hat) = Wd hP (p-outer, RB accumulators, Wd rows
+// wave-uniform), one-tap quotients, slicing + error counts for both CSI
+// branches, and either the row-local re-precoding v / u (p_diag, OFDM) or the
+// decisions for k_precode.  diag(D_hat) is written only for traces; the
+// contraction uses a W band with a zero diagonal, so nothing else reads it.
+// Flat grid, row block fastest (the blocks of one unit group share hP in L2).
+template <int NPT, int RB>
+__global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, int nrb, const double2* __restrict__ Wd,
+                                                     const double2* __restrict__ xp,
+                                                     const uint16_t* __restrict__ sidx,
+                                                     const double2* __restrict__ h,
+                                                     const double2* __restrict__ hp, double2* __restrict__ hest,
+                                                     uint16_t* __restrict__ qe, uint16_t* __restrict__ qp,
+                                                     double2* __restrict__ v, double2* __restrict__ u,
+                                                     unsigned long long* __restrict__ counters) {
+    __shared__ double2 sym[256];
+    __shared__ SlicerLds slt;
+    for (int i = threadIdx.x; i < sk.M; i += 256) sym[i] = sk.symbols[i];
+    slicer_load(slt, sk, threadIdx.x, 256);
     __syncthreads();
-    const int unit = blockIdx.x * (64 * BW) + threadIdx.x;
-    const int snr = (blockIdx.x * (64 * BW) + wv * 64) / st.R;
+    // Work order: row block fastest, then SNR point, then 256-realisation group,
+    // so the blocks sharing hP (same units) and h (same realisations) run close
+    // together; with xcd_order each XCD (block b runs on XCD b % 8) walks its own
+    // contiguous range of that order, keeping the reuse inside one L2.
+    int L = blockIdx.x;
+    if (st.xcd_order) L = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    const int rbk = L % nrb;
+    int ug = L / nrb;
+    if (st.xcd_order) {
+        const int nchunk = st.U / st.R, rgs = st.R >> 8;
+        ug = (ug % nchunk) * rgs + ug / nchunk;
+    }
+    // wave index made provably uniform so Wd / row tables become scalar loads
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int ubase = ug * 256 + wv * 64;
+    if (ubase >= st.U) return;
+    const int unit = ubase + lane;
+    const int snr = st.snr0 + ubase / st.R;
     const int rl = unit % st.R;
     const int U = st.U, R = st.R;
-    const double sqk = 1.0 / sk.inv_sqrt_kappa;
-    const int r0 = blockIdx.y * DSCE_SRB;
-    const int nr = min(sk.LK - r0, DSCE_SRB);
-    const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP +
-                                     (size_t)r0 * sk.NP;
-    double2 hv[DSCE_SRB];
+    const int r0 = rbk * RB;
+    const int nr = min(RB, sk.LK - r0);
+    const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * NPT + (size_t)r0 * NPT;
+    double2 acc[RB];
 #pragma unroll
-    for (int r = 0; r < DSCE_SRB; ++r) hv[r] = make_double2(0.0, 0.0);
-    for (int p = 0; p < sk.NP; ++p) {
-        const double2 yv = st.ysrc_e[(size_t)sk.pilot_pos[p] * U + unit];
-        const double2 q = c_div(yv, xp[(size_t)p * R + rl]);
-        const double2 hpv = make_double2(q.x / sqk, q.y / sqk);      // LS estimate, script:412-414
-        if (blockIdx.y == 0) hp[(size_t)p * U + unit] = hpv;
+    for (int r = 0; r < RB; ++r) acc[r] = make_double2(0.0, 0.0);
 #pragma unroll
-        for (int r = 0; r < DSCE_SRB; ++r)
-            if (r < nr) c_fma(hv[r], wd[(size_t)r * sk.NP + p], hpv);
+    for (int p = 0; p < NPT; ++p) {
+        const double2 hv = hp[(size_t)p * U + unit];
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+            if (r < nr) c_fma(acc[r], wd[r * NPT + p], hv);
     }
+    const double idd = 1.0 / sk.data_div;
+    const double sI = 1.0 / (sk.nI > 1 ? sk.lvI[1] - sk.lvI[0] : 1.0);
+    const double sQ = 1.0 / (sk.nQ > 1 ? sk.lvQ[1] - sk.lvQ[0] : 1.0);
     int cnt[4] = {0, 0, 0, 0};
-    const double dd = sk.data_div;
 #pragma unroll
-    for (int r = 0; r < DSCE_SRB; ++r) {
-        if (r >= nr) continue;
-        const size_t ix = (size_t)(r0 + r) * U + unit;
-        hest[ix] = hv[r];
-        const int i = sk.row_data[r0 + r];
-        if (i < 0) continue;
-        const double2 ze = c_div(st.ysrc_e[ix], hv[r]);
-        const double2 zp = c_div(st.ysrc_p[ix], h[(size_t)(r0 + r) * R + rl]);
-        const int de = slice(sk, sk.real_detect ? make_double2(ze.x / dd, 0.0) : make_double2(ze.x / dd, ze.y / dd));
-        const int dp = slice(sk, sk.real_detect ? make_double2(zp.x / dd, 0.0) : make_double2(zp.x / dd, zp.y / dd));
-        const int tx = sidx[(size_t)i * R + rl];
-        const int ne = __popc((unsigned)(de ^ tx)), np_ = __popc((unsigned)(dp ^ tx));
-        cnt[0] += ne;
-        cnt[2] += np_;
-        if (sk.considered[i]) {
-            cnt[1] += ne;
-            cnt[3] += np_;
-        }
-        if (!st.last) {
-            if (fuse_precode) {
-                qloc[r * WAVE + lane] = (uint16_t)de;
-                qloc[(DSCE_SRB + r) * WAVE + lane] = (uint16_t)dp;
-            } else {
-                qe[(size_t)i * U + unit] = (uint16_t)de;
-                qp[(size_t)i * U + unit] = (uint16_t)dp;
+    for (int r = 0; r < RB; ++r) {
+        if (r < nr) {
+        const int row = r0 + r;
+        const size_t ix = (size_t)row * U + unit;
+        if (st.trace) hest[ix] = acc[r];
+        const int i = sk.row_data[row];
+        if (i >= 0) {
+            const double2 ye = st.ysrc_e[ix], yp = st.ysrc_p[ix], hh = h[(size_t)row * R + rl];
+            const int tx = sidx[(size_t)i * R + rl];
+            const double2 ze = c_div1(ye, acc[r]), zp = c_div1(yp, hh);
+            const int de = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(ze.x * idd, 0.0)
+                                                         : make_double2(ze.x * idd, ze.y * idd), sI, sQ);
+            const int dp = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(zp.x * idd, 0.0)
+                                                         : make_double2(zp.x * idd, zp.y * idd), sI, sQ);
+            const int ne = __popc((unsigned)(de ^ tx)), np_ = __popc((unsigned)(dp ^ tx));
+            const int cons = sk.considered[i];
+            cnt[0] += ne;
+            cnt[2] += np_;
+            cnt[1] += cons ? ne : 0;
+            cnt[3] += cons ? np_ : 0;
+            if (!st.last) {
+                if (sk.p_diag) {
+                    const double2 pv = sk.row_pval[row];
+                    double2 av = make_double2(0.0, 0.0), au = av;
+                    if (sk.row_pcol[row] >= 0) {
+                        c_fma(av, pv, sym[de]);
+                        c_fma(au, pv, sym[dp]);
+                    }
+                    v[ix] = av;
+                    u[ix] = au;
+                } else {
+                    qe[(size_t)i * U + unit] = (uint16_t)de;
+                    qp[(size_t)i * U + unit] = (uint16_t)dp;
+                }
             }
+        } else if (!st.last && sk.p_diag) {                // pilot / empty row
+            const int kc = sk.row_pcol[row];
+            double2 av = make_double2(0.0, 0.0);
+            if (kc >= 0) c_fma(av, sk.row_pval[row], xp[(size_t)kc * R + rl]);
+            v[ix] = av;
+            u[ix] = av;
+        }
         }
     }
 #pragma unroll
@@ -712,29 +795,31 @@ __global__ void __launch_bounds__(64 * BW) k_stage_sel(SchemeK sk, StageArgs st,
             atomicAdd(&counters[idx], (unsigned long long)tot);
         }
     }
-    if (st.last || !fuse_precode) return;
-    for (int r = r0; r < r0 + nr; ++r) {
-        double2 av = make_double2(0.0, 0.0), au = make_double2(0.0, 0.0);
-        for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
-            const int k = sk.p_col[j];
-            const double2 pv = sk.p_val[j];
-            if (k < sk.NP) {
-                const double2 x = xp[(size_t)k * R + rl];
-                c_fma(av, pv, x);
-                c_fma(au, pv, x);
-            } else {
-                const int row = sk.data_pos[k - sk.NP] - r0;
-                c_fma(av, pv, sym[qloc[row * WAVE + lane]]);
-                c_fma(au, pv, sym[qloc[(DSCE_SRB + row) * WAVE + lane]]);
-            }
-        }
-        v[(size_t)r * U + unit] = av;
-        u[(size_t)r * U + unit] = au;
+}
+
+template <int NPT>
+static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
+                                  unsigned long long* counters, int rb) {
+    const int ug = (b.U + 255) / 256;
+    const char* xe = getenv("DSCE_XCD");
+    const bool xcd = !xe || xe[0] != '0';
+#define LAUNCH_SF(RBV)                                                                                          \
+    {                                                                                                           \
+        const int nrb = (sk.LK + (RBV) - 1) / (RBV);                                                            \
+        StageArgs sa = st;                                                                                      \
+        sa.xcd_order = xcd && (b.R % 256) == 0 && ((ug * nrb) % 8) == 0;                                        \
+        hipLaunchKernelGGL((k_stage_fused<NPT, RBV>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb, mm.Wd, b.xp,  \
+                           b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);                          \
+        return true;                                                                                            \
     }
+    if (rb == 4) LAUNCH_SF(4)
+    if (rb == 16) LAUNCH_SF(16)
+    LAUNCH_SF(8)
+#undef LAUNCH_SF
 }
 
 void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, const uint64_t*) {
+                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace) {
     StageArgs st;
     st.stage = stage;
     st.var = var;
@@ -742,27 +827,27 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     st.nstage = n_iter + 1;
     st.scheme = scheme_index;
     st.last = last ? 1 : 0;
+    st.trace = trace ? 1 : 0;
     st.R = b.R;
     st.U = b.U;
+    st.snr0 = b.snr0;
+    st.xcd_order = 0;
     st.ysrc_e = stage == 0 ? b.y : b.yest;
     st.ysrc_p = stage == 0 ? b.y : b.yperf;
     const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
-    // DSCE_STAGE=fused selects the one-pass stage for select-mode schemes; the
-    // 3-kernel split is the default (measured faster: the fused pass is
-    // latency-bound at 4 waves/SIMD).
+    // select-mode schemes: k_ls + one fused pass (DSCE_STAGE=split keeps the
+    // 3-kernel path for A/B; DSCE_STAGE_RB = rows per fused block, 4 | 8 | 16)
     const char* mode = getenv("DSCE_STAGE");
-    const bool fused = mode && mode[0] == 'f';
-    if (!sk.despread && fused) {
-        const bool b4 = (b.U % 256) == 0;
-        const int sblk = (sk.LK + DSCE_SRB - 1) / DSCE_SRB;
-        const size_t lds = (size_t)sk.M * sizeof(double2) + (b4 ? 4 : 1) * 2 * DSCE_SRB * WAVE * sizeof(uint16_t);
-        if (b4)
-            hipLaunchKernelGGL(k_stage_sel<4>, dim3(b.U / 256, sblk), dim3(256), lds, s, sk, st, mm.Wd, b.xp, b.sidx,
-                               b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters, sk.p_blocklocal);
-        else
-            hipLaunchKernelGGL(k_stage_sel<1>, dim3(b.U / WAVE, sblk), dim3(WAVE), lds, s, sk, st, mm.Wd, b.xp,
-                               b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters, sk.p_blocklocal);
-        if (!last && !sk.p_blocklocal)
+    const bool split = mode && mode[0] == 's';
+    if (!sk.despread && !split && (sk.NP == 8 || sk.NP == 16 || sk.NP == 32) && sk.M <= 256 && sk.nI <= 16 &&
+        sk.nQ <= 16) {
+        const char* e = getenv("DSCE_STAGE_RB");
+        const int rb = e ? atoi(e) : 8;
+        hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);
+        if (sk.NP == 8) launch_stage_fused_np<8>(s, sk, st, mm, b, counters, rb);
+        else if (sk.NP == 16) launch_stage_fused_np<16>(s, sk, st, mm, b, counters, rb);
+        else launch_stage_fused_np<32>(s, sk, st, mm, b, counters, rb);
+        if (!last && !sk.p_diag)
             hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v,
                                b.u);
         return;

@@ -271,8 +271,10 @@ __global__ void k_w(SetupArgs a, Band Wb, const double2* __restrict__ rd, const 
                 for (int p = 0; p < a.NP; ++p)
                     c_fma(acc, in[((size_t)cl * a.NP + p) * rb + rl], rinv[(size_t)pp * a.NP + p]);
             if (hypot(acc.x, acc.y) < a.thr) acc = make_double2(0.0, 0.0);
-            out[((size_t)cl * a.NP + pp) * rb + rl] = acc;
-            if (rl < nrows && row0 + rl == c) wd[(size_t)c * a.NP + pp] = acc;
+            // the diagonal lives in wd only: the contraction applies D_hat - diag(D_hat)
+            const bool dg = rl < nrows && row0 + rl == c;
+            out[((size_t)cl * a.NP + pp) * rb + rl] = dg ? make_double2(0.0, 0.0) : acc;
+            if (dg) wd[(size_t)c * a.NP + pp] = acc;
         }
     }
 }
