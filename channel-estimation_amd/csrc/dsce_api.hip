@@ -90,6 +90,9 @@ struct Scheme {
     long long w_elems = 0, w_struct = 0;
     double2* W = nullptr;
     double2* Wd = nullptr;
+    double2* Wp = nullptr;          // pair-tile copy of W for k_wpair (null: not eligible)
+    long long wp_elems = 0, wp_exec = 0;
+    PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
     bool mmse_ready = false;
     int64_t bits_all = 0, bits_noedge = 0;
@@ -105,6 +108,8 @@ using namespace dsce;
 struct dsce_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;        // perfect-CSI branch of the IC iterations
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool chan_set = false;
     ChannelK ch{};
@@ -114,6 +119,7 @@ struct dsce_ctx {
     double* d_pn = nullptr;
     std::vector<std::unique_ptr<Scheme>> schemes;
     int batch = 8192;
+    bool streams2 = true;                 // DSCE_STREAMS=1 serialises the two IC chains
     McBuffers buf{};
     size_t buf_key[6] = {0, 0, 0, 0, 0, 0};
     std::vector<void*> buf_allocs;
@@ -171,17 +177,19 @@ struct Timed {
     dsce_ctx* c;
     dsce_ctx::Ev ev;
     bool on;
-    Timed(dsce_ctx* ctx, const char* name) : c(ctx), on(ctx->timing) {
+    hipStream_t st;
+    Timed(dsce_ctx* ctx, const char* name, hipStream_t on_stream = nullptr)
+        : c(ctx), on(ctx->timing), st(on_stream ? on_stream : ctx->stream) {
         if (on) {
             ev.name = name;
             ev.a = get_event(c);
             ev.b = get_event(c);
-            DSCE_HIP_CHECK(hipEventRecord(ev.a, c->stream));
+            DSCE_HIP_CHECK(hipEventRecord(ev.a, st));
         }
     }
     ~Timed() {
         if (on) {
-            (void)hipEventRecord(ev.b, c->stream);
+            (void)hipEventRecord(ev.b, st);
             c->pending.push_back(ev);
         }
     }
@@ -348,13 +356,15 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.data_div = s.d.data_div;
     k.pilot_pos = dupload(c, s.pilot_pos);
     k.data_pos = dupload(c, s.data_pos);
-    k.considered = dupload(c, s.considered);
+    k.considered = dupload(c, std::vector<int>(s.considered.begin(), s.considered.end()));
     k.symbols = dupload(c, s.symbols);
     k.nI = (int)lvI.size();
     k.nQ = (int)lvQ.size();
     k.lvI = dupload(c, lvI);
     k.lvQ = dupload(c, lvQ);
     k.grid_sym = dupload(c, grid);
+    k.slI = lvI.size() > 1 ? 1.0 / (lvI[1] - lvI[0]) : 1.0;
+    k.slQ = lvQ.size() > 1 ? 1.0 / (lvQ[1] - lvQ[0]) : 1.0;
     k.p_ptr = dupload(c, pptr);
     k.p_col = dupload(c, pcol);
     k.p_val = dupload(c, pval);
@@ -387,7 +397,11 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
                 row_pval[r] = pval[pptr[r]];
             }
         }
+        std::vector<int> row_cons(LK, 0);
+        for (int r = 0; r < LK; ++r)
+            if (row_data[r] >= 0) row_cons[r] = s.considered[row_data[r]] ? 1 : 0;
         s.k.row_data = dupload(c, row_data);
+        s.k.row_cons = dupload(c, row_cons);
         s.k.row_pcol = dupload(c, row_pcol);
         s.k.row_pval = dupload(c, row_pval);
         s.k.p_diag = diag ? 1 : 0;
@@ -457,6 +471,46 @@ void trim_w_band(dsce_ctx* c, Scheme& s, std::vector<void*>& tmp) {
 
 // ---------------------------------------------------------------------------
 // setup pipeline: R_hP, R_est, R_noI, R_Dij, W, W0 (script:208-313)
+// Pair-tile copy of the trimmed W band for k_wpair (NP a multiple of 4 with
+// NP/4 in {2, 4, 8}; 24-row pair blocks when every block has <= 24 rows, else 32).
+void build_wpair(dsce_ctx* c, Scheme& s) {
+    const int NP = s.d.n_pilots, nblk = (int)s.wband.row0.size();
+    if (NP % 4 != 0 || (NP / 4 != 2 && NP / 4 != 4 && NP / 4 != 8)) return;
+    int maxrows = 0;
+    for (int b = 0; b < nblk; ++b) maxrows = std::max(maxrows, s.wband.nrows[b]);
+    if (maxrows > 32) return;
+    const int rbp = maxrows <= 24 ? 24 : 32;
+    std::vector<int> row0(nblk), nrows(nblk), clo(nblk), ntile(nblk);
+    std::vector<long long> off(nblk);
+    long long o = 0, exec = 0;
+    for (int b = 0; b < nblk; ++b) {
+        row0[b] = s.wband.row0[b];
+        nrows[b] = s.wband.nrows[b];
+        clo[b] = s.wband.klo[b] / NP;
+        int ncol = (s.wband.khi[b] - s.wband.klo[b]) / NP;
+        if (rbp == 24) ncol += ncol & 1;                 // tiles come in periods of 3 (2 columns)
+        ntile[b] = ncol * rbp / 16;
+        off[b] = o;
+        o += (long long)ntile[b] * NP * 16;
+        exec += (long long)ntile[b] * 16 * NP;
+    }
+    s.Pb.nblk = nblk;
+    s.Pb.rbp = rbp;
+    s.Pb.nks = NP / 4;
+    s.Pb.row0 = dupload(c, row0);
+    s.Pb.nrows = dupload(c, nrows);
+    s.Pb.clo = dupload(c, clo);
+    s.Pb.ntile = dupload(c, ntile);
+    s.Pb.off = dupload(c, off);
+    s.wp_elems = std::max<long long>(o, 1);
+    s.wp_exec = exec;
+    const int nsl = 2 * c->nsnr;
+    s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
+    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl);
+    DSCE_HIP_CHECK(hipStreamSynchronize(c->stream));
+    DSCE_HIP_CHECK(hipGetLastError());
+}
+
 // ---------------------------------------------------------------------------
 void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
     hipStream_t st = c->stream;
@@ -471,7 +525,8 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
     if (s.W) {                     // rebuild (e.g. new SNR list): back to the structural band
         free_alloc(c, s.W);
         free_alloc(c, s.Wd);
-        s.W = s.Wd = nullptr;
+        if (s.Wp) free_alloc(c, s.Wp);
+        s.W = s.Wd = s.Wp = nullptr;
         s.wband = s.wband_struct;
         s.w_elems = s.wband.elems;
         s.Wb = upload_band(c, s.wband, false);
@@ -566,6 +621,7 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         DSCE_HIP_CHECK(hipStreamSynchronize(st));
         DSCE_HIP_CHECK(hipGetLastError());
         trim_w_band(c, s, tmp);
+        build_wpair(c, s);
     } catch (...) {
         for (void* p : tmp) (void)hipFree(p);
         throw;
@@ -650,6 +706,10 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
     }
     (void)valid;
     const int chunk = snr_chunk(c);
+    {
+        const char* e = getenv("DSCE_STREAMS");
+        c->streams2 = !(e && atoi(e) == 1);
+    }
     for (size_t si = 0; si < c->schemes.size(); ++si) {
         Scheme& s = *c->schemes[si];
         MmseK mm{};
@@ -658,10 +718,14 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.w_elems = s.w_elems;
         mm.nsnr = c->nsnr;
         mm.Wb = s.Wb;
+        mm.Wp = s.Wp;
+        mm.wp_elems = s.wp_elems;
+        mm.Pb = s.Pb;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
         }
+        const bool pfuse = perfect_fusable(s.k);
         for (int s0 = 0; s0 < c->nsnr; s0 += chunk) {
             b.snr0 = s0;
             b.U = R * std::min(chunk, c->nsnr - s0);
@@ -675,27 +739,46 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
                 copy_col(c, tr->y, b.y, s.LK, b.U, tunit);
                 copy_col(c, tr->h, b.h, s.LK, R, tr->lane);
             }
+            // With the perfect-CSI branch fused into perfect_ic, the IC iterations
+            // are two independent chains after stage 0: MMSE (k_wcontract ->
+            // stage, MFMA-bound) on the main stream and perfect CSI (perfect_ic,
+            // HBM-bound) on stream2, overlapping; joined before the next chunk.
+            const bool two = pfuse && c->streams2;
             for (int it = 0; it <= c->niter; ++it) {
+                if (it == 1 && two) {
+                    DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
+                    DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+                    for (int jt = 1; jt <= c->niter; ++jt) {
+                        Timed t(c, "perfect_ic", c->stream2);
+                        PerfectDetectArgs pd{c->d_counters, (int)si, jt, c->niter + 1, c->nsnr, jt == c->niter,
+                                             s.k.slI, s.k.slQ};
+                        launch_perfect_ic(c->stream2, s.k, c->ch, b, &pd);
+                    }
+                    DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
+                }
                 if (it > 0) {
                     {
                         Timed t(c, "k_wcontract");
                         launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
                     }
-                    {
+                    if (!two) {
                         Timed t(c, "perfect_ic");
-                        launch_perfect_ic(c->stream, s.k, c->ch, b);
+                        PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
+                                             s.k.slI, s.k.slQ};
+                        launch_perfect_ic(c->stream, s.k, c->ch, b, pfuse ? &pd : nullptr);
                     }
                 }
                 {
                     Timed t(c, "k_stage");
                     launch_stage(c->stream, s.k, mm, it, var_of_stage(it, c->niter), c->niter, it == c->niter, b,
-                                 c->d_counters, (int)si, tracing);
+                                 c->d_counters, (int)si, tracing, !(pfuse && it > 0));
                 }
                 if (tracing) {
                     copy_col(c, tr->hp + (size_t)2 * it * s.d.n_pilots, b.hp, s.d.n_pilots, b.U, tunit);
                     copy_col(c, tr->hest + (size_t)2 * it * s.LK, b.hest, s.LK, b.U, tunit);
                 }
             }
+            if (two && c->niter > 0) DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
         }
     }
     DSCE_HIP_CHECK(hipGetLastError());
@@ -737,6 +820,9 @@ int dsce_create(int hip_device, dsce_ctx** out) {
     try {
         DSCE_HIP_CHECK(hipSetDevice(hip_device));
         DSCE_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        DSCE_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+        DSCE_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+        DSCE_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     } catch (const std::exception& e) {
         delete ctx;
         return DSCE_EHIP;
@@ -757,6 +843,9 @@ void dsce_destroy(dsce_ctx* ctx) {
     }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     delete ctx;
 }
 

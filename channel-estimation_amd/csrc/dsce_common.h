@@ -92,6 +92,20 @@ struct Band {
     const double2* vals;
 };
 
+// The MMSE estimator W as pair tiles for k_wpair: per block the (row, column)
+// pairs q = c_local * rbp + r (r fastest, rbp = 24 or 32 rows) in tiles of 16,
+// each tile stored as [k-step][4 pilots][16 pairs] (one MFMA A operand per
+// k-step, one 16-byte load per lane).  Element of (pair q, pilot p):
+// vals[off + ((q/16) * nks + p/4) * 64 + (p%4) * 16 + q%16].
+struct PairBand {
+    int nblk, rbp, nks;
+    const int* row0;
+    const int* nrows;
+    const int* clo;               // first column of the block
+    const int* ntile;             // pair tiles (a multiple of 3 for rbp 24, of 2 for rbp 32)
+    const long long* off;
+};
+
 // ---------------------------------------------------------------------------
 // Scheme operators as seen by the Monte-Carlo kernels (all device pointers).
 // ---------------------------------------------------------------------------
@@ -100,13 +114,14 @@ struct SchemeK {
     double inv_sqrt_kappa, data_div;
     const int* pilot_pos;
     const int* data_pos;
-    const uint8_t* considered;
+    const int* considered;        // ND no-edge flags (int: uniform reads are scalar loads)
     const double2* symbols;       // M, sorted by bit label
     // nearest-neighbour slicer on the constellation grid
     int nI, nQ;
     const double* lvI;            // nI ascending real levels
     const double* lvQ;            // nQ ascending imag levels (nQ = 1, {0} for PAM)
     const int* grid_sym;          // nI * nQ -> symbol index
+    double slI, slQ;              // 1 / level step (1 for a single level)
     // precoder P (LK x Nsym) and P^H (Nsym x LK), CSR
     const int* p_ptr;
     const int* p_col;
@@ -128,6 +143,7 @@ struct SchemeK {
     // per row and every data entry sits on its own row (p_diag, e.g. OFDM), the
     // entry's column (-1: none) and value, so re-precoding is row-local
     const int* row_data;          // LK
+    const int* row_cons;          // LK: 1 if the row carries a considered (no-edge) data symbol
     const int* row_pcol;          // LK
     const double2* row_pval;      // LK
     int p_diag;

@@ -40,6 +40,9 @@ struct MmseK {
     long long w_elems;
     int nsnr;
     Band Wb;              // block geometry (vals unused; per-(var,snr) base added)
+    const double2* Wp;    // [var][snr][wp_elems] pair-tile layout (k_wpair), or null
+    long long wp_elems;
+    PairBand Pb;
 };
 
 // Monte-Carlo pipeline
@@ -49,9 +52,18 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
                      uint64_t rep0, McBuffers& b);
 void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace);
+                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace, bool perfect);
+// true when launch_stage uses the fused select-mode pass and the precoder is
+// row-local, so the perfect-CSI branch of IC iterations can ride on perfect_ic
+bool perfect_fusable(const SchemeK& sk);
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
-void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b);
+// Perfect-CSI detection fused into the perfect IC pass (select mode, row-local P)
+struct PerfectDetectArgs {
+    unsigned long long* counters;
+    int scheme, stage, nstage, nsnr, last;
+    double sI, sQ;   // 1 / slicer step (I, Q)
+};
+void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)
@@ -78,6 +90,8 @@ void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const
 void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv);
 void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
                 const int* q_start, int QL, double2* rd /* packed, w_elems */);
+void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
+                 double2* wp, long long wp_elems, int nslices);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);
 void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
              const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);

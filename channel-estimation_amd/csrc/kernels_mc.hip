@@ -15,6 +15,7 @@
 #include "dsce_kernels.h"
 
 #include <math.h>
+#include <type_traits>
 #include <stdlib.h>
 #include <string.h>
 
@@ -30,6 +31,76 @@ __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
+}
+
+// Slicer tables staged in LDS (levels and the level-grid -> symbol map are
+// gathered per lane; from global memory these gathers were the stage's latency
+// chain).  The cell index comes from a multiply by 1/step: an index off by one
+// can only occur when x sits (to rounding) on a level, where both candidate
+// pairs resolve to that level; ties (mid-points) keep the first-minimum rule.
+struct SlicerLds {
+    double lvI[16], lvQ[16];
+    int grid[256];
+};
+
+__device__ __forceinline__ void slicer_load(SlicerLds& t, const SchemeK& sk, int tid, int nthreads) {
+    for (int i = tid; i < sk.nI; i += nthreads) t.lvI[i] = sk.lvI[i];
+    for (int i = tid; i < sk.nQ; i += nthreads) t.lvQ[i] = sk.lvQ[i];
+    for (int i = tid; i < sk.nI * sk.nQ; i += nthreads) t.grid[i] = sk.grid_sym[i];
+}
+
+// Constellation + slicer tables into LDS with every global load issued before
+// the first LDS write (one memory round trip, not one per table).  NTH threads.
+template <int NTH>
+__device__ __forceinline__ void stage_tables(double2* sym, SlicerLds& t, const SchemeK& sk, int tid) {
+    constexpr int PER = 256 / NTH;                      // entries of the 256-slot tables per thread
+    double2 sv[PER];
+    int gv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = tid + k * NTH;
+        sv[k] = i < sk.M ? sk.symbols[i] : make_double2(0.0, 0.0);
+        gv[k] = i < sk.nI * sk.nQ ? sk.grid_sym[i] : 0;
+    }
+    const double li = tid < sk.nI && tid < 16 ? sk.lvI[tid] : 0.0;
+    const double lq = tid < sk.nQ && tid < 16 ? sk.lvQ[tid] : 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        sym[tid + k * NTH] = sv[k];
+        t.grid[tid + k * NTH] = gv[k];
+    }
+    if (tid < 16) {
+        t.lvI[tid] = li;
+        t.lvQ[tid] = lq;
+    }
+}
+
+__device__ __forceinline__ int nearest_level_fast(const double* lv, int n, double x, double istep, int& alt) {
+    alt = -1;
+    if (n == 1) return 0;
+    int i = (int)floor((x - lv[0]) * istep);
+    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i + 1]);
+    if (d1 < d0) return i + 1;
+    if (d1 == d0) alt = i + 1;
+    return i;
+}
+
+__device__ __forceinline__ int slice_fast(const SlicerLds& t, int nI, int nQ, double2 z, double sI, double sQ) {
+    int aI, aQ;
+    const int iI = nearest_level_fast(t.lvI, nI, z.x, sI, aI);
+    const int iQ = nearest_level_fast(t.lvQ, nQ, z.y, sQ, aQ);
+    int best = t.grid[iI * nQ + iQ];
+    if (aI >= 0) best = min(best, t.grid[aI * nQ + iQ]);
+    if (aQ >= 0) best = min(best, t.grid[iI * nQ + aQ]);
+    if (aI >= 0 && aQ >= 0) best = min(best, t.grid[aI * nQ + aQ]);
+    return best;
+}
+
+// a / b with one division (rounding-level differences to c_div)
+__device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
+    const double id = 1.0 / (b.x * b.x + b.y * b.y);
+    return make_double2((a.x * b.x + a.y * b.y) * id, (a.y * b.x - a.x * b.y) * id);
 }
 
 // ---------------------------------------------------------------------------
@@ -112,53 +183,126 @@ void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep
 
 // ---------------------------------------------------------------------------
 // generic banded block matvec: out[row][lane] = sum_k A[row, k] * in(k, lane)
-// grid (lanes/64, nblk), block 64.  A's values are wave-uniform (scalar loads).
+// block 64, 1-D grid of (lanes/64) x nblk blocks.  A's values are wave-uniform
+// (scalar loads).  Work order (BandOrder): unit group fastest, or — for passes
+// that read per-realisation data shared by the SNR points (the channel taps) —
+// SNR point fastest, then row block, then realisation group, each XCD (block b
+// runs on XCD b % 8) walking a contiguous range so the reuse stays in one L2.
 // ---------------------------------------------------------------------------
+struct BandOrder {
+    int nug;       // unit groups of 64 lanes
+    int nchunk;    // SNR points per unit range (units = snr * R + rep)
+    int rgs;       // R / 64
+    int xcd;       // 1: SNR-fastest XCD-aware order
+};
+
+__device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug, int& blk) {
+    int L = blockIdx.x;
+    if (o.xcd) {
+        L = (L & 7) * (gridDim.x >> 3) + (L >> 3);
+        const int sn = L % o.nchunk, rest = L / o.nchunk;
+        blk = rest % nblk;
+        ug = sn * o.rgs + rest / nblk;
+    } else {
+        ug = L % o.nug;
+        blk = L / o.nug;
+    }
+}
+
 template <class In, class Out>
-__global__ void __launch_bounds__(64) k_band(Band A, In in, Out out) {
-    const int lane = blockIdx.x * WAVE + threadIdx.x;
-    const int blk = blockIdx.y;
+__global__ void __launch_bounds__(64) k_band(Band A, BandOrder ord, In in, Out out) {
+    extern __shared__ double2 band_lds[];
+    int ug, blk;
+    band_block(ord, A.nblk, ug, blk);
+    const int lane = ug * WAVE + threadIdx.x;
+    Out o = out;
+    o.prepare(band_lds);
     const int row0 = A.row0[blk], nrows = A.nrows[blk], klo = A.klo[blk], khi = A.khi[blk];
     const double2* __restrict__ a = A.vals + A.off[blk];
     double2 acc[DSCE_RB];
 #pragma unroll
     for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
+    // operands of column k+1 requested before column k's row updates (latency hiding)
+    typename In::Regs ld = in.load(klo < khi ? klo : 0, lane);
     for (int k = klo; k < khi; ++k) {
-        const double2 x = in(k, lane);
+        const typename In::Regs ldn = in.load(k + 1 < khi ? k + 1 : k, lane);
+        // keep the scheduler from pulling column k+1's uses up to its loads
+        __builtin_amdgcn_sched_barrier(0);
+        const double2 x = in.combine(ld);
         const double2* __restrict__ ak = a + (size_t)(k - klo) * DSCE_RB;
 #pragma unroll
         for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], ak[r], x);
+        ld = ldn;
     }
 #pragma unroll
     for (int r = 0; r < DSCE_RB; ++r)
-        if (r < nrows) out(row0 + r, lane, acc[r]);
+        if (r < nrows) o(row0 + r, lane, acc[r]);
+    o.finish(lane);
+}
+
+template <class In, class Out>
+void launch_band(hipStream_t s, const Band& A, int lanes, const BandOrder* ord, const In& in, const Out& out,
+                 size_t lds = 0) {
+    BandOrder o{lanes / WAVE, 1, 1, 0};
+    if (ord && ((size_t)o.nug * A.nblk) % 8 == 0) o = *ord;
+    hipLaunchKernelGGL((k_band<In, Out>), dim3((lanes / WAVE) * A.nblk), dim3(WAVE), lds, s, A, o, in, out);
 }
 
 struct LoadSoA {
     const double2* __restrict__ p;
     int stride;
-    __device__ __forceinline__ double2 operator()(int k, int lane) const { return p[(size_t)k * stride + lane]; }
+    typedef double2 Regs;
+    __device__ __forceinline__ Regs load(int k, int lane) const { return p[(size_t)k * stride + lane]; }
+    __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
 };
 struct StoreSoA {
     double2* __restrict__ p;
     int stride;
+    __device__ __forceinline__ void prepare(double2*) {}
+    __device__ __forceinline__ void finish(int) {}
     __device__ __forceinline__ void operator()(int row, int lane, double2 v) const {
         p[(size_t)row * stride + lane] = v;
     }
 };
-// (H t)[n] = sum_tau IR[tau][n] t[n - d_tau]  (GetConvolutionMatrix, FastFading.m:284)
+// (H t)[n] = sum_tau IR[tau][n] t[n - d_tau]  (GetConvolutionMatrix, FastFading.m:284).
+// NT > 0: exactly NT taps, unrolled so all 2*NT loads of a column are in flight
+// together (load) before the taps are combined; NT == 0: any tap count, loop.
+template <int NT>
 struct LoadChannelApplied {
+    static constexpr int NTS = NT > 0 ? NT : 1;
     const double2* __restrict__ t;     // [N][U]
     const double2* __restrict__ ir;    // [ntap][N][R]
     int U, R, N, ntap;
-    int delay[8];
-    __device__ __forceinline__ double2 operator()(int n, int lane) const {
+    int delay[NT > 0 ? NT : DSCE_MAX_TAPS];
+    struct Regs {
+        double2 a[NTS], b[NTS];
+    };
+    __device__ __forceinline__ Regs load(int n, int lane) const {
+        Regs g;
         const int rep = lane % R;
-        double2 acc = make_double2(0.0, 0.0);
-        for (int q = 0; q < ntap; ++q) {
-            const int m = n - delay[q];
-            if (m >= 0) c_fma(acc, ir[((size_t)q * N + n) * R + rep], t[(size_t)m * U + lane]);
+        if (NT > 0) {
+#pragma unroll
+            for (int q = 0; q < NTS; ++q) {
+                const int m = n - delay[q];
+                g.a[q] = ir[((size_t)q * N + n) * R + rep];
+                g.b[q] = t[(size_t)(m > 0 ? m : 0) * U + lane];
+                if (m < 0) g.b[q] = make_double2(0.0, 0.0);
+            }
+        } else {
+            double2 acc = make_double2(0.0, 0.0);
+            for (int q = 0; q < ntap; ++q) {
+                const int m = n - delay[q];
+                if (m >= 0) c_fma(acc, ir[((size_t)q * N + n) * R + rep], t[(size_t)m * U + lane]);
+            }
+            g.a[0] = acc;
         }
+        return g;
+    }
+    __device__ __forceinline__ double2 combine(const Regs& g) const {
+        if (NT == 0) return g.a[0];
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int q = 0; q < NTS; ++q) c_fma(acc, g.a[q], g.b[q]);
         return acc;
     }
 };
@@ -169,12 +313,100 @@ struct StorePerfectIC {
     const double2* __restrict__ h;     // [LK][R]
     const double2* __restrict__ u;     // [LK][U]
     int U, R;
+    __device__ __forceinline__ void prepare(double2*) {}
+    __device__ __forceinline__ void finish(int) {}
     __device__ __forceinline__ void operator()(int row, int lane, double2 acc) const {
         const size_t i = (size_t)row * U + lane;
         const double2 hv = h[(size_t)row * R + lane % R];
         double2 r = c_sub(y[i], acc);
         r = c_add(r, c_mul(hv, u[i]));
         yperf[i] = r;
+    }
+};
+
+// Perfect-CSI branch of an IC iteration fused into the second pass (select-mode
+// schemes whose precoder is row-local, e.g. OFDM): y_perf of the row is formed
+// in registers, equalised by the true diag(D), sliced and counted (script:548-561)
+// and — unless this is the last iteration — replaced in place by the
+// re-precoded decision u = P [xP; Q(x_perf)] (script:541-543).  Pilot rows of u
+// are constant (P xP) and are left untouched.  LDS: constellation + slicer.
+struct StorePerfectDetect {
+    const double2* __restrict__ y;
+    const double2* __restrict__ h;     // [LK][R]
+    double2* __restrict__ u;           // [LK][U], in/out
+    const uint16_t* __restrict__ sidx; // [ND][R]
+    const int* __restrict__ row_data;
+    const int* __restrict__ row_cons;
+    const double2* __restrict__ row_pval;
+    const double2* __restrict__ symbols;
+    const double* __restrict__ lvI;
+    const double* __restrict__ lvQ;
+    const int* __restrict__ grid_sym;
+    unsigned long long* __restrict__ counters;
+    size_t cidx0;                      // counter index of (scheme, csi=1, edge=0, snr=0, stage)
+    int cstride_edge, cstride_snr;
+    int U, R, snr0, last, M, nI, nQ, real_detect;
+    double idd, sI, sQ;
+    double2* sym;
+    SlicerLds* slt;
+    int c0, c1;
+    __device__ __forceinline__ void prepare(double2* lds) {
+        sym = lds;
+        slt = (SlicerLds*)(lds + 256);
+        constexpr int PER = 256 / WAVE;
+        double2 sv[PER];
+        int gv[PER];
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = tid + k * WAVE;
+            sv[k] = i < M ? symbols[i] : make_double2(0.0, 0.0);
+            gv[k] = i < nI * nQ ? grid_sym[i] : 0;
+        }
+        const double li = tid < nI && tid < 16 ? lvI[tid] : 0.0;
+        const double lq = tid < nQ && tid < 16 ? lvQ[tid] : 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            sym[tid + k * WAVE] = sv[k];
+            slt->grid[tid + k * WAVE] = gv[k];
+        }
+        if (tid < 16) {
+            slt->lvI[tid] = li;
+            slt->lvQ[tid] = lq;
+        }
+        __syncthreads();
+        c0 = 0;
+        c1 = 0;
+    }
+    __device__ __forceinline__ void operator()(int row, int lane, double2 acc) {
+        const size_t i = (size_t)row * U + lane;
+        const int rl = lane % R;
+        const double2 hv = h[(size_t)row * R + rl];
+        const int d = row_data[row];
+        if (d < 0) return;
+        const double2 uv = u[i];
+        double2 r = c_sub(y[i], acc);
+        r = c_add(r, c_mul(hv, uv));
+        const double2 z = c_div1(r, hv);
+        const int dp = slice_fast(*slt, nI, nQ, real_detect ? make_double2(z.x * idd, 0.0)
+                                                            : make_double2(z.x * idd, z.y * idd), sI, sQ);
+        const int ne = __popc((unsigned)(dp ^ (int)sidx[(size_t)d * R + rl]));
+        c0 += ne;
+        c1 += row_cons[row] ? ne : 0;
+        if (!last) {
+            double2 av = make_double2(0.0, 0.0);
+            c_fma(av, row_pval[row], sym[dp]);
+            u[i] = av;
+        }
+    }
+    __device__ __forceinline__ void finish(int lane) {
+        const int t0 = wave_sum(c0), t1 = wave_sum(c1);
+        if (threadIdx.x == 0) {
+            const int snr = snr0 + (lane - (int)threadIdx.x) / R;
+            const size_t i0 = cidx0 + (size_t)snr * cstride_snr;
+            if (t0) atomicAdd(&counters[i0], (unsigned long long)t0);
+            if (t1) atomicAdd(&counters[i0 + cstride_edge], (unsigned long long)t1);
+        }
     }
 };
 
@@ -264,8 +496,7 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
     hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
                        b.xp, b.sidx, b.xs);
     // s = G x (script:376-378)
-    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(R / WAVE, sk.G.nblk), dim3(WAVE), 0, s, sk.G,
-                       LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
+    launch_band(s, sk.G, R, nullptr, LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
     hipLaunchKernelGGL(k_channel_apply, dim3(R / WAVE, (ch.N + 63) / 64), dim3(WAVE), 0, s, ch, R, b.ir, b.ss, b.r0);
     hipLaunchKernelGGL(k_hdiag, dim3(R / WAVE, (sk.LK + 15) / 16), dim3(WAVE), 0, s, sk, ch, R, b.ir, b.h);
 }
@@ -297,21 +528,76 @@ void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const
     hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)
-    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(b.U / WAVE, sk.QH.nblk), dim3(WAVE), 0, s, sk.QH,
-                       LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});
+    launch_band(s, sk.QH, b.U, nullptr, LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});
 }
 
 // ---------------------------------------------------------------------------
 // perfect-CSI interference cancellation product (D - diag h) u = Q'(H(G u)) - h.*u
 // (script:541-543), two banded passes.
 // ---------------------------------------------------------------------------
-void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b) {
-    hipLaunchKernelGGL((k_band<LoadSoA, StoreSoA>), dim3(b.U / WAVE, sk.G.nblk), dim3(WAVE), 0, s, sk.G,
-                       LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
-    LoadChannelApplied in{b.t, b.ir, b.U, b.R, ch.N, ch.ntap, {0}};
-    for (int q = 0; q < ch.ntap && q < 8; ++q) in.delay[q] = ch.tap_delay[q];
-    hipLaunchKernelGGL((k_band<LoadChannelApplied, StorePerfectIC>), dim3(b.U / WAVE, sk.QH.nblk), dim3(WAVE), 0, s,
-                       sk.QH, in, StorePerfectIC{b.yperf, b.y, b.h, b.u, b.U, b.R});
+template <int NT, class Out>
+static void launch_pass2(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
+                         const Out& o, size_t lds) {
+    LoadChannelApplied<NT> in{};
+    in.t = b.t;
+    in.ir = b.ir;
+    in.U = b.U;
+    in.R = b.R;
+    in.N = ch.N;
+    in.ntap = ch.ntap;
+    for (int q = 0; q < ch.ntap && q < (NT > 0 ? NT : DSCE_MAX_TAPS); ++q) in.delay[q] = ch.tap_delay[q];
+    launch_band(s, sk.QH, b.U, &ord, in, o, lds);
+}
+
+template <class Out>
+static void launch_pass2_nt(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
+                            const Out& o, size_t lds = 0) {
+    switch (ch.ntap) {
+        case 1: launch_pass2<1>(s, sk, ch, b, ord, o, lds); break;
+        case 2: launch_pass2<2>(s, sk, ch, b, ord, o, lds); break;
+        case 3: launch_pass2<3>(s, sk, ch, b, ord, o, lds); break;
+        case 4: launch_pass2<4>(s, sk, ch, b, ord, o, lds); break;
+        default: launch_pass2<0>(s, sk, ch, b, ord, o, lds); break;
+    }
+}
+
+void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd) {
+    launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
+    // SNR-fastest XCD-aware order: the SNR units of a realisation share its taps
+    const char* xe = getenv("DSCE_XCD");
+    const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, (!xe || xe[0] != '0') ? 1 : 0};
+    if (!pd) {
+        launch_pass2_nt(s, sk, ch, b, ord, StorePerfectIC{b.yperf, b.y, b.h, b.u, b.U, b.R});
+        return;
+    }
+    StorePerfectDetect o{};
+    o.y = b.y;
+    o.h = b.h;
+    o.u = b.u;
+    o.sidx = b.sidx;
+    o.row_data = sk.row_data;
+    o.row_cons = sk.row_cons;
+    o.row_pval = sk.row_pval;
+    o.symbols = sk.symbols;
+    o.lvI = sk.lvI;
+    o.lvQ = sk.lvQ;
+    o.grid_sym = sk.grid_sym;
+    o.counters = pd->counters;
+    o.cidx0 = ((((size_t)pd->scheme * 2 + 1) * 2 + 0) * pd->nsnr) * pd->nstage + pd->stage;
+    o.cstride_edge = pd->nsnr * pd->nstage;
+    o.cstride_snr = pd->nstage;
+    o.U = b.U;
+    o.R = b.R;
+    o.snr0 = b.snr0;
+    o.last = pd->last;
+    o.M = sk.M;
+    o.nI = sk.nI;
+    o.nQ = sk.nQ;
+    o.real_detect = sk.real_detect;
+    o.idd = 1.0 / sk.data_div;
+    o.sI = pd->sI;
+    o.sQ = pd->sQ;
+    launch_pass2_nt(s, sk, ch, b, ord, o, 256 * sizeof(double2) + sizeof(SlicerLds));
 }
 
 // ---------------------------------------------------------------------------
@@ -453,9 +739,149 @@ __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* _
     }
 }
 
+// k_wpair: the same contraction regrouped so no MFMA row is padding.  With
+// D_hat[r,c] = sum_p W[(r,c),p] hP_p,  y_est[r] = y[r] - sum_c D_hat[r,c] v_c.
+// The first product is a GEMM with M = (row, column) pairs of the block (q = c*RBP
+// + r; 24 x 24 pairs of an OFDM symbol tile exactly into 16-pair tiles), K = NP
+// and N = units, B = hP constant for the whole block (loaded once); the second
+// is applied in the MFMA epilogue: D row (lane>>4)+4*reg of tile t is pair
+// 16t + g + 4 reg, whose row index is g (mod 4) for every tile, so each lane
+// accumulates RBP/4 rows of its unit with no cross-lane traffic.  Tiles come in
+// periods (RBP 24: 3 tiles = 2 columns, RBP 32: 2 tiles = 1 column) so pair ->
+// (column, row) is compile-time.  Wave = 16 units, block = 4 waves = 64 units of
+// one SNR point; grid (U/64, nblk).
+template <int RBP, int NKS, bool PF>
+__global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __restrict__ Wall, long long wp_elems,
+                                               int var, int nsnr, int snr0, int R, int U,
+                                               const double2* __restrict__ hp, const double2* __restrict__ v,
+                                               const double2* __restrict__ y, double2* __restrict__ yest) {
+    constexpr int PER = RBP == 24 ? 3 : 2;           // tiles per period
+    constexpr int CPP = RBP == 24 ? 2 : 1;           // columns per period
+    constexpr int NACC = RBP / 4;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int unit = blockIdx.x * 64 + wv * 16 + j;
+    const int snr = snr0 + (blockIdx.x * 64) / R;
+    const int blk = blockIdx.y;
+    double2 hb[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) hb[ks] = hp[(size_t)(4 * ks + g) * U + unit];
+    const int clo = P.clo[blk], ntile = P.ntile[blk];
+    const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)wp_elems + P.off[blk] + lane;
+    double2 acc[NACC];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) acc[k] = make_double2(0.0, 0.0);
+    const double2* __restrict__ vb = v + (size_t)clo * U + unit;
+    // one 16-pair tile: 4*NKS MFMAs, then the v epilogue of its 4 D rows (tile tt
+    // of a period; which column / accumulator each row feeds is compile-time)
+    auto tile = [&](const double2 (&aa)[NKS], const double2 (&vvv)[CPP], auto ttc) {
+        constexpr int tt = decltype(ttc)::value;
+        d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            re = MFMA64(aa[ks].x, hb[ks].x, re);
+            im = MFMA64(aa[ks].x, hb[ks].y, im);
+            re = MFMA64(-aa[ks].y, hb[ks].y, re);
+            im = MFMA64(aa[ks].y, hb[ks].x, im);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int q0 = 16 * tt + 4 * i;                // pair offset in the period, less g
+            const int cc = q0 / RBP, rho = (q0 % RBP) / 4;
+            c_fma(acc[rho], make_double2(re[i], im[i]), vvv[cc]);
+        }
+    };
+    auto ldt = [&](int t, double2 (&aa)[NKS]) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) aa[ks] = w[((size_t)t * NKS + ks) * 64];
+    };
+    auto ldv = [&](int t0, double2 (&vvv)[CPP]) {
+#pragma unroll
+        for (int cc = 0; cc < CPP; ++cc) vvv[cc] = vb[(size_t)((t0 / PER) * CPP + cc) * U];
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    double2 A0[NKS], A1[NKS], vv[CPP];
+    if (PF) {
+        // tile-level ping-pong: tile t+1's W loads are in flight during tile t's MFMAs
+        if (ntile > 0) ldt(0, A0);
+        for (int t0 = 0; t0 < ntile; t0 += PER) {
+            ldv(t0, vv);
+            const int tn = t0 + PER < ntile ? t0 + PER : t0;          // clamp: harmless reload at the end
+            if (PER == 3) {
+                // period of 3 tiles: A0 A1 A0, and the next period's first tile lands in A1 ->
+                // swap roles by reloading it into A0 after the last tile (one register copy)
+                ldt(t0 + 1, A1);
+                tile(A0, vv, I0{});
+                ldt(t0 + 2, A0);
+                tile(A1, vv, I1{});
+                ldt(tn, A1);
+                tile(A0, vv, I2{});
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) A0[ks] = A1[ks];
+            } else {
+                ldt(t0 + 1, A1);
+                tile(A0, vv, I0{});
+                ldt(tn, A0);
+                tile(A1, vv, I1{});
+            }
+        }
+    } else {
+        for (int t0 = 0; t0 < ntile; t0 += PER) {
+            ldv(t0, vv);
+            ldt(t0, A0);
+            tile(A0, vv, I0{});
+            ldt(t0 + 1, A1);
+            tile(A1, vv, I1{});
+            if (PER == 3) {
+                ldt(t0 + 2, A0);
+                tile(A0, vv, I2{});
+            }
+        }
+    }
+    const int row0 = P.row0[blk], nrows = P.nrows[blk];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+        const int r = g + 4 * k;
+        if (r < nrows) {
+            const size_t i = (size_t)(row0 + r) * U + unit;
+            yest[i] = c_sub(y[i], acc[k]);
+        }
+    }
+}
+
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
-    // DSCE_WCONTRACT = mfma (default) | valu — read per launch for in-process A/B.
+    // DSCE_WCONTRACT = pair (default) | mfma (32-row tiles) | valu — read per launch for A/B.
     const char* mode = getenv("DSCE_WCONTRACT");
+    const bool pair_ok = mm.Wp && (b.U % 64) == 0 && (b.R % 64) == 0 && !(mode && mode[0] != 'p');
+    if (pair_ok) {
+        const dim3 grid(b.U / 64, mm.Pb.nblk);
+        const char* pfe = getenv("DSCE_WPAIR_PF");
+        const bool pf = !(pfe && pfe[0] == '0');
+#define LAUNCH_WP(RBPV, NKSV)                                                                                    \
+    {                                                                                                            \
+        if (pf)                                                                                                  \
+            hipLaunchKernelGGL((k_wpair<RBPV, NKSV, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var,  \
+                               mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                               \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_wpair<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var, \
+                               mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                               \
+    }
+        if (mm.Pb.rbp == 24) {
+            if (mm.Pb.nks == 2) LAUNCH_WP(24, 2)
+            else if (mm.Pb.nks == 4) LAUNCH_WP(24, 4)
+            else LAUNCH_WP(24, 8)
+        } else {
+            if (mm.Pb.nks == 2) LAUNCH_WP(32, 2)
+            else if (mm.Pb.nks == 4) LAUNCH_WP(32, 4)
+            else LAUNCH_WP(32, 8)
+        }
+#undef LAUNCH_WP
+        return;
+    }
     bool valu = (sk.NP % 8) != 0 || mm.Wb.rb != 32 || (b.U % 128) != 0 || (b.R % 32) != 0;
     if (mode && mode[0] == 'v') valu = true;
     if (valu) {
@@ -499,52 +925,8 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
     return best;
 }
 
-// Slicer tables staged in LDS (levels and the level-grid -> symbol map are
-// gathered per lane; from global memory these gathers were the stage's latency
-// chain).  The cell index comes from a multiply by 1/step: an index off by one
-// can only occur when x sits (to rounding) on a level, where both candidate
-// pairs resolve to that level; ties (mid-points) keep the first-minimum rule.
-struct SlicerLds {
-    double lvI[16], lvQ[16];
-    int grid[256];
-};
-
-__device__ __forceinline__ void slicer_load(SlicerLds& t, const SchemeK& sk, int tid, int nthreads) {
-    for (int i = tid; i < sk.nI; i += nthreads) t.lvI[i] = sk.lvI[i];
-    for (int i = tid; i < sk.nQ; i += nthreads) t.lvQ[i] = sk.lvQ[i];
-    for (int i = tid; i < sk.nI * sk.nQ; i += nthreads) t.grid[i] = sk.grid_sym[i];
-}
-
-__device__ __forceinline__ int nearest_level_fast(const double* lv, int n, double x, double istep, int& alt) {
-    alt = -1;
-    if (n == 1) return 0;
-    int i = (int)floor((x - lv[0]) * istep);
-    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
-    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i + 1]);
-    if (d1 < d0) return i + 1;
-    if (d1 == d0) alt = i + 1;
-    return i;
-}
-
-__device__ __forceinline__ int slice_fast(const SlicerLds& t, int nI, int nQ, double2 z, double sI, double sQ) {
-    int aI, aQ;
-    const int iI = nearest_level_fast(t.lvI, nI, z.x, sI, aI);
-    const int iQ = nearest_level_fast(t.lvQ, nQ, z.y, sQ, aQ);
-    int best = t.grid[iI * nQ + iQ];
-    if (aI >= 0) best = min(best, t.grid[aI * nQ + iQ]);
-    if (aQ >= 0) best = min(best, t.grid[iI * nQ + aQ]);
-    if (aI >= 0 && aQ >= 0) best = min(best, t.grid[aI * nQ + aQ]);
-    return best;
-}
-
-// a / b with one division (rounding-level differences to c_div)
-__device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
-    const double id = 1.0 / (b.x * b.x + b.y * b.y);
-    return make_double2((a.x * b.x + a.y * b.y) * id, (a.y * b.x - a.x * b.y) * id);
-}
-
 struct StageArgs {
-    int stage, var, nsnr, nstage, scheme, last, trace, R, U, snr0, xcd_order;
+    int stage, var, nsnr, nstage, scheme, last, trace, perfect, R, U, snr0, xcd_order;
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
 };
@@ -592,8 +974,7 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
     const bool lds_slicer = sk.nI <= 16 && sk.nQ <= 16;
     if (lds_slicer) slicer_load(slt, sk, threadIdx.x, WAVE);
     __syncthreads();
-    const double sI = 1.0 / (sk.nI > 1 ? sk.lvI[1] - sk.lvI[0] : 1.0);
-    const double sQ = 1.0 / (sk.nQ > 1 ? sk.lvQ[1] - sk.lvQ[0] : 1.0);
+    const double sI = sk.slI, sQ = sk.slQ;
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int snr = st.snr0 + (blockIdx.x * WAVE) / st.R;
     const int rl = unit % st.R;
@@ -690,7 +1071,7 @@ __global__ void __launch_bounds__(64) k_ls(SchemeK sk, StageArgs st, const doubl
 // decisions for k_precode.  diag(D_hat) is written only for traces; the
 // contraction uses a W band with a zero diagonal, so nothing else reads it.
 // Flat grid, row block fastest (the blocks of one unit group share hP in L2).
-template <int NPT, int RB>
+template <int NPT, int RB, bool PERF>
 __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, int nrb, const double2* __restrict__ Wd,
                                                      const double2* __restrict__ xp,
                                                      const uint16_t* __restrict__ sidx,
@@ -701,10 +1082,11 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                                                      unsigned long long* __restrict__ counters) {
     __shared__ double2 sym[256];
     __shared__ SlicerLds slt;
-    for (int i = threadIdx.x; i < sk.M; i += 256) sym[i] = sk.symbols[i];
-    slicer_load(slt, sk, threadIdx.x, 256);
-    __syncthreads();
-    // Work order: row block fastest, then SNR point, then 256-realisation group,
+    __shared__ double2 shp[NPT * 64];                      // the block's 64 units' LS pilot estimates
+    __shared__ double2 swd[4 * RB * NPT];                  // diag(W) rows of the block (broadcast reads)
+    // Block = 64 units x 4*RB rows (wave w: rows [4 RB blk + w RB, +RB)); the LS
+    // pilot estimates of the 64 units go through LDS once for the 4 waves.
+    // Work order: row block fastest, then SNR point, then 64-realisation group,
     // so the blocks sharing hP (same units) and h (same realisations) run close
     // together; with xcd_order each XCD (block b runs on XCD b % 8) walks its own
     // contiguous range of that order, keeping the reuse inside one L2.
@@ -713,83 +1095,138 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
     const int rbk = L % nrb;
     int ug = L / nrb;
     if (st.xcd_order) {
-        const int nchunk = st.U / st.R, rgs = st.R >> 8;
+        const int nchunk = st.U / st.R, rgs = st.R >> 6;
         ug = (ug % nchunk) * rgs + ug / nchunk;
     }
     // wave index made provably uniform so Wd / row tables become scalar loads
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int ubase = ug * 256 + wv * 64;
-    if (ubase >= st.U) return;
-    const int unit = ubase + lane;
-    const int snr = st.snr0 + ubase / st.R;
-    const int rl = unit % st.R;
     const int U = st.U, R = st.R;
-    const int r0 = rbk * RB;
-    const int nr = min(RB, sk.LK - r0);
-    const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * NPT + (size_t)r0 * NPT;
+    const int unit = ug * 64 + lane;
+    const int snr = st.snr0 + (ug * 64) / R;
+    const int rl = unit % R;
+    const int r0 = (rbk * 4 + wv) * RB;
+    const int nr = max(0, min(RB, sk.LK - r0));
+    // every per-row operand of the wave is requested up front (rows past the
+    // end / pilot rows read a valid dummy), so their latency overlaps diag(D_hat)
+    double2 ye[RB], yp[RB], hh[RB];
+    int tx[RB];
+    const bool same_y = st.ysrc_p == st.ysrc_e;
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int row = r < nr ? r0 + r : 0;
+        const int i = sk.row_data[row];
+        const size_t ix = (size_t)row * U + unit;
+        ye[r] = st.ysrc_e[ix];
+        tx[r] = sidx[(size_t)(i > 0 ? i : 0) * R + rl];
+        if (PERF) {
+            yp[r] = same_y ? ye[r] : st.ysrc_p[ix];
+            hh[r] = h[(size_t)row * R + rl];
+        }
+    }
+    // per-row scalars of the wave's rows, requested together (no dependent chains)
+    int rdat[RB], rcons[RB], rpcol[RB];
+    double2 rpval[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int row = r < nr ? r0 + r : 0;
+        rdat[r] = sk.row_data[row];
+        rcons[r] = sk.row_cons[row];
+        rpcol[r] = sk.row_pcol[row];
+        rpval[r] = sk.row_pval[row];
+    }
+    {
+        // LDS staging: hP of the 64 units, diag(W) rows of the block, tables;
+        // every global load is issued before the first LDS write
+        constexpr int NW = (4 * RB * NPT + 255) / 256;
+        double2 hv[NPT / 4], wv_[NW];
+#pragma unroll
+        for (int k = 0; k < NPT / 4; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            hv[k] = hp[(size_t)(i >> 6) * U + ug * 64 + (i & 63)];
+        }
+        const int rb0 = rbk * 4 * RB;
+        const double2* __restrict__ wdb = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * NPT;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const int i = threadIdx.x + 256 * k;
+            const int row = rb0 + i / NPT;
+            wv_[k] = (i < 4 * RB * NPT && row < sk.LK) ? wdb[(size_t)rb0 * NPT + i] : make_double2(0.0, 0.0);
+        }
+        stage_tables<256>(sym, slt, sk, threadIdx.x);
+#pragma unroll
+        for (int k = 0; k < NPT / 4; ++k) shp[threadIdx.x + 256 * k] = hv[k];
+#pragma unroll
+        for (int k = 0; k < NW; ++k)
+            if (threadIdx.x + 256 * k < 4 * RB * NPT) swd[threadIdx.x + 256 * k] = wv_[k];
+    }
+    __syncthreads();
+    if (nr == 0) return;
+    const double2* __restrict__ wds = swd + wv * RB * NPT;
     double2 acc[RB];
 #pragma unroll
     for (int r = 0; r < RB; ++r) acc[r] = make_double2(0.0, 0.0);
 #pragma unroll
     for (int p = 0; p < NPT; ++p) {
-        const double2 hv = hp[(size_t)p * U + unit];
+        const double2 hv = shp[p * 64 + lane];
 #pragma unroll
         for (int r = 0; r < RB; ++r)
-            if (r < nr) c_fma(acc[r], wd[r * NPT + p], hv);
+            if (r < nr) c_fma(acc[r], wds[r * NPT + p], hv);
     }
     const double idd = 1.0 / sk.data_div;
-    const double sI = 1.0 / (sk.nI > 1 ? sk.lvI[1] - sk.lvI[0] : 1.0);
-    const double sQ = 1.0 / (sk.nQ > 1 ? sk.lvQ[1] - sk.lvQ[0] : 1.0);
+    const double sI = sk.slI, sQ = sk.slQ;
     int cnt[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
         if (r < nr) {
-        const int row = r0 + r;
-        const size_t ix = (size_t)row * U + unit;
-        if (st.trace) hest[ix] = acc[r];
-        const int i = sk.row_data[row];
-        if (i >= 0) {
-            const double2 ye = st.ysrc_e[ix], yp = st.ysrc_p[ix], hh = h[(size_t)row * R + rl];
-            const int tx = sidx[(size_t)i * R + rl];
-            const double2 ze = c_div1(ye, acc[r]), zp = c_div1(yp, hh);
-            const int de = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(ze.x * idd, 0.0)
-                                                         : make_double2(ze.x * idd, ze.y * idd), sI, sQ);
-            const int dp = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(zp.x * idd, 0.0)
-                                                         : make_double2(zp.x * idd, zp.y * idd), sI, sQ);
-            const int ne = __popc((unsigned)(de ^ tx)), np_ = __popc((unsigned)(dp ^ tx));
-            const int cons = sk.considered[i];
-            cnt[0] += ne;
-            cnt[2] += np_;
-            cnt[1] += cons ? ne : 0;
-            cnt[3] += cons ? np_ : 0;
-            if (!st.last) {
-                if (sk.p_diag) {
-                    const double2 pv = sk.row_pval[row];
-                    double2 av = make_double2(0.0, 0.0), au = av;
-                    if (sk.row_pcol[row] >= 0) {
-                        c_fma(av, pv, sym[de]);
-                        c_fma(au, pv, sym[dp]);
-                    }
-                    v[ix] = av;
-                    u[ix] = au;
-                } else {
-                    qe[(size_t)i * U + unit] = (uint16_t)de;
-                    qp[(size_t)i * U + unit] = (uint16_t)dp;
+            const int row = r0 + r;
+            const size_t ix = (size_t)row * U + unit;
+            if (st.trace) hest[ix] = acc[r];
+            const int i = rdat[r];
+            if (i >= 0) {
+                const double2 ze = c_div1(ye[r], acc[r]);
+                const int de = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(ze.x * idd, 0.0)
+                                                             : make_double2(ze.x * idd, ze.y * idd), sI, sQ);
+                const int ne = __popc((unsigned)(de ^ tx[r]));
+                const int cons = rcons[r];
+                cnt[0] += ne;
+                cnt[1] += cons ? ne : 0;
+                int dp = 0;
+                if (PERF) {
+                    const double2 zp = c_div1(yp[r], hh[r]);
+                    dp = slice_fast(slt, sk.nI, sk.nQ, sk.real_detect ? make_double2(zp.x * idd, 0.0)
+                                                      : make_double2(zp.x * idd, zp.y * idd), sI, sQ);
+                    const int np_ = __popc((unsigned)(dp ^ tx[r]));
+                    cnt[2] += np_;
+                    cnt[3] += cons ? np_ : 0;
                 }
+                if (!st.last) {
+                    if (sk.p_diag) {
+                        const double2 pv = rpval[r];
+                        double2 av = make_double2(0.0, 0.0), au = av;
+                        if (rpcol[r] >= 0) {
+                            c_fma(av, pv, sym[de]);
+                            c_fma(au, pv, sym[dp]);
+                        }
+                        v[ix] = av;
+                        if (PERF) u[ix] = au;
+                    } else {
+                        qe[(size_t)i * U + unit] = (uint16_t)de;
+                        qp[(size_t)i * U + unit] = (uint16_t)dp;
+                    }
+                }
+            } else if (!st.last && sk.p_diag && st.stage == 0) {   // pilot / empty row: constant P xP
+                const int kc = rpcol[r];
+                double2 av = make_double2(0.0, 0.0);
+                if (kc >= 0) c_fma(av, rpval[r], xp[(size_t)kc * R + rl]);
+                v[ix] = av;
+                u[ix] = av;
             }
-        } else if (!st.last && sk.p_diag) {                // pilot / empty row
-            const int kc = sk.row_pcol[row];
-            double2 av = make_double2(0.0, 0.0);
-            if (kc >= 0) c_fma(av, sk.row_pval[row], xp[(size_t)kc * R + rl]);
-            v[ix] = av;
-            u[ix] = av;
-        }
         }
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int tot = wave_sum(cnt[k]);
-        if (lane == 0 && tot) {
+        if (lane == 0 && tot && (k < 2 || PERF)) {
             const int csi = k >> 1, edge = k & 1;
             const size_t idx = ((((size_t)st.scheme * 2 + csi) * 2 + edge) * st.nsnr + snr) * st.nstage + st.stage;
             atomicAdd(&counters[idx], (unsigned long long)tot);
@@ -800,16 +1237,20 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
 template <int NPT>
 static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
                                   unsigned long long* counters, int rb) {
-    const int ug = (b.U + 255) / 256;
+    const int ug = b.U / 64;
     const char* xe = getenv("DSCE_XCD");
     const bool xcd = !xe || xe[0] != '0';
 #define LAUNCH_SF(RBV)                                                                                          \
     {                                                                                                           \
-        const int nrb = (sk.LK + (RBV) - 1) / (RBV);                                                            \
+        const int nrb = (sk.LK + 4 * (RBV) - 1) / (4 * (RBV));                                                  \
         StageArgs sa = st;                                                                                      \
-        sa.xcd_order = xcd && (b.R % 256) == 0 && ((ug * nrb) % 8) == 0;                                        \
-        hipLaunchKernelGGL((k_stage_fused<NPT, RBV>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb, mm.Wd, b.xp,  \
-                           b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);                          \
+        sa.xcd_order = xcd && ((ug * nrb) % 8) == 0;                                                            \
+        if (st.perfect)                                                                                         \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb, mm.Wd, \
+                               b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);                 \
+        else                                                                                                    \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb,      \
+                               mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);          \
         return true;                                                                                            \
     }
     if (rb == 4) LAUNCH_SF(4)
@@ -818,9 +1259,22 @@ static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageA
 #undef LAUNCH_SF
 }
 
+static bool stage_fused_ok(const SchemeK& sk) {
+    const char* mode = getenv("DSCE_STAGE");
+    const bool split = mode && mode[0] == 's';
+    return !sk.despread && !split && (sk.NP == 8 || sk.NP == 16 || sk.NP == 32) && sk.M <= 256 && sk.nI <= 16 &&
+           sk.nQ <= 16;
+}
+
+bool perfect_fusable(const SchemeK& sk) {
+    const char* e = getenv("DSCE_PFUSE");
+    return stage_fused_ok(sk) && sk.p_diag && !(e && e[0] == '0');
+}
+
 void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace) {
+                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace, bool perfect) {
     StageArgs st;
+    st.perfect = perfect ? 1 : 0;
     st.stage = stage;
     st.var = var;
     st.nsnr = mm.nsnr;
@@ -837,10 +1291,7 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
     // select-mode schemes: k_ls + one fused pass (DSCE_STAGE=split keeps the
     // 3-kernel path for A/B; DSCE_STAGE_RB = rows per fused block, 4 | 8 | 16)
-    const char* mode = getenv("DSCE_STAGE");
-    const bool split = mode && mode[0] == 's';
-    if (!sk.despread && !split && (sk.NP == 8 || sk.NP == 16 || sk.NP == 32) && sk.M <= 256 && sk.nI <= 16 &&
-        sk.nQ <= 16) {
+    if (stage_fused_ok(sk)) {
         const char* e = getenv("DSCE_STAGE_RB");
         const int rb = e ? atoi(e) : 8;
         hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);

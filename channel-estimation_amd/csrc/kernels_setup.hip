@@ -315,4 +315,28 @@ void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, lon
     hipLaunchKernelGGL(k_w_extent, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, lohi);
 }
 
+// Pair-tile repack of the (trimmed, zero-diagonal) W band for k_wpair; rows past
+// nrows and columns past the band's extent are zero.  grid (nblk, nslices).
+__global__ void k_wpair_pack(Band Wb, int NP, const double2* __restrict__ w, long long w_elems, PairBand P,
+                             double2* __restrict__ wp, long long wp_elems) {
+    const int blk = blockIdx.x, sl = blockIdx.y;
+    const double2* __restrict__ src = w + (size_t)sl * w_elems + Wb.off[blk];
+    double2* __restrict__ dst = wp + (size_t)sl * wp_elems + P.off[blk];
+    const int ncol = (Wb.khi[blk] - Wb.klo[blk]) / NP, nrows = Wb.nrows[blk];
+    const long long n = (long long)P.ntile[blk] * P.nks * 64;
+    for (long long e = threadIdx.x; e < n; e += blockDim.x) {
+        const int t = (int)(e / (P.nks * 64)), rem = (int)(e % (P.nks * 64));
+        const int ks = rem / 64, k4 = (rem % 64) / 16, i = rem % 16;
+        const int q = 16 * t + i, cl = q / P.rbp, r = q % P.rbp, p = 4 * ks + k4;
+        double2 v = make_double2(0.0, 0.0);
+        if (r < nrows && cl < ncol && p < NP) v = src[((size_t)cl * NP + p) * Wb.rb + r];
+        dst[e] = v;
+    }
+}
+
+void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
+                 double2* wp, long long wp_elems, int nslices) {
+    hipLaunchKernelGGL(k_wpair_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, P, wp, wp_elems);
+}
+
 }  // namespace dsce

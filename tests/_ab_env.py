@@ -26,4 +26,4 @@ for rnd in range(3):
         if ref is None: ref = c
         assert np.array_equal(c, ref), v
 for v, r in res.items():
-    print(v, json.dumps(max(r)))
+    print(v, json.dumps(max(r, key=lambda x: x[0])))

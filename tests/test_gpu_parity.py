@@ -202,9 +202,10 @@ def test_w_band_trim_is_bit_exact(monkeypatch):
 
 @pytest.mark.parametrize("name", ["ofdm", "fbmc_aux"])
 def test_stage_variants_agree(monkeypatch, name):
-    """The fused select-mode stage (k_ls + k_stage_fused, any row-block size)
-    and the 3-kernel split path (k_ls_hest, k_detect, k_precode) differ only in
-    rounding of the one-tap quotient: identical counts on 1024 realisations."""
+    """The fused select-mode stage (k_ls + k_stage_fused, any row-block size,
+    perfect-CSI branch fused into perfect_ic or not, any work order) and the
+    3-kernel split path (k_ls_hest, k_detect, k_precode) differ only in rounding
+    of the one-tap quotient: identical counts on 1024 realisations."""
     from dsce.engine import build_engine
     S = build_setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = build_engine(S, batch=512)
@@ -214,4 +215,10 @@ def test_stage_variants_agree(monkeypatch, name):
     for rb in ("4", "8", "16"):
         monkeypatch.setenv("DSCE_STAGE_RB", rb)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=rb)
+    # perfect-CSI detection fused into perfect_ic (OFDM) on/off, XCD-aware
+    # work order on/off, SNR-chunked receiver, one stream instead of two
+    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "1")):
+        monkeypatch.setenv(var, val)
+        np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=var)
+        monkeypatch.delenv(var)
     eng.close()
