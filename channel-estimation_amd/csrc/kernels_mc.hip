@@ -114,8 +114,44 @@ __device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
 // parity tolerance).  grid (ceil(nchunk/64), R/4, ntap).
 // Output IR[tap][n][rep] (only the non-zero-power taps).
 // ---------------------------------------------------------------------------
+// (cos, sin)(2 pi x) for |x| of a few turns: quarter-turn reduction (exact),
+// then Taylor polynomials on |theta| <= pi/4 (truncation < 1e-16); ~25 FP64
+// instructions instead of the general-argument library sincos.
+__device__ __forceinline__ double2 cis_turns(double x) {
+    const double k = rint(4.0 * x);
+    const double r = fma(-0.25, k, x);                      // exact: |r| <= 1/8
+    const double t = TWO_PI * r, t2 = t * t;
+    double sp = 1.0 / 1307674368000.0;                      // 1/15!
+    sp = fma(sp, -t2, 1.0 / 6227020800.0);
+    sp = fma(sp, -t2, 1.0 / 39916800.0);
+    sp = fma(sp, -t2, 1.0 / 362880.0);
+    sp = fma(sp, -t2, 1.0 / 5040.0);
+    sp = fma(sp, -t2, 1.0 / 120.0);
+    sp = fma(sp, -t2, 1.0 / 6.0);
+    const double sn = fma(-t * t2, sp, t);
+    double cp = 1.0 / 20922789888000.0;                     // 1/16!
+    cp = fma(cp, -t2, 1.0 / 87178291200.0);
+    cp = fma(cp, -t2, 1.0 / 479001600.0);
+    cp = fma(cp, -t2, 1.0 / 3628800.0);
+    cp = fma(cp, -t2, 1.0 / 40320.0);
+    cp = fma(cp, -t2, 1.0 / 720.0);
+    cp = fma(cp, -t2, 1.0 / 24.0);
+    cp = fma(cp, -t2, 0.5);
+    const double cs = fma(-t2, cp, 1.0);
+    // quadrant q: (c, s) = (cs, sn), (-sn, cs), (-cs, -sn), (sn, -cs) -- selects, no branches
+    const int q = ((int)k) & 3;
+    const double a = (q & 1) ? sn : cs, b = (q & 1) ? cs : sn;
+    return make_double2(((q + 1) & 2) ? -a : a, (q & 2) ? -b : b);
+}
+
+// z * w with two fused multiply-adds per component
+__device__ __forceinline__ double2 c_mul_fma(double2 z, double2 w) {
+    return make_double2(fma(z.x, w.x, -z.y * w.y), fma(z.x, w.y, z.y * w.x));
+}
+
 static constexpr int JCH_MAX = 16;
-__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R, int jch,
+template <int JCH>
+__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
                                                double2* __restrict__ ir) {
     extern __shared__ double sm[];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -142,43 +178,76 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
         wi[p] = sn;
     }
     __syncthreads();
-    const int n0 = (blockIdx.x * WAVE + lane) * jch;
+    const int n0 = (blockIdx.x * WAVE + lane) * JCH;
     if (n0 >= ch.N) return;
     const double t0 = (double)n0 * ch.dt;
-    double2 acc[JCH_MAX];
+    double2 acc[JCH];
 #pragma unroll
-    for (int i = 0; i < JCH_MAX; ++i) acc[i] = make_double2(0.0, 0.0);
-    for (int p = 0; p < P; ++p) {
-        double sn, cs;
-        sincos(TWO_PI * (ph[p] + ds[p] * t0), &sn, &cs);
-        double2 z = make_double2(cs, sn);
+    for (int i = 0; i < JCH; ++i) acc[i] = make_double2(0.0, 0.0);
+    // two paths per step: independent rotation chains interleave (ILP)
+    int p = 0;
+    for (; p + 1 < P; p += 2) {
+        double2 z0 = cis_turns(ph[p] + ds[p] * t0);
+        double2 z1 = cis_turns(ph[p + 1] + ds[p + 1] * t0);
+        const double2 w0 = make_double2(wr[p], wi[p]), w1 = make_double2(wr[p + 1], wi[p + 1]);
+#pragma unroll
+        for (int i = 0; i < JCH; ++i) {
+            acc[i].x += z0.x + z1.x;
+            acc[i].y += z0.y + z1.y;
+            if (i + 1 < JCH) {
+                z0 = c_mul_fma(z0, w0);
+                z1 = c_mul_fma(z1, w1);
+            }
+        }
+    }
+    for (; p < P; ++p) {
+        double2 z = cis_turns(ph[p] + ds[p] * t0);
         const double2 w = make_double2(wr[p], wi[p]);
 #pragma unroll
-        for (int i = 0; i < JCH_MAX; ++i) {
-            if (i < jch) {
-                acc[i].x += z.x;
-                acc[i].y += z.y;
-                z = c_mul(z, w);
-            }
+        for (int i = 0; i < JCH; ++i) {
+            acc[i].x += z.x;
+            acc[i].y += z.y;
+            if (i + 1 < JCH) z = c_mul_fma(z, w);
         }
     }
     const double sp = sqrt((double)P);
     const double g = ch.sqrt_pdp[tap];
 #pragma unroll
-    for (int i = 0; i < JCH_MAX; ++i) {
+    for (int i = 0; i < JCH; ++i) {
         const int n = n0 + i;
-        if (i < jch && n < ch.N)
-            ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
+        if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
     }
 }
 
-void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
-    int jch = (ch.N + WAVE - 1) / WAVE;
-    if (jch > JCH_MAX) jch = JCH_MAX;
-    const int nchunk = (ch.N + jch - 1) / jch;
+template <int JCH>
+static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+    const int nchunk = (ch.N + JCH - 1) / JCH;
     dim3 grid((nchunk + WAVE - 1) / WAVE, R / 4, ch.ntap);
-    hipLaunchKernelGGL(k_jakes, grid, dim3(256), (size_t)4 * 4 * ch.paths * sizeof(double), s, ch, seed, rep0, R, jch,
+    hipLaunchKernelGGL(k_jakes<JCH>, grid, dim3(256), (size_t)4 * 4 * ch.paths * sizeof(double), s, ch, seed, rep0, R,
                        ir);
+}
+
+void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+    int jch = (ch.N + WAVE - 1) / WAVE;           // samples per lane: one wave covers N when N <= 1024
+    if (jch > JCH_MAX) jch = JCH_MAX;
+    switch (jch) {
+        case 1: launch_jakes_t<1>(s, ch, seed, rep0, R, ir); break;
+        case 2: launch_jakes_t<2>(s, ch, seed, rep0, R, ir); break;
+        case 3: launch_jakes_t<3>(s, ch, seed, rep0, R, ir); break;
+        case 4: launch_jakes_t<4>(s, ch, seed, rep0, R, ir); break;
+        case 5: launch_jakes_t<5>(s, ch, seed, rep0, R, ir); break;
+        case 6: launch_jakes_t<6>(s, ch, seed, rep0, R, ir); break;
+        case 7: launch_jakes_t<7>(s, ch, seed, rep0, R, ir); break;
+        case 8: launch_jakes_t<8>(s, ch, seed, rep0, R, ir); break;
+        case 9: launch_jakes_t<9>(s, ch, seed, rep0, R, ir); break;
+        case 10: launch_jakes_t<10>(s, ch, seed, rep0, R, ir); break;
+        case 11: launch_jakes_t<11>(s, ch, seed, rep0, R, ir); break;
+        case 12: launch_jakes_t<12>(s, ch, seed, rep0, R, ir); break;
+        case 13: launch_jakes_t<13>(s, ch, seed, rep0, R, ir); break;
+        case 14: launch_jakes_t<14>(s, ch, seed, rep0, R, ir); break;
+        case 15: launch_jakes_t<15>(s, ch, seed, rep0, R, ir); break;
+        default: launch_jakes_t<16>(s, ch, seed, rep0, R, ir); break;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -557,6 +626,8 @@ static void launch_pass2_nt(hipStream_t s, const SchemeK& sk, const ChannelK& ch
         case 2: launch_pass2<2>(s, sk, ch, b, ord, o, lds); break;
         case 3: launch_pass2<3>(s, sk, ch, b, ord, o, lds); break;
         case 4: launch_pass2<4>(s, sk, ch, b, ord, o, lds); break;
+        case 5: launch_pass2<5>(s, sk, ch, b, ord, o, lds); break;
+        case 6: launch_pass2<6>(s, sk, ch, b, ord, o, lds); break;
         default: launch_pass2<0>(s, sk, ch, b, ord, o, lds); break;
     }
 }

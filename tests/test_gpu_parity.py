@@ -216,8 +216,8 @@ def test_stage_variants_agree(monkeypatch, name):
         monkeypatch.setenv("DSCE_STAGE_RB", rb)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=rb)
     # perfect-CSI detection fused into perfect_ic (OFDM) on/off, XCD-aware
-    # work order on/off, SNR-chunked receiver, one stream instead of two
-    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "1")):
+    # work order on/off, SNR-chunked receiver, two streams instead of one
+    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "2")):
         monkeypatch.setenv(var, val)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=var)
         monkeypatch.delenv(var)
