@@ -1,0 +1,77 @@
+"""C5 (48 subcarriers at SR 720 kHz, N = 1080, NP = 32 pilots, 3
+channel taps; build-defined scale-up of the script's geometry) against the CPU
+oracle: Jakes taps, pilot correlations, W / W0, per-unit traces of every stage
+and (OFDM) bit-error counts.  Two of the 16 SNR points keep the literal oracle
+(dense Q'HG, full(W)) within a couple of minutes."""
+import numpy as np
+import pytest
+
+import harness  # noqa: F401  (sys.path)
+from dsce.configs import build_setup
+from oracle import refsim
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0005
+SNR = [20.0, 36.0]
+
+
+def _check_w(eng, mm, nsnr):
+    for k in range(nsnr):
+        for var, key, R in ((0, "W", mm["R_est"][k]), (1, "W0", mm["R_noI"][k])):
+            wg = eng.W(0, k, var)
+            wo = mm[key][:, k]
+            scale = np.abs(wo).max()
+            tol = max(1e-14 * np.linalg.cond(R) * max(1, R.shape[0] / 16), 1e-12) * scale
+            border = np.abs(np.abs(wo) - 1e-8) <= tol
+            assert np.all((np.abs(wg - wo) <= tol) | border), (k, var)
+
+
+def _check_trace(S, sc, eng, mm, rep, snrs):
+    tr = {}
+    refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
+                    trace=tr)
+    for k in snrs:
+        g = eng.trace_unit(0, SEED, rep, k)
+        np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
+        for st in range(S.n_iter + 1):
+            np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
+            np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
+
+
+def test_c5_ofdm_matches_oracle():
+    from dsce.engine import build_engine
+    S = build_setup("c5", schemes=("ofdm",), snr_db=SNR)
+    sc = S.schemes["ofdm"]
+    assert S.N == 1080 and sc.LK == 672 and len(sc.pilot_pos) == 32 and len(S.channel.IndexDelayTaps) == 3
+    eng = build_engine(S, batch=64)
+    for rep in (0, 3):
+        ir_g = eng.channel_impulse_response(SEED, rep)
+        ch = S.channel
+        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
+                               ch.MaximumDopplerShift, ch.Paths)
+        np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
+    mm = harness.oracle_mmse(S, sc)
+    rhp, rest, rnoi = eng.correlation(0)
+    scale = np.abs(mm["R_hP"]).max()
+    np.testing.assert_allclose(rhp, mm["R_hP"], rtol=0, atol=1e-12 * scale)
+    np.testing.assert_allclose(rest, mm["R_est"], rtol=0, atol=1e-12 * scale)
+    _check_w(eng, mm, len(SNR))
+    _check_trace(S, sc, eng, mm, 7, (0, 1))
+    cg = eng.run(SEED, 0, 64)
+    res = refsim.simulate(SEED, 0, 64, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
+                          [mm])
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
+    eng.close()
+
+
+def test_c5_fbmc_aux_matches_oracle():
+    from dsce.engine import build_engine
+    S = build_setup("c5", schemes=("fbmc_aux",), snr_db=SNR[1:])
+    sc = S.schemes["fbmc_aux"]
+    assert sc.LK == 1440
+    eng = build_engine(S, batch=64)
+    mm = harness.oracle_mmse(S, sc)
+    _check_w(eng, mm, 1)
+    _check_trace(S, sc, eng, mm, 2, (0,))
+    eng.close()
