@@ -91,6 +91,7 @@ struct Scheme {
     double2* W = nullptr;
     double2* Wd = nullptr;
     double2* Wp = nullptr;          // pair-tile copy of W for k_wpair (null: not eligible)
+    double* Wp3 = nullptr;          // its Re / Im / Re+Im planes (3M complex products)
     long long wp_elems = 0, wp_exec = 0;
     PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
@@ -506,7 +507,8 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
     s.wp_exec = exec;
     const int nsl = 2 * c->nsnr;
     s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
-    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl);
+    s.Wp3 = dalloc<double>(c, (size_t)nsl * 3 * s.wp_elems);
+    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3);
     DSCE_HIP_CHECK(hipStreamSynchronize(c->stream));
     DSCE_HIP_CHECK(hipGetLastError());
 }
@@ -526,7 +528,9 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         free_alloc(c, s.W);
         free_alloc(c, s.Wd);
         if (s.Wp) free_alloc(c, s.Wp);
+        if (s.Wp3) free_alloc(c, s.Wp3);
         s.W = s.Wd = s.Wp = nullptr;
+        s.Wp3 = nullptr;
         s.wband = s.wband_struct;
         s.w_elems = s.wband.elems;
         s.Wb = upload_band(c, s.wband, false);
@@ -722,6 +726,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.nsnr = c->nsnr;
         mm.Wb = s.Wb;
         mm.Wp = s.Wp;
+        mm.Wp3 = s.Wp3;
         mm.wp_elems = s.wp_elems;
         mm.Pb = s.Pb;
         {

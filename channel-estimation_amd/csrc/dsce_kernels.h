@@ -41,6 +41,7 @@ struct MmseK {
     int nsnr;
     Band Wb;              // block geometry (vals unused; per-(var,snr) base added)
     const double2* Wp;    // [var][snr][wp_elems] pair-tile layout (k_wpair), or null
+    const double* Wp3;    // [var][snr][3 wp_elems] Re / Im / Re+Im planes (3M form), or null
     long long wp_elems;
     PairBand Pb;
 };
@@ -91,7 +92,7 @@ void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv
 void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
                 const int* q_start, int QL, double2* rd /* packed, w_elems */);
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices);
+                 double2* wp, long long wp_elems, int nslices, double* w3);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);
 void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
              const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);

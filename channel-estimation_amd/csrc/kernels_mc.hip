@@ -924,6 +924,131 @@ __global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __rest
     }
 }
 
+// 3M (Gauss / Karatsuba) form of k_wpair: per k-step three real MFMAs
+//   P1 += Wr hr,  P2 += Wi hi,  P3 += (Wr + Wi)(hr + hi);  Re = P1 - P2, Im = P3 - P1 - P2
+// instead of four (-25 % matrix-core work); W arrives as three 64-double planes
+// per (tile, k-step) (k_wpair_pack3), hP as Re / Im / Re+Im registers.
+template <int RBP, int NKS>
+__global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems,
+                                                int var, int nsnr, int snr0, int R, int U,
+                                                const double2* __restrict__ hp, const double2* __restrict__ v,
+                                                const double2* __restrict__ y, double2* __restrict__ yest) {
+    constexpr int PER = RBP == 24 ? 3 : 2;
+    constexpr int CPP = RBP == 24 ? 2 : 1;
+    constexpr int NACC = RBP / 4;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int unit = blockIdx.x * 64 + wv * 16 + j;
+    const int snr = snr0 + (blockIdx.x * 64) / R;
+    const int blk = blockIdx.y;
+    double br[NKS], bi[NKS], bs[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const double2 h = hp[(size_t)(4 * ks + g) * U + unit];
+        br[ks] = h.x;
+        bi[ks] = h.y;
+        bs[ks] = h.x + h.y;
+    }
+    const int clo = P.clo[blk], ntile = P.ntile[blk];
+    const double* __restrict__ w = W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + lane;
+    double2 acc[NACC];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) acc[k] = make_double2(0.0, 0.0);
+    const double2* __restrict__ vb = v + (size_t)clo * U + unit;
+    struct T3 {
+        double r[NKS], i[NKS], s[NKS];
+    };
+    struct D3 {
+        d4 p1, p2, p3;
+    };
+    auto ldt = [&](int t, T3& a) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const double* q = w + ((size_t)t * NKS + ks) * 192;
+            a.r[ks] = q[0];
+            a.i[ks] = q[64];
+            a.s[ks] = q[128];
+        }
+    };
+    auto mma = [&](const T3& a, D3& d) {
+        d.p1 = d4{0, 0, 0, 0};
+        d.p2 = d.p1;
+        d.p3 = d.p1;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            d.p1 = MFMA64(a.r[ks], br[ks], d.p1);
+            d.p2 = MFMA64(a.i[ks], bi[ks], d.p2);
+            d.p3 = MFMA64(a.s[ks], bs[ks], d.p3);
+        }
+    };
+    // epilogue of a finished tile (period position TT): Re/Im, x v_c, accumulate
+    auto epi = [&](const D3& d, const double2 (&vvv)[CPP], auto ttc) {
+        constexpr int tt = decltype(ttc)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int q0 = 16 * tt + 4 * i;
+            const int cc = q0 / RBP, rho = (q0 % RBP) / 4;
+            const double re = d.p1[i] - d.p2[i], im = d.p3[i] - d.p1[i] - d.p2[i];
+            c_fma(acc[rho], make_double2(re, im), vvv[cc]);
+        }
+    };
+    auto ldv = [&](int per, double2 (&vvv)[CPP]) {
+#pragma unroll
+        for (int cc = 0; cc < CPP; ++cc) vvv[cc] = vb[(size_t)(per * CPP + cc) * U];
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    // ping-pong W tiles: tile t+1's loads are issued before tile t's MFMAs;
+    // sched_barrier keeps the compiler from sinking them back to their uses
+    T3 A0, A1;
+    D3 Da;
+    double2 vv[CPP];
+    if (ntile > 0) ldt(0, A0);
+    for (int t0 = 0; t0 < ntile; t0 += PER) {
+        ldv(t0 / PER, vv);
+        const int tn = t0 + PER < ntile ? t0 + PER : t0;
+        if (PER == 3) {
+            ldt(t0 + 1, A1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A0, Da);
+            epi(Da, vv, I0{});
+            __builtin_amdgcn_sched_barrier(0);
+            ldt(t0 + 2, A0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A1, Da);
+            epi(Da, vv, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+            ldt(tn, A1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A0, Da);
+            epi(Da, vv, I2{});
+            __builtin_amdgcn_sched_barrier(0);
+            A0 = A1;
+        } else {
+            ldt(t0 + 1, A1);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A0, Da);
+            epi(Da, vv, I0{});
+            __builtin_amdgcn_sched_barrier(0);
+            ldt(tn, A0);
+            __builtin_amdgcn_sched_barrier(0);
+            mma(A1, Da);
+            epi(Da, vv, I1{});
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    const int row0 = P.row0[blk], nrows = P.nrows[blk];
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+        const int r = g + 4 * k;
+        if (r < nrows) {
+            const size_t i = (size_t)(row0 + r) * U + unit;
+            yest[i] = c_sub(y[i], acc[k]);
+        }
+    }
+}
+
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
     // DSCE_WCONTRACT = pair (default) | mfma (32-row tiles) | valu — read per launch for A/B.
     const char* mode = getenv("DSCE_WCONTRACT");
@@ -932,6 +1057,29 @@ void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
         const dim3 grid(b.U / 64, mm.Pb.nblk);
         const char* pfe = getenv("DSCE_WPAIR_PF");
         const bool pf = !(pfe && pfe[0] == '0');
+        // DSCE_WPAIR_3M=0 selects the 4-MFMA complex product
+        // 3M form by default where its extra registers still leave 3 waves/SIMD
+        // (NP <= 16); DSCE_WPAIR_3M=0 / 1 forces it off / on
+        const char* m3e = getenv("DSCE_WPAIR_3M");
+        const bool m3 = m3e ? m3e[0] != '0' : mm.Pb.nks <= 4;
+        if (mm.Wp3 && m3) {
+#define LAUNCH_W3(RBPV, NKSV)                                                                                    \
+    {                                                                                                            \
+        hipLaunchKernelGGL((k_wpair3<RBPV, NKSV>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,           \
+                           mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                                   \
+    }
+            if (mm.Pb.rbp == 24) {
+                if (mm.Pb.nks == 2) LAUNCH_W3(24, 2)
+                else if (mm.Pb.nks == 4) LAUNCH_W3(24, 4)
+                else LAUNCH_W3(24, 8)
+            } else {
+                if (mm.Pb.nks == 2) LAUNCH_W3(32, 2)
+                else if (mm.Pb.nks == 4) LAUNCH_W3(32, 4)
+                else LAUNCH_W3(32, 8)
+            }
+#undef LAUNCH_W3
+            return;
+        }
 #define LAUNCH_WP(RBPV, NKSV)                                                                                    \
     {                                                                                                            \
         if (pf)                                                                                                  \

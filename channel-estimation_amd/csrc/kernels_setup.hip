@@ -352,9 +352,25 @@ __global__ void k_wpair_pack(Band Wb, int NP, const double2* __restrict__ w, lon
     }
 }
 
+// 3M planes of the pair tiles: per (tile, k-step) the 64 lanes' Re, Im and
+// Re+Im as three contiguous 64-double rows (k_wpair's Gauss/Karatsuba form).
+__global__ void k_wpair_pack3(long long wp_elems, const double2* __restrict__ wp, double* __restrict__ w3) {
+    const long long n = wp_elems;
+    const double2* __restrict__ src = wp + (size_t)blockIdx.y * wp_elems;
+    double* __restrict__ dst = w3 + (size_t)blockIdx.y * 3 * wp_elems;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+        const double2 v = src[e];
+        const long long g = e / 64, l = e % 64;
+        dst[(g * 3 + 0) * 64 + l] = v.x;
+        dst[(g * 3 + 1) * 64 + l] = v.y;
+        dst[(g * 3 + 2) * 64 + l] = v.x + v.y;
+    }
+}
+
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices) {
+                 double2* wp, long long wp_elems, int nslices, double* w3) {
     hipLaunchKernelGGL(k_wpair_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, P, wp, wp_elems);
+    if (w3) hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, wp, w3);
 }
 
 }  // namespace dsce
