@@ -287,6 +287,37 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
                 const double2 q = s.Q[(size_t)(s.qband.row0[blk] + rl) * N + k];
                 s.qband.vals[s.qband.off[blk] + (size_t)(k - s.qband.klo[blk]) * DSCE_RB + rl] = make_double2(q.x, -q.y);
             }
+    // fused perfect-CSI IC tables (see SchemeK::pic_ok)
+    {
+        int md = 0;
+        for (int q = 0; q < c->ch.ntap; ++q) md = std::max(md, c->ch.tap_delay[q]);
+        const int nb = (int)s.qband.row0.size();
+        std::vector<int> s0v(nb);
+        std::vector<long long> goff(nb);
+        std::vector<double2> gtab;
+        bool ok = true;
+        int prow = 0;
+        for (int b = 0; b < nb && ok; ++b) {
+            const int r0 = s.qband.row0[b], klo = s.qband.klo[b], khi = s.qband.khi[b];
+            const int s0 = std::max(0, klo - md);
+            for (int n = s0; n < khi && ok; ++n)
+                for (int col = 0; col < LK && ok; ++col)
+                    if (nz(s.G[(size_t)col * N + n]) && (col < r0 || col >= r0 + DSCE_RB)) ok = false;
+            s0v[b] = s0;
+            prow = std::max(prow, (khi - s0) + (khi - klo));
+            goff[b] = (long long)gtab.size();
+            for (int n = s0; n < khi; ++n)
+                for (int cc = 0; cc < DSCE_RB; ++cc)
+                    gtab.push_back(r0 + cc < LK ? s.G[(size_t)(r0 + cc) * N + n] : make_double2(0, 0));
+        }
+        s.k.pic_ok = ok && nb > 0 && prow * DSCE_RB * 16 <= 96 * 1024 ? 1 : 0;
+        s.k.pic_rows = prow;
+        if (s.k.pic_ok) {
+            s.k.pic_s0 = dupload(c, s0v);
+            s.k.pic_goff = dupload(c, goff);
+            s.k.pic_g = dupload(c, gtab);
+        }
+    }
     // W band: rows r, k = (c, p); c overlaps where Q-support(r) meets (H G)-support(c)
     int maxd = 0;
     for (int q = 0; q < c->ch.ntap; ++q) maxd = std::max(maxd, c->ch.tap_delay[q]);

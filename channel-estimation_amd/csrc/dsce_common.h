@@ -147,6 +147,15 @@ struct SchemeK {
     const int* row_pcol;          // LK
     const double2* row_pval;      // LK
     int p_diag;
+    // fused perfect-CSI IC pass (pic_ok: every Q^H block's rows are the G
+    // columns of its own samples, e.g. OFDM symbols): per Q^H block the first
+    // sample s0 = klo - max delay and the dense G rows [s0, khi) x 24 columns
+    // starting at the block's first row, at pic_goff
+    int pic_ok;
+    int pic_rows;                 // max over blocks of (khi - s0) + (khi - klo): LDS rows of k_pic
+    const int* pic_s0;
+    const long long* pic_goff;
+    const double2* pic_g;
 };
 
 struct ChannelK {

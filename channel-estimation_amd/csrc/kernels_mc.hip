@@ -303,9 +303,7 @@ __global__ void __launch_bounds__(64) k_band(Band A, BandOrder ord, In in, Out o
         for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], ak[r], x);
         ld = ldn;
     }
-#pragma unroll
-    for (int r = 0; r < DSCE_RB; ++r)
-        if (r < nrows) o(row0 + r, lane, acc[r]);
+    o.rows(row0, nrows, lane, acc);
     o.finish(lane);
 }
 
@@ -329,10 +327,20 @@ struct StoreSoA {
     int stride;
     __device__ __forceinline__ void prepare(double2*) {}
     __device__ __forceinline__ void finish(int) {}
+    template <int RBN>
+    __device__ __forceinline__ void rows(int row0, int nrows, int lane, const double2 (&acc)[RBN]) {
+#pragma unroll
+        for (int r = 0; r < RBN; ++r)
+            if (r < nrows) (*this)(row0 + r, lane, acc[r]);
+    }
     __device__ __forceinline__ void operator()(int row, int lane, double2 v) const {
         p[(size_t)row * stride + lane] = v;
     }
 };
+struct TapDelays {
+    int d[DSCE_MAX_TAPS];
+};
+
 // (H t)[n] = sum_tau IR[tau][n] t[n - d_tau]  (GetConvolutionMatrix, FastFading.m:284).
 // NT > 0: exactly NT taps, unrolled so all 2*NT loads of a column are in flight
 // together (load) before the taps are combined; NT == 0: any tap count, loop.
@@ -384,6 +392,12 @@ struct StorePerfectIC {
     int U, R;
     __device__ __forceinline__ void prepare(double2*) {}
     __device__ __forceinline__ void finish(int) {}
+    template <int RBN>
+    __device__ __forceinline__ void rows(int row0, int nrows, int lane, const double2 (&acc)[RBN]) {
+#pragma unroll
+        for (int r = 0; r < RBN; ++r)
+            if (r < nrows) (*this)(row0 + r, lane, acc[r]);
+    }
     __device__ __forceinline__ void operator()(int row, int lane, double2 acc) const {
         const size_t i = (size_t)row * U + lane;
         const double2 hv = h[(size_t)row * R + lane % R];
@@ -448,12 +462,70 @@ struct StorePerfectDetect {
         c1 = 0;
     }
     __device__ __forceinline__ void operator()(int row, int lane, double2 acc) {
+        if (row_data[row] < 0) return;
+        detect(row, lane, acc, u[(size_t)row * U + lane]);
+    }
+    // Rows in groups of 4: every input of a group (y, h, u, transmitted symbol
+    // index, row tables) is requested before the group's first store, so one
+    // memory round trip covers four rows instead of one.  ur: the rows' u values
+    // if the caller holds them in registers (k_pic), else null.
+    template <int RBN>
+    __device__ __forceinline__ void rows(int row0, int nrows, int lane, const double2 (&acc)[RBN]) {
+        rows_impl<RBN, false>(row0, nrows, lane, acc, acc);
+    }
+    template <int RBN>
+    __device__ __forceinline__ void rows_u(int row0, int nrows, int lane, const double2 (&acc)[RBN],
+                                           const double2 (&ur)[RBN]) {
+        rows_impl<RBN, true>(row0, nrows, lane, acc, ur);
+    }
+    template <int RBN, bool UREG>
+    __device__ __forceinline__ void rows_impl(int row0, int nrows, int lane, const double2 (&acc)[RBN],
+                                              const double2 (&ur)[RBN]) {
+        const int rl = lane % R;
+#pragma unroll
+        for (int g0 = 0; g0 < RBN; g0 += 4) {
+            double2 yv[4], hv[4], uv[4], pv[4];
+            int tx[4], dd[4], cn[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = g0 + k;
+                const int row = row0 + (r < nrows ? r : 0);
+                dd[k] = r < nrows ? row_data[row] : -1;
+                cn[k] = row_cons[row];
+                pv[k] = row_pval[row];
+                const size_t i = (size_t)row * U + lane;
+                yv[k] = y[i];
+                hv[k] = h[(size_t)row * R + rl];
+                uv[k] = UREG ? ur[r < RBN ? r : 0] : u[i];
+                tx[k] = sidx[(size_t)(dd[k] > 0 ? dd[k] : 0) * R + rl];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = g0 + k;
+                if (dd[k] < 0) continue;
+                double2 rr = c_sub(yv[k], acc[r < RBN ? r : 0]);
+                rr = c_add(rr, c_mul(hv[k], uv[k]));
+                const double2 z = c_div1(rr, hv[k]);
+                const int dp = slice_fast(*slt, nI, nQ, real_detect ? make_double2(z.x * idd, 0.0)
+                                                                    : make_double2(z.x * idd, z.y * idd), sI, sQ);
+                const int ne = __popc((unsigned)(dp ^ tx[k]));
+                c0 += ne;
+                c1 += cn[k] ? ne : 0;
+                if (!last) {
+                    double2 av = make_double2(0.0, 0.0);
+                    c_fma(av, pv[k], sym[dp]);
+                    u[(size_t)(row0 + r) * U + lane] = av;
+                }
+            }
+        }
+    }
+    // y_perf = y - acc + h u of one row, sliced, counted, re-precoded into u
+    __device__ __forceinline__ void detect(int row, int lane, double2 acc, double2 uv) {
         const size_t i = (size_t)row * U + lane;
         const int rl = lane % R;
         const double2 hv = h[(size_t)row * R + rl];
         const int d = row_data[row];
         if (d < 0) return;
-        const double2 uv = u[i];
         double2 r = c_sub(y[i], acc);
         r = c_add(r, c_mul(hv, uv));
         const double2 z = c_div1(r, hv);
@@ -604,6 +676,91 @@ void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const
 // perfect-CSI interference cancellation product (D - diag h) u = Q'(H(G u)) - h.*u
 // (script:541-543), two banded passes.
 // ---------------------------------------------------------------------------
+// Perfect-CSI IC iteration in one pass for schemes whose Q^H blocks only see
+// their own G columns (SchemeK::pic_ok, OFDM): per (64 units, Q^H block) the
+// block's u values stay in registers, t = G u is formed on the fly for each
+// sample and tap delay from the dense per-block G rows, (H t)[n] from the taps
+// and y_perf = Q^H (H t) accumulated for the block's rows; the epilogue is
+// StorePerfectDetect (y - acc + h u, slice, count, re-precode u in place).
+// t never touches memory.  grid: Q^H blocks x units/64 in BandOrder.
+template <int NT>
+__global__ void __launch_bounds__(64) k_pic(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, int ntap,
+                                            TapDelays dl, StorePerfectDetect out) {
+    extern __shared__ double2 pic_lds[];
+    constexpr int NTS = NT > 0 ? NT : DSCE_MAX_TAPS;
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int lane = ug * WAVE + threadIdx.x;
+    const int U = out.U, R = out.R, rl = lane % R;
+    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk], khi = sk.QH.khi[blk];
+    const int s0 = sk.pic_s0[blk];
+    // LDS: constellation + slicer (epilogue), then the block's G rows [s0, khi) x 24
+    // and Q^H columns [klo, khi) x 24, read as broadcasts
+    double2* sg = pic_lds + 256 + (sizeof(SlicerLds) + 15) / 16;
+    const int ng = (khi - s0) * DSCE_RB, nq = (khi - klo) * DSCE_RB;
+    double2* sq = sg + ng;
+    {
+        const double2* __restrict__ gsrc = sk.pic_g + sk.pic_goff[blk];
+        const double2* __restrict__ qsrc = sk.QH.vals + sk.QH.off[blk];
+        for (int i = threadIdx.x; i < ng; i += WAVE) sg[i] = gsrc[i];
+        for (int i = threadIdx.x; i < nq; i += WAVE) sq[i] = qsrc[i];
+    }
+    StorePerfectDetect o = out;
+    double2 ur[DSCE_RB];
+#pragma unroll
+    for (int c = 0; c < DSCE_RB; ++c)
+        ur[c] = row0 + c < sk.LK ? o.u[(size_t)(row0 + c) * U + lane] : make_double2(0.0, 0.0);
+    o.prepare(pic_lds);                                  // stages its tables and syncs the block
+    double2 acc[DSCE_RB];
+#pragma unroll
+    for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
+    const int nt = NT > 0 ? NT : ntap;
+    // taps of sample n+1 are requested while sample n is processed
+    constexpr int NPF = NT > 0 ? NT : 1;
+    double2 hcur[NPF], hnxt[NPF];
+    if (NT > 0) {
+#pragma unroll
+        for (int q = 0; q < NPF; ++q) hcur[q] = ir[((size_t)q * N + klo) * R + rl];
+    }
+    for (int n = klo; n < khi; ++n) {
+        if (NT > 0) {
+            const int nn = n + 1 < khi ? n + 1 : n;
+#pragma unroll
+            for (int q = 0; q < NPF; ++q) hnxt[q] = ir[((size_t)q * N + nn) * R + rl];
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        double2 x = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int q = 0; q < NTS; ++q) {
+            if (q >= nt) break;
+            const int m = n - dl.d[q];
+            if (m < 0) continue;
+            const double2 hq = NT > 0 ? hcur[q < NPF ? q : 0] : ir[((size_t)q * N + n) * R + rl];
+            const double2* gr = sg + (m - s0) * DSCE_RB;
+            // t = G[m, :] u with 4 partial sums (independent FMA chains)
+            double2 t0 = make_double2(0.0, 0.0), t1 = t0, t2 = t0, t3 = t0;
+#pragma unroll
+            for (int c = 0; c < DSCE_RB; c += 4) {
+                c_fma(t0, gr[c], ur[c]);
+                c_fma(t1, gr[c + 1], ur[c + 1]);
+                c_fma(t2, gr[c + 2], ur[c + 2]);
+                c_fma(t3, gr[c + 3], ur[c + 3]);
+            }
+            const double2 t = c_add(c_add(t0, t1), c_add(t2, t3));
+            c_fma(x, hq, t);
+        }
+        const double2* qk = sq + (n - klo) * DSCE_RB;
+#pragma unroll
+        for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], qk[r], x);
+        if (NT > 0) {
+#pragma unroll
+            for (int q = 0; q < NPF; ++q) hcur[q] = hnxt[q];
+        }
+    }
+    o.rows_u(row0, nrows, lane, acc, ur);
+    o.finish(lane);
+}
+
 template <int NT, class Out>
 static void launch_pass2(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
                          const Out& o, size_t lds) {
@@ -633,7 +790,11 @@ static void launch_pass2_nt(hipStream_t s, const SchemeK& sk, const ChannelK& ch
 }
 
 void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd) {
-    launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
+    // DSCE_PIC=1: one-pass k_pic (t never written; 248 VGPRs -> 2 waves/SIMD,
+    // measured 5 % slower than the two passes at C2, so opt-in)
+    const char* pe = getenv("DSCE_PIC");
+    const bool pic = pd && sk.pic_ok && (pe && pe[0] == '1') && ((size_t)(b.U / WAVE) * sk.QH.nblk) % 8 == 0;
+    if (!pic) launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
     // SNR-fastest XCD-aware order: the SNR units of a realisation share its taps
     const char* xe = getenv("DSCE_XCD");
     const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, (!xe || xe[0] != '0') ? 1 : 0};
@@ -668,7 +829,23 @@ void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McB
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
-    launch_pass2_nt(s, sk, ch, b, ord, o, 256 * sizeof(double2) + sizeof(SlicerLds));
+    const size_t lds = 256 * sizeof(double2) + sizeof(SlicerLds);
+    if (pic) {
+        // one pass, t never written (the G u pass above is skipped)
+        TapDelays dl{};
+        for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
+        // + the G rows and Q^H columns of the widest block
+        const size_t plds = lds + 16 + (size_t)sk.pic_rows * DSCE_RB * sizeof(double2);
+        const dim3 grid((b.U / WAVE) * sk.QH.nblk);
+        switch (ch.ntap) {
+            case 1: hipLaunchKernelGGL(k_pic<1>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
+            case 2: hipLaunchKernelGGL(k_pic<2>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
+            case 3: hipLaunchKernelGGL(k_pic<3>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
+            default: hipLaunchKernelGGL(k_pic<0>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
+        }
+        return;
+    }
+    launch_pass2_nt(s, sk, ch, b, ord, o, lds);
 }
 
 // ---------------------------------------------------------------------------

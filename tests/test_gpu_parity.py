@@ -217,8 +217,11 @@ def test_stage_variants_agree(monkeypatch, name):
         monkeypatch.setenv("DSCE_STAGE_RB", rb)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=rb)
     # perfect-CSI detection fused into perfect_ic (OFDM) on/off, XCD-aware
-    # work order on/off, SNR-chunked receiver, two streams instead of one
-    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "2")):
+    # work order on/off, SNR-chunked receiver, two streams instead of one, the
+    # one-pass perfect-CSI IC (k_pic) instead of the two passes, 4-MFMA instead of
+    # 3M complex products, 32-row contraction tiles instead of pairs
+    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "2"),
+                     ("DSCE_PIC", "1"), ("DSCE_WPAIR_3M", "0"), ("DSCE_WCONTRACT", "mfma")):
         monkeypatch.setenv(var, val)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=var)
         monkeypatch.delenv(var)
