@@ -85,7 +85,7 @@ struct Scheme {
     std::vector<uint8_t> considered;
     std::vector<double2> symbols;
     SchemeK k{};
-    HostBand gband, qband, wband, wband_struct;   // wband: trimmed after build_mmse
+    HostBand gband, qband, hband, wband, wband_struct;   // wband: trimmed after build_mmse
     Band Wb{};
     long long w_elems = 0, w_struct = 0;
     double2* W = nullptr;
@@ -287,6 +287,24 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
                 const double2 q = s.Q[(size_t)(s.qband.row0[blk] + rl) * N + k];
                 s.qband.vals[s.qband.off[blk] + (size_t)(k - s.qband.klo[blk]) * DSCE_RB + rl] = make_double2(q.x, -q.y);
             }
+    // diag(D) = diag(Q' H G) as a banded matvec over the channel taps, rows c,
+    // k = n * ntap + tau:  h[c] = sum_k conj(Q[n,c]) G[n - d_tau, c] IR[tau][n]
+    {
+        const int nt = c->ch.ntap;
+        s.hband = band_geometry(LK, [&](int r, int& a, int& b) { a = qs[r] * nt; b = (qe[r] + 1) * nt; }, 1);
+        s.hband.vals.assign(s.hband.elems, make_double2(0, 0));
+        for (size_t blk = 0; blk < s.hband.row0.size(); ++blk)
+            for (int rl = 0; rl < s.hband.nrows[blk]; ++rl) {
+                const int col = s.hband.row0[blk] + rl;
+                for (int k = s.hband.klo[blk]; k < s.hband.khi[blk]; ++k) {
+                    const int n = k / nt, m = n - c->ch.tap_delay[k % nt];
+                    if (m < 0 || n >= N) continue;
+                    const double2 q = s.Q[(size_t)col * N + n], g = s.G[(size_t)col * N + m];
+                    s.hband.vals[s.hband.off[blk] + (size_t)(k - s.hband.klo[blk]) * DSCE_RB + rl] =
+                        make_double2(q.x * g.x + q.y * g.y, q.x * g.y - q.y * g.x);
+                }
+            }
+    }
     // fused perfect-CSI IC tables (see SchemeK::pic_ok)
     {
         int md = 0;
@@ -405,6 +423,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.ph_val = dupload(c, hval);
     k.G = upload_band(c, s.gband, true);
     k.QH = upload_band(c, s.qband, true);
+    k.HD = upload_band(c, s.hband, true);
     k.q_start = dupload(c, qs);
     k.q_col = dupload(c, qcol);
     k.QL = s.QL;

@@ -131,6 +131,7 @@ struct SchemeK {
     const double2* ph_val;
     Band G;                       // N x LK
     Band QH;                      // LK x N (conj(Q)^T)
+    Band HD;                      // LK x (N * ntap): diag(Q'HG) coefficients, k = n * ntap + tau
     // perfect-CSI diag(D): Q columns compact (support start + QL values)
     const int* q_start;
     const double2* q_col;         // LK x QL

@@ -322,6 +322,17 @@ struct LoadSoA {
     __device__ __forceinline__ Regs load(int k, int lane) const { return p[(size_t)k * stride + lane]; }
     __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
 };
+// channel taps as the column operand of the diag(D) band: k = n * ntap + tau
+struct LoadTapInterleaved {
+    const double2* __restrict__ ir;    // [ntap][N][R]
+    int N, R, ntap;
+    typedef double2 Regs;
+    __device__ __forceinline__ Regs load(int k, int lane) const {
+        const int n = k / ntap, q = k - n * ntap;
+        return ir[((size_t)q * N + n) * R + lane];
+    }
+    __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
+};
 struct StoreSoA {
     double2* __restrict__ p;
     int stride;
@@ -605,32 +616,6 @@ __global__ void __launch_bounds__(64) k_channel_apply(ChannelK ch, int R, const 
     }
 }
 
-// a8: h = diag(Q' H G) (script:388-393) without forming D:
-// h[c] = sum_n conj(Q[n,c]) sum_tau IR[tau][n] G[n - d_tau, c]; grid (R/64, ceil(LK/16)).
-__global__ void __launch_bounds__(64) k_hdiag(SchemeK sk, ChannelK ch, int R, const double2* __restrict__ ir,
-                                              double2* __restrict__ h) {
-    const int rl = blockIdx.x * WAVE + threadIdx.x;
-    const int c0 = blockIdx.y * 16;
-    for (int c = c0; c < c0 + 16 && c < sk.LK; ++c) {
-        const int qs = sk.q_start[c], gs = sk.g_start[c];
-        const double2* __restrict__ qc = sk.q_col + (size_t)c * sk.QL;
-        const double2* __restrict__ gc = sk.g_col + (size_t)c * sk.GL;
-        double2 acc = make_double2(0.0, 0.0);
-        for (int i = 0; i < sk.QL; ++i) {
-            const int n = qs + i;
-            const double2 qv = qc[i];
-            if (n >= ch.N || (qv.x == 0.0 && qv.y == 0.0)) continue;
-            double2 hg = make_double2(0.0, 0.0);
-            for (int q = 0; q < ch.ntap; ++q) {
-                const int m = n - ch.tap_delay[q] - gs;
-                if (m >= 0 && m < sk.GL) c_fma(hg, ir[((size_t)q * ch.N + n) * R + rl], gc[m]);
-            }
-            c_fma(acc, c_conj(qv), hg);
-        }
-        h[(size_t)c * R + rl] = acc;
-    }
-}
-
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
                uint64_t rep0, McBuffers& b) {
     const int R = b.R;
@@ -639,7 +624,8 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
     // s = G x (script:376-378)
     launch_band(s, sk.G, R, nullptr, LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
     hipLaunchKernelGGL(k_channel_apply, dim3(R / WAVE, (ch.N + 63) / 64), dim3(WAVE), 0, s, ch, R, b.ir, b.ss, b.r0);
-    hipLaunchKernelGGL(k_hdiag, dim3(R / WAVE, (sk.LK + 15) / 16), dim3(WAVE), 0, s, sk, ch, R, b.ir, b.h);
+    // a8: h = diag(Q' H G) (script:388-393) without forming D: banded matvec over the taps
+    launch_band(s, sk.HD, R, nullptr, LoadTapInterleaved{b.ir, ch.N, R, ch.ntap}, StoreSoA{b.h, R});
 }
 
 // ---------------------------------------------------------------------------
@@ -657,10 +643,9 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, con
         const uint4 w = stream_block(seed, rep, STREAM_NOISE, (uint32_t)snr, (uint32_t)n);
         const double u1 = u53(w.x, w.y), u2 = u53(w.z, w.w);
         const double rad = sqrt(-2.0 * log(1.0 - u1));
-        double sn, cs;
-        sincos(TWO_PI * u2, &sn, &cs);
+        const double2 cz = cis_turns(u2);                     // (cos, sin)(2 pi u2), u2 in [0, 1)
         const double2 r = r0[(size_t)n * R + rl];
-        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * (rad * cs), r.y + sc * (rad * sn));
+        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * (rad * cz.x), r.y + sc * (rad * cz.y));
     }
 }
 
