@@ -188,7 +188,7 @@ def main():
         "config": {"workload": "C2: OFDM 24sc x 14sym, N=540, Jakes 500 km/h VehA, 256-QAM, 16 pilots, "
                                "7 SNR (10:5:40 dB) x (one-tap + 4 IC) x (MMSE + perfect CSI)",
                    "reps_per_step_per_gpu": B, "engine_batch": args.batch, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "kernel": "k_wpair (MMSE contraction, timed as k_wcontract)",
+        "roofline": {"bound": "mfma", "kernel": "k_wpair3 (pair-tile MMSE contraction, 3M; timed as k_wcontract)",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
                      "traffic": traffic, "launches": launches,
