@@ -107,11 +107,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one rank per GPU; DSCE_DIST_BACKEND=gloo + more ranks than GPUs rehearses
+        # the multi-rank path on a single-GPU box (ranks share device local % count)
+        device = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        dist.init_process_group(os.environ.get("DSCE_DIST_BACKEND", "nccl"))
 
     import numpy as np
     from dsce.configs import build_setup
@@ -119,7 +123,7 @@ def main():
 
     S = build_setup("default", schemes=("ofdm",))
     t_setup = time.perf_counter()
-    eng = build_engine(S, device=local if world > 1 else 0, batch=args.batch)
+    eng = build_engine(S, device=device, batch=args.batch)
     setup_s = time.perf_counter() - t_setup
     B = args.reps_per_step
     counts = np.zeros(eng.counter_shape(), dtype=np.int64)
