@@ -1162,44 +1162,51 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     // ping-pong W tiles: tile t+1's loads are issued before tile t's MFMAs;
-    // sched_barrier keeps the compiler from sinking them back to their uses
+    // sched_barrier keeps the compiler from sinking them back to their uses.
+    // RBP 24 runs two periods (6 tiles) per step so the buffers alternate
+    // without a register copy (a copy would wait on the just-issued loads).
     T3 A0, A1;
     D3 Da;
-    double2 vv[CPP];
+    double2 vv[CPP], vw[CPP];
+#define WSTEP(LD_T, LD_BUF, MMA_BUF, VV, TT)   \
+    ldt(LD_T, LD_BUF);                         \
+    __builtin_amdgcn_sched_barrier(0);         \
+    mma(MMA_BUF, Da);                          \
+    epi(Da, VV, TT{});                         \
+    __builtin_amdgcn_sched_barrier(0);
+    const int nper = ntile / PER;
     if (ntile > 0) ldt(0, A0);
-    for (int t0 = 0; t0 < ntile; t0 += PER) {
-        ldv(t0 / PER, vv);
-        const int tn = t0 + PER < ntile ? t0 + PER : t0;
-        if (PER == 3) {
-            ldt(t0 + 1, A1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(A0, Da);
-            epi(Da, vv, I0{});
-            __builtin_amdgcn_sched_barrier(0);
-            ldt(t0 + 2, A0);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(A1, Da);
-            epi(Da, vv, I1{});
-            __builtin_amdgcn_sched_barrier(0);
-            ldt(tn, A1);
-            __builtin_amdgcn_sched_barrier(0);
+    if (PER == 3) {
+        int per = 0;
+        for (; per + 1 < nper; per += 2) {
+            const int t0 = per * 3;
+            const int tn = t0 + 6 < ntile ? t0 + 6 : t0;
+            ldv(per, vv);
+            ldv(per + 1, vw);
+            WSTEP(t0 + 1, A1, A0, vv, I0)
+            WSTEP(t0 + 2, A0, A1, vv, I1)
+            WSTEP(t0 + 3, A1, A0, vv, I2)
+            WSTEP(t0 + 4, A0, A1, vw, I0)
+            WSTEP(t0 + 5, A1, A0, vw, I1)
+            WSTEP(tn, A0, A1, vw, I2)
+        }
+        if (per < nper) {                                   // odd period count: last period
+            const int t0 = per * 3;
+            ldv(per, vv);
+            WSTEP(t0 + 1, A1, A0, vv, I0)
+            WSTEP(t0 + 2, A0, A1, vv, I1)
             mma(A0, Da);
             epi(Da, vv, I2{});
-            __builtin_amdgcn_sched_barrier(0);
-            A0 = A1;
-        } else {
-            ldt(t0 + 1, A1);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(A0, Da);
-            epi(Da, vv, I0{});
-            __builtin_amdgcn_sched_barrier(0);
-            ldt(tn, A0);
-            __builtin_amdgcn_sched_barrier(0);
-            mma(A1, Da);
-            epi(Da, vv, I1{});
-            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        for (int t0 = 0; t0 < ntile; t0 += PER) {
+            const int tn = t0 + PER < ntile ? t0 + PER : t0;
+            ldv(t0 / PER, vv);
+            WSTEP(t0 + 1, A1, A0, vv, I0)
+            WSTEP(tn, A0, A1, vv, I1)
         }
     }
+#undef WSTEP
     const int row0 = P.row0[blk], nrows = P.nrows[blk];
 #pragma unroll
     for (int k = 0; k < NACC; ++k) {
