@@ -1100,6 +1100,60 @@ int dsce_get_correlation(dsce_ctx* ctx, int32_t id, double* r_hp, double* r_est,
     API_END
 }
 
+int dsce_tx_matrices(dsce_ctx* ctx, const dsce_tx_desc* d, double* G_out, double* Q_out) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!d || d->n_subcarriers <= 0 || d->n_symbols <= 0 || d->n_samples <= 0 || d->fft_size <= 0 ||
+        d->time_spacing <= 0 || (d->kind != 0 && d->kind != 1))
+        throw ApiError(DSCE_EINVAL, "invalid tx description");
+    if (d->kind == 1 && (!d->prototype || d->proto_len <= 0)) throw ApiError(DSCE_EINVAL, "FBMC needs the prototype");
+    if (d->kind == 0 && d->time_spacing - d->cyclic_prefix != d->fft_size)
+        throw ApiError(DSCE_EINVAL, "OFDM: time_spacing - cyclic_prefix must equal fft_size");
+    TxDesc t{};
+    t.kind = d->kind;
+    t.L = d->n_subcarriers;
+    t.K = d->n_symbols;
+    t.N = d->n_samples;
+    t.fft = d->fft_size;
+    t.ifb = d->intermediate_bin;
+    t.ts = d->time_spacing;
+    t.cp = d->cyclic_prefix;
+    t.zg = d->zero_guard;
+    t.proto = d->proto_len;
+    t.norm = d->norm;
+    t.phase0 = d->initial_phase;
+    t.rx_scale = d->rx_scale;
+    const size_t n = (size_t)t.N * t.L * t.K;
+    std::vector<void*> tmp;
+    try {
+        double* proto = nullptr;
+        if (t.kind == 1) {
+            DSCE_HIP_CHECK(hipMalloc((void**)&proto, t.proto * sizeof(double)));
+            tmp.push_back(proto);
+            DSCE_HIP_CHECK(hipMemcpy(proto, d->prototype, t.proto * sizeof(double), hipMemcpyHostToDevice));
+        }
+        double2 *G = nullptr, *Q = nullptr;
+        if (G_out) {
+            DSCE_HIP_CHECK(hipMalloc((void**)&G, n * sizeof(double2)));
+            tmp.push_back(G);
+        }
+        if (Q_out) {
+            DSCE_HIP_CHECK(hipMalloc((void**)&Q, n * sizeof(double2)));
+            tmp.push_back(Q);
+        }
+        setup_tx_matrix(ctx->stream, t, proto, G, Q);
+        DSCE_HIP_CHECK(hipGetLastError());
+        if (G_out) DSCE_HIP_CHECK(hipMemcpyAsync(G_out, G, n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+        if (Q_out) DSCE_HIP_CHECK(hipMemcpyAsync(Q_out, Q, n * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+        DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+        for (void* p : tmp) (void)hipFree(p);
+        throw;
+    }
+    for (void* p : tmp) DSCE_HIP_CHECK(hipFree(p));
+    API_END
+}
+
 int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out) {
     API_BEGIN
     check_ctx(ctx);

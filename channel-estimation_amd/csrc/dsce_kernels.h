@@ -91,6 +91,11 @@ void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const
 void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv);
 void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
                 const int* q_start, int QL, double2* rd /* packed, w_elems */);
+struct TxDesc {
+    int kind, L, K, N, fft, ifb, ts, cp, zg, proto;
+    double norm, phase0, rx_scale;
+};
+void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q);
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
                  double2* wp, long long wp_elems, int nslices, double* w3);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);

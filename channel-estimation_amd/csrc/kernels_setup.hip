@@ -373,4 +373,56 @@ void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long l
     if (w3) hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, wp, w3);
 }
 
+// G[n, l + L k] in closed form (OFDM.m:153-165, :184-203; FBMC.m:255-285,
+// :318-342) and Q = G * rx_scale with OFDM cyclic-prefix samples zeroed
+// (OFDM.m:205-218).  The IFFT of a unit impulse at bin b is
+// exp(j 2 pi b j / FFT) / FFT; the phase is reduced exactly in integers.
+__global__ void k_tx_matrix(TxDesc d, const double* __restrict__ proto, double2* __restrict__ G,
+                            double2* __restrict__ Q) {
+    const long long LK = (long long)d.L * d.K;
+    const long long total = LK * d.N;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int n = (int)(e % d.N), col = (int)(e / d.N);
+        const int l = col % d.L, k = col / d.L;
+        double2 g = make_double2(0.0, 0.0);
+        bool cp = false;
+        if (d.kind == 0) {                                   // OFDM
+            const int m = n - d.zg - k * d.ts;
+            const int body = d.ts - d.cp;                    // = FFT size
+            if (m >= 0 && m < d.ts) {
+                const int j = m >= d.cp ? m - d.cp : body - d.cp + m;
+                cp = m < d.cp;
+                const long long ph = ((long long)(l + d.ifb) * j) % d.fft;
+                double sn, cs;
+                sincospi(2.0 * (double)ph / (double)d.fft, &sn, &cs);
+                const double a = d.norm / (double)d.fft;
+                g = make_double2(a * cs, a * sn);
+            }
+        } else {                                             // FBMC Hermite-OQAM
+            int np_ = n - k * d.ts;
+            np_ %= d.N;
+            if (np_ < 0) np_ += d.N;                         // np.roll is circular
+            if (np_ < d.proto) {
+                const int row = (l + d.ifb) % d.fft;
+                const long long ph = ((long long)row * (np_ % d.fft)) % d.fft;
+                double sn, cs;
+                sincospi(2.0 * (double)ph / (double)d.fft, &sn, &cs);
+                // PhaseShift[l, 0] = exp(j pi/2 l) exp(j phase0); times j^k (FBMC.m:336)
+                double ps, pc;
+                sincos(0.5 * M_PI * (double)((l + k) & 3) + d.phase0, &ps, &pc);
+                const double a = proto[np_] * d.norm / (double)d.fft;
+                const double2 e1 = make_double2(cs, sn), e2 = make_double2(pc, ps);
+                g = make_double2(a * (e1.x * e2.x - e1.y * e2.y), a * (e1.x * e2.y + e1.y * e2.x));
+            }
+        }
+        if (G) G[e] = g;
+        if (Q) Q[e] = cp ? make_double2(0.0, 0.0) : make_double2(g.x * d.rx_scale, g.y * d.rx_scale);
+    }
+}
+
+void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q) {
+    hipLaunchKernelGGL(k_tx_matrix, dim3(4096), dim3(256), 0, s, d, proto, G, Q);
+}
+
 }  // namespace dsce

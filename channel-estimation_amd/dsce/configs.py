@@ -172,7 +172,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
             pilot_pos=np.flatnonzero(_col(pm_fbmc) == 1), data_pos=np.flatnonzero(_col(aux_pm) == 0),
             despread=False, real_detect=True, data_div=float(np.sqrt(aux.DataPowerReduction)),
             kappa=float(kappa), dpr=aux.DataPowerReduction, const=pam, considered_symbols=cm,
-            n_pilots=NP, n_data=nd, bits_slot=0, pilot_slot=0, extras=dict(iic=aux, pilot_matrix=aux_pm))
+            n_pilots=NP, n_data=nd, bits_slot=0, pilot_slot=0, extras=dict(iic=aux, pilot_matrix=aux_pm, modulation=fbmc))
     if "fbmc_cod" in schemes:
         cod = IIC("Coding", pm_fbmc, Dfbmc, 20, 2 * p2d)        # script:123-129
         kappa = cod.PilotToDataPowerOffset * cod.DataPowerReduction
@@ -185,7 +185,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
             pilot_pos=np.flatnonzero(_col(pm_fbmc) == 1), data_pos=np.arange(NP, cod.PrecodingMatrix.shape[1]),
             despread=True, real_detect=True, data_div=float(cod.DataPowerReduction),
             kappa=float(kappa), dpr=cod.DataPowerReduction, const=pam, considered_symbols=cm,
-            n_pilots=NP, n_data=nd, bits_slot=1, pilot_slot=0, extras=dict(iic=cod, pilot_matrix=pm_fbmc))
+            n_pilots=NP, n_data=nd, bits_slot=1, pilot_slot=0, extras=dict(iic=cod, pilot_matrix=pm_fbmc, modulation=fbmc))
     if "ofdm" in schemes:
         G_ofdm = ofdm.GetTXMatrix()
         Q_ofdm = ofdm.GetRXMatrix().conj().T                   # script:195
@@ -204,7 +204,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
             pilot_pos=np.flatnonzero(pmv == 1), data_pos=np.flatnonzero(pmv == 0),
             despread=False, real_detect=False, data_div=float(np.sqrt(dpr)),
             kappa=float(kappa), dpr=float(dpr), const=qam, considered_symbols=cm,
-            n_pilots=NP, n_data=ND_ofdm, bits_slot=2, pilot_slot=1, extras=dict(pilot_matrix=pm_ofdm, ofdm=ofdm))
+            n_pilots=NP, n_data=ND_ofdm, bits_slot=2, pilot_slot=1, extras=dict(pilot_matrix=pm_ofdm, ofdm=ofdm, modulation=ofdm))
 
     fD = velocity / 3.6 * 2.5e9 / 2.998e8                      # script:180
     chan = FastFading(SR, "VehicularA", N, fD, "Jakes", 200, 1, 1, 1)

@@ -20,7 +20,7 @@ EXPORTED = [
     "dsce_abi_version", "dsce_device_count", "dsce_create", "dsce_destroy", "dsce_last_error",
     "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
     "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
-    "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap",
+    "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
 ]
 
 
@@ -39,6 +39,14 @@ class SchemeDesc(C.Structure):
                 ("P", C.POINTER(C.c_double)), ("pilot_pos", C.POINTER(C.c_int32)),
                 ("data_pos", C.POINTER(C.c_int32)), ("considered", C.POINTER(C.c_uint8)),
                 ("symbols", C.POINTER(C.c_double))]
+
+
+class TxDesc(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("n_subcarriers", C.c_int32), ("n_symbols", C.c_int32),
+                ("n_samples", C.c_int32), ("fft_size", C.c_int32), ("intermediate_bin", C.c_int32),
+                ("time_spacing", C.c_int32), ("cyclic_prefix", C.c_int32), ("zero_guard", C.c_int32),
+                ("proto_len", C.c_int32), ("norm", C.c_double), ("initial_phase", C.c_double),
+                ("rx_scale", C.c_double), ("prototype", C.POINTER(C.c_double))]
 
 
 _lib = None
@@ -79,6 +87,7 @@ def load_library(path=None):
     lib.dsce_kernel_time.argtypes = [vp, C.c_char_p, i64p, dp]
     lib.dsce_work_model.argtypes = [vp, C.c_int32, dp, dp]
     lib.dsce_mmse_onetap.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, dp, C.c_int32, dp]
+    lib.dsce_tx_matrices.argtypes = [vp, C.POINTER(TxDesc), dp, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -193,6 +202,35 @@ class Engine:
         self._chk(self.lib.dsce_bits_per_rep(self.h, int(sid), b.ctypes.data_as(C.POINTER(C.c_int64))),
                   "dsce_bits_per_rep")
         return b
+
+    # -- setup producers (row f1) ----------------------------------------------
+    def tx_matrices(self, mod):
+        """(G, Q) of a dsce.modulation.OFDM / FBMC object computed on the GPU:
+        G = mod.GetTXMatrix(), Q = mod.GetRXMatrix()' (script:191-195)."""
+        from dsce.modulation import FBMC, OFDM
+        Nr, Impl, PHY = mod.Nr, mod.Implementation, mod.PHY
+        L, K, N = Nr.Subcarriers, Nr.MCSymbols, Nr.SamplesTotal
+        proto = None
+        if isinstance(mod, OFDM):
+            if PHY.TransmitRealSignal:
+                raise DsceError("GetTXMatrix is not supported for PHY.TransmitRealSignal == true")
+            d = TxDesc(0, L, K, N, Impl.FFTSize, Impl.IntermediateFrequency, Impl.TimeSpacing, Impl.CyclicPrefix,
+                       Impl.ZeroGuardSamples, 0, Impl.NormalizationFactor, 0.0,
+                       L * PHY.SubcarrierSpacing / PHY.SamplingRate, None)
+        elif isinstance(mod, FBMC):
+            if PHY.TransmitRealSignal:
+                raise DsceError("real-signal FBMC is not supported")
+            proto = np.ascontiguousarray(mod.PrototypeFilter.TimeDomain, dtype=np.float64)
+            d = TxDesc(1, L, K, N, Impl.FFTSize, Impl.IntermediateFrequency, Impl.TimeSpacing, 0, 0, proto.size,
+                       Impl.NormalizationFactor, Impl.InitialPhaseShift, L / (PHY.SamplingRate * PHY.TimeSpacing),
+                       _dptr(proto))
+        else:
+            raise TypeError("OFDM or FBMC object expected")
+        G = np.zeros(2 * N * L * K)
+        Q = np.zeros(2 * N * L * K)
+        self._chk(self.lib.dsce_tx_matrices(self.h, C.byref(d), _dptr(G), _dptr(Q)), "dsce_tx_matrices")
+        shape = (N, L * K)
+        return (G.view(np.complex128).reshape(shape, order="F"), Q.view(np.complex128).reshape(shape, order="F"))
 
     # -- probes ----------------------------------------------------------------
     def channel_impulse_response(self, seed, rep):

@@ -24,6 +24,7 @@
  *                            method 'MMSE' (PSACE.m:128-129 stub): h_hat = diag(sum_p W_p hP_p),
  *                            script:417-428
  *   dsce_get_correlation / dsce_get_W <- R_hP*, W_MMSE_*          script:210-313 (parity probes)
+ *   dsce_tx_matrices      <- OFDM/FBMC.GetTXMatrix / GetRXMatrix OFDM.m:184-218, FBMC.m:318-354
  *
  * Conventions
  *  - Return 0 on success, a negative DSCE_E* code on failure; the message is
@@ -109,6 +110,29 @@ typedef struct {
     const double* symbols;      /* M complex, SymbolMapping sorted by bit label */
 } dsce_scheme_desc;
 
+/* On-GPU producer of the transmit / receive matrices,
+ * replacing Modulation.OFDM/FBMC.GetTXMatrix / GetRXMatrix (OFDM.m:184-218,
+ * FBMC.m:318-354): column l + L k of G is the modulated unit impulse of
+ * subcarrier l, symbol k, evaluated in closed form per element instead of L
+ * Modulation() calls; Q = GetRXMatrix' = G * rx_scale with the OFDM cyclic-
+ * prefix samples zeroed (OFDM.m:216-217). */
+typedef struct {
+    int32_t kind;               /* 0 = OFDM, 1 = FBMC Hermite-OQAM             */
+    int32_t n_subcarriers;      /* L                                          */
+    int32_t n_symbols;          /* K                                          */
+    int32_t n_samples;          /* N = Nr.SamplesTotal                         */
+    int32_t fft_size;           /* Implementation.FFTSize                      */
+    int32_t intermediate_bin;   /* Implementation.IntermediateFrequency       */
+    int32_t time_spacing;       /* Implementation.TimeSpacing (samples)        */
+    int32_t cyclic_prefix;      /* OFDM Implementation.CyclicPrefix            */
+    int32_t zero_guard;         /* OFDM Implementation.ZeroGuardSamples        */
+    int32_t proto_len;          /* FBMC Nr.SamplesPrototypeFilter              */
+    double norm;                /* Implementation.NormalizationFactor          */
+    double initial_phase;       /* FBMC Implementation.InitialPhaseShift       */
+    double rx_scale;            /* GetRXMatrix scale (OFDM L F/SR, FBMC L/(SR T)) */
+    const double* prototype;    /* FBMC PrototypeFilter.TimeDomain (proto_len) */
+} dsce_tx_desc;
+
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
 
@@ -141,6 +165,9 @@ int dsce_bits_per_rep(dsce_ctx* ctx, int32_t scheme_id, int64_t* bits2);
  * (column-major), h_out LK x n_units complex; variant 0 = W, 1 = W0. */
 int dsce_mmse_onetap(dsce_ctx* ctx, int32_t scheme_id, int32_t snr_index, int32_t variant, const double* hp_ls,
                      int32_t n_units, double* h_out);
+
+/* G (and Q, each optional) as N x LK complex column-major host buffers. */
+int dsce_tx_matrices(dsce_ctx* ctx, const dsce_tx_desc* desc, double* G_out, double* Q_out);
 
 /* ---- parity probes (same kernels as dsce_run) ---------------------------- */
 /* ImpulseResponse of realisation `rep`: N x n_taps complex, column-major. */

@@ -226,3 +226,20 @@ def test_stage_variants_agree(monkeypatch, name):
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=var)
         monkeypatch.delenv(var)
     eng.close()
+
+
+@pytest.mark.parametrize("name", ["default", "c5", "paper"])
+def test_tx_matrices_on_gpu_match_host_mirror(name):
+    """Row f1: G and Q = GetRXMatrix' produced on the GPU in closed form equal
+    the host mirror's L Modulation() calls (OFDM.m:184-218, FBMC.m:318-354)."""
+    from dsce.engine import Engine
+    from dsce.configs import build_setup
+    S = build_setup(name, schemes=("fbmc_aux", "ofdm"))
+    eng = Engine()
+    for key in ("fbmc_aux", "ofdm"):
+        sc = S.schemes[key]
+        G, Q = eng.tx_matrices(sc.extras["modulation"])
+        scale = np.abs(sc.G).max()
+        np.testing.assert_allclose(G, sc.G, rtol=0, atol=1e-13 * scale, err_msg=key)
+        np.testing.assert_allclose(Q, sc.Q, rtol=0, atol=1e-13 * np.abs(sc.Q).max(), err_msg=key)
+    eng.close()
