@@ -190,7 +190,8 @@ class PilotSymbolAidedChannelEstimation:
 
     Supported interpolation methods: 'FullAverage', 'MovingBlockAverage',
     'linear'/'nearest' (MATLAB ``scatteredInterpolant`` semantics with
-    extrapolation restated on the host: CPU-only, config 1 plumbing), and
+    extrapolation restated on the host: CPU-only, config 1 plumbing,
+    ``_scattered``), and
     'MMSE' — the slot the reference leaves as ``error('Needs to be
     implemented')``.  For 'MMSE' the object carries the engine handle
     (``set_mmse_engine``) and ``ChannelInterpolation`` returns the MMSE
@@ -280,15 +281,64 @@ class PilotSymbolAidedChannelEstimation:
             return np.ones(self.PilotMatrix.shape) * np.mean(LS)
         if m == "MovingBlockAverage":
             return (self.InterpolationMatrix @ LS).reshape(self.PilotMatrix.shape, order="F")
-        if m in ("linear", "nearest", "natural"):
-            # scatteredInterpolant with extrapolation is config-1 CPU plumbing
-            # (SURVEY.md §8f row f4); not part of the doubly-selective hot path.
-            raise NotImplementedError("scatteredInterpolant interpolation is not provided (SURVEY §8f f4)")
+        if m in ("linear", "nearest"):
+            return self._scattered(LS, m)
+        if m == "natural":
+            raise NotImplementedError("natural-neighbour interpolation is not provided")
         if m == "MMSE":
             if self._mmse is None:
                 raise RuntimeError("MMSE interpolation needs an engine: call set_mmse_engine()")
             return self._mmse(LS)
         raise ValueError("Interpolation method not implemented")
+
+    def _scattered(self, LS, method):
+        """``scatteredInterpolant(x_pilot, y_pilot, v, method)`` evaluated on the
+        full grid (PSACE.m:75-77, :119-121), config-1 CPU plumbing (SURVEY §8f
+        f4).  'linear': barycentric on the Delaunay triangulation of the pilot
+        positions; outside the convex hull the affine function of the boundary
+        triangle nearest to the query point (MATLAB's default linear
+        extrapolation; exact for affine fields).  'nearest': value of the
+        closest pilot (its default extrapolation too)."""
+        from scipy.spatial import Delaunay, cKDTree
+        PM = self.PilotMatrix
+        # [x, y] = find(PilotMatrix): column-major, 1-based (row, column)
+        rows, cols = np.nonzero(PM.T)
+        pts = np.stack([cols + 1.0, rows + 1.0], axis=1)
+        nL, nK = PM.shape
+        gx, gy = np.meshgrid(np.arange(1, nL + 1.0), np.arange(1, nK + 1.0), indexing="ij")
+        q = np.stack([gx.ravel(), gy.ravel()], axis=1)
+        if method == "nearest":
+            _, idx = cKDTree(pts).query(q)
+            return LS[idx].reshape(nL, nK)
+        tri = Delaunay(pts)
+        simp = tri.find_simplex(q)
+        out = np.empty(q.shape[0], dtype=complex)
+
+        def affine_eval(si, xy):
+            T = tri.transform[si]
+            b = T[:2].dot(xy - T[2])
+            w = np.array([b[0], b[1], 1.0 - b[0] - b[1]])
+            return w.dot(LS[tri.simplices[si]])
+        # boundary edges of the hull and the triangle owning each
+        hull_edges = []
+        for si, nb in enumerate(tri.neighbors):
+            for k in range(3):
+                if nb[k] == -1:
+                    e = [tri.simplices[si][j] for j in range(3) if j != k]
+                    hull_edges.append((e[0], e[1], si))
+        for i, xy in enumerate(q):
+            si = simp[i]
+            if si < 0:
+                best, bd = None, np.inf
+                for a, b, s_ in hull_edges:
+                    pa, pb = pts[a], pts[b]
+                    t = np.clip(np.dot(xy - pa, pb - pa) / np.dot(pb - pa, pb - pa), 0.0, 1.0)
+                    d = np.sum((pa + t * (pb - pa) - xy) ** 2)
+                    if d < bd - 1e-12:
+                        best, bd = s_, d
+                si = best
+            out[i] = affine_eval(si, xy)
+        return out.reshape(nL, nK)
 
     def GetAuxiliaryMatrix(self, NrAuxiliarySymbols):
         """PSACE.m:137-169."""

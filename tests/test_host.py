@@ -88,3 +88,26 @@ def test_precoders_cancel_pilot_interference():
     assert aux.NrDataSymbols == 640 and cod.NrDataSymbols == 688 and aux.NrAuxiliarySymbols == 64
     o = S.schemes["ofdm"]
     assert o.kappa == pytest.approx(2 * o.dpr) and o.dpr == pytest.approx(336 / (16 * 2 + 320))
+
+
+def test_psace_scattered_interpolation():
+    """Config-1 plumbing: 'linear' scatteredInterpolant on the
+    pilot grid is exact for affine channels inside and outside the pilot hull
+    (SimpleVersion_DoublyFlat.m:47-66 uses Diamond pilots + 'linear'); 'nearest'
+    returns the closest pilot's LS value."""
+    from dsce.estimation import PilotSymbolAidedChannelEstimation as PSACE
+    for pattern, params in (("Diamond", [[12, 4], [15, 4]]), ("Rectangular", [[24, 6], [14, 7]])):
+        est = PSACE(pattern, params, "linear")
+        PM = est.PilotMatrix
+        nL, nK = PM.shape
+        f, t = np.meshgrid(np.arange(1, nL + 1), np.arange(1, nK + 1), indexing="ij")
+        H = (0.3 - 0.2j) + (0.05 + 0.01j) * f - (0.02 - 0.03j) * t
+        ls = H.reshape(-1, order="F")[PM.reshape(-1, order="F") == 1]
+        np.testing.assert_allclose(est.ChannelInterpolation(ls), H, rtol=0, atol=1e-12)
+        near = PSACE(pattern, params, "nearest").ChannelInterpolation(ls)
+        np.testing.assert_allclose(near[PM == 1], H[PM == 1], rtol=0, atol=1e-15)
+        pr, pc = np.nonzero(PM)
+        for (r, c) in ((0, 0), (nL - 1, nK - 1), (nL // 2, nK // 3)):
+            d = (pr - r) ** 2 + (pc - c) ** 2
+            assert np.isclose(d[np.argmin(d)], ((pr - r) ** 2 + (pc - c) ** 2)[
+                np.argmin(np.abs(H[pr, pc] - near[r, c]))])
