@@ -96,6 +96,10 @@ struct Scheme {
     PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
     bool mmse_ready = false;
+    // one-tap estimator given as an interpolation matrix (dsce_set_interpolation,
+    // PSACE.m:115-133) instead of the MMSE W: LK x NP, row-major [c][p] like Wd
+    bool interp = false;
+    std::vector<double2> interp_I;
     int64_t bits_all = 0, bits_noedge = 0;
     std::vector<int> g_start, q_start;
     int GL = 0, QL = 0;
@@ -564,6 +568,20 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
 }
 
 // ---------------------------------------------------------------------------
+// Interpolation estimator (dsce_set_interpolation): the one-tap channel of every
+// stage is I hP, held in the Wd slots [var][snr] so the stage kernels and
+// dsce_mmse_onetap use it unchanged; there is no W, so no IC iterations.
+void upload_interp(dsce_ctx* c, Scheme& s) {
+    if (s.Wd) free_alloc(c, s.Wd);
+    s.Wd = nullptr;
+    const int nsl = 2 * std::max(c->nsnr, 1);
+    std::vector<double2> rep((size_t)nsl * s.interp_I.size());
+    for (int i = 0; i < nsl; ++i) std::copy(s.interp_I.begin(), s.interp_I.end(), rep.begin() + (size_t)i * s.interp_I.size());
+    s.Wd = dupload(c, rep);
+    s.mmse_ready = c->nsnr > 0;
+}
+
+// ---------------------------------------------------------------------------
 void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
     hipStream_t st = c->stream;
     const int N = s.N, LK = s.LK, NP = s.d.n_pilots, Nsym = s.d.n_tx_symbols, nsnr = c->nsnr;
@@ -595,6 +613,9 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         int* dpil = (int*)talloc(NP * sizeof(int));
         DSCE_HIP_CHECK(hipMemcpy(dpil, s.pilot_pos.data(), NP * sizeof(int), hipMemcpyHostToDevice));
         double* j0tab = (double*)talloc((2 * N - 1) * sizeof(double));
+        if (c->ch.model >= 2 && c->ch.fD > 0)     // FastFading.m:331-336: no TimeCorrelation for 'Discrete-*'
+            throw ApiError(DSCE_EINVAL, "the time correlation (and so the MMSE estimator) is undefined for a "
+                                        "discrete Doppler spectrum (FastFading.m:321-336)");
         setup_time_correlation(st, N, c->ch.fD, c->ch.dt, c->ch.model, j0tab);
         SetupArgs a{};
         a.N = N;
@@ -914,7 +935,7 @@ int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
     check_ctx(ctx);
     if (!d || !d->pdp_norm || d->n_samples <= 1 || d->n_taps <= 0 || d->n_paths <= 0 || d->sampling_rate <= 0)
         throw ApiError(DSCE_EINVAL, "invalid channel description");
-    if (d->doppler_model != 0 && d->doppler_model != 1) throw ApiError(DSCE_EINVAL, "doppler_model must be 0 or 1");
+    if (d->doppler_model < 0 || d->doppler_model > 3) throw ApiError(DSCE_EINVAL, "doppler_model must be 0..3");
     if (!ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "set the channel before adding schemes");
     ChannelK ch{};
     ch.N = d->n_samples;
@@ -933,8 +954,33 @@ int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
         }
     }
     if (nt == 0) throw ApiError(DSCE_EINVAL, "power delay profile is all zero");
-    if (d->max_doppler <= 0) throw ApiError(DSCE_EINVAL, "max_doppler must be > 0 (time-variant channel)");
+    if (!(d->max_doppler >= 0)) throw ApiError(DSCE_EINVAL, "max_doppler must be >= 0");
     ch.ntap = nt;
+    if (ch.model >= 2 && ch.fD > 0) {
+        // discrete Doppler spectrum, FastFading.m:153-177
+        const double df = d->sampling_rate / d->n_samples;
+        if (ch.fD / df <= 0.5) {
+            ch.fD = 0.0;                                   // FastFading.m:153-156: velocity set to zero
+        } else {
+            const int nd = (int)ceil(ch.fD / df);
+            if (2 * nd + 1 > d->n_samples) throw ApiError(DSCE_EINVAL, "discrete Doppler spectrum wider than N");
+            std::vector<double> ip(2 * nd + 2), spec(2 * nd + 1);
+            for (int i = 0; i < 2 * nd + 2; ++i) {
+                double v = df * ((double)(i - nd - 1) + 0.5);
+                if (v <= -ch.fD) v = -ch.fD;
+                if (v >= ch.fD) v = ch.fD;
+                ip[i] = v;
+            }
+            double sum = 0.0;
+            for (int i = 0; i < 2 * nd + 1; ++i) {
+                spec[i] = ch.model == 2 ? asin(ip[i + 1] / ch.fD) - asin(ip[i] / ch.fD) : ip[i + 1] - ip[i];
+                sum += spec[i];
+            }
+            for (auto& v : spec) v = sqrt(v / sum);
+            ch.nd = nd;
+            ch.sqrt_dspec = dupload(ctx, spec);
+        }
+    }
     ctx->ch = ch;
     ctx->chan_set = true;
     API_END
@@ -944,11 +990,17 @@ int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_
     API_BEGIN
     check_ctx(ctx);
     if (!pn_time || n_snr <= 0 || n_iter < 0) throw ApiError(DSCE_EINVAL, "invalid SNR list");
+    for (auto& s : ctx->schemes)
+        if (s->k.noise_slot > 0 && n_snr > 256) throw ApiError(DSCE_EINVAL, "at most 256 SNR points with noise slots");
     ctx->pn.assign(pn_time, pn_time + n_snr);
     ctx->nsnr = n_snr;
     ctx->niter = n_iter;
+    if (ctx->d_pn) free_alloc(ctx, ctx->d_pn);
     ctx->d_pn = dupload(ctx, ctx->pn);
-    for (auto& s : ctx->schemes) s->mmse_ready = false;
+    for (auto& s : ctx->schemes) {
+        s->mmse_ready = false;
+        if (s->interp) upload_interp(ctx, *s);
+    }
     const size_t n = ctx->schemes.size() * 4 * (size_t)n_snr * (n_iter + 1);
     ctx->counters_n = 0;
     (void)n;
@@ -1007,7 +1059,8 @@ int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold) {
     check_ctx(ctx);
     if (ctx->nsnr <= 0) throw ApiError(DSCE_ESTATE, "dsce_set_snr first");
     if (ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "no scheme added");
-    for (auto& s : ctx->schemes) build_mmse(ctx, *s, zero_threshold);
+    for (auto& s : ctx->schemes)
+        if (!s->interp) build_mmse(ctx, *s, zero_threshold);
     API_END
 }
 
@@ -1021,8 +1074,12 @@ int dsce_set_batch(dsce_ctx* ctx, int32_t reps) {
 
 static void prepare_run(dsce_ctx* ctx) {
     if (ctx->schemes.empty()) throw ApiError(DSCE_ESTATE, "no scheme added");
-    for (auto& s : ctx->schemes)
+    for (auto& s : ctx->schemes) {
         if (!s->mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+        if (s->interp && ctx->niter > 0)
+            throw ApiError(DSCE_ESTATE, "interference-cancellation iterations need the MMSE estimator (n_iter must be 0 "
+                                        "with an interpolation estimator)");
+    }
     const size_t n = ctx->schemes.size() * 4 * (size_t)ctx->nsnr * (ctx->niter + 1);
     if (ctx->counters_n != n) {
         ctx->d_counters = dalloc<unsigned long long>(ctx, n);
@@ -1094,6 +1151,7 @@ int dsce_get_correlation(dsce_ctx* ctx, int32_t id, double* r_hp, double* r_est,
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
     if (!s.mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    if (s.interp) throw ApiError(DSCE_ESTATE, "scheme uses an interpolation estimator (no correlation matrices)");
     if (r_hp) memcpy(r_hp, s.R_hP.data(), s.R_hP.size() * sizeof(double2));
     if (r_est) memcpy(r_est, s.R_est.data(), s.R_est.size() * sizeof(double2));
     if (r_noi) memcpy(r_noi, s.R_noI.data(), s.R_noI.size() * sizeof(double2));
@@ -1159,6 +1217,7 @@ int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out)
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
     if (!s.mmse_ready) throw ApiError(DSCE_ESTATE, "dsce_build_mmse first");
+    if (!s.W) throw ApiError(DSCE_ESTATE, "scheme uses an interpolation estimator (no MMSE W)");
     if (k < 0 || k >= ctx->nsnr || var < 0 || var > 1 || !w_out) throw ApiError(DSCE_EINVAL, "bad W index");
     std::vector<double2> packed(s.w_elems);
     DSCE_HIP_CHECK(hipMemcpy(packed.data(), s.W + ((size_t)var * ctx->nsnr + k) * s.w_elems,
@@ -1230,6 +1289,38 @@ int dsce_mmse_onetap(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, const do
     }
     DSCE_HIP_CHECK(hipFree(dp));
     DSCE_HIP_CHECK(hipFree(dh));
+    API_END
+}
+
+int dsce_set_noise_slot(dsce_ctx* ctx, int32_t id, int32_t slot) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (slot < 0 || slot > 255) throw ApiError(DSCE_EINVAL, "noise slot must be 0..255");
+    if (slot > 0 && ctx->nsnr > 256) throw ApiError(DSCE_EINVAL, "at most 256 SNR points with noise slots");
+    s.k.noise_slot = slot;
+    API_END
+}
+
+int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!I) throw ApiError(DSCE_EINVAL, "null interpolation matrix");
+    const int LK = s.LK, NP = s.d.n_pilots;
+    s.interp_I.assign((size_t)LK * NP, make_double2(0, 0));
+    for (int c = 0; c < LK; ++c)
+        for (int p = 0; p < NP; ++p) s.interp_I[(size_t)c * NP + p] = cx(I, (size_t)p * LK + c);   // column-major in
+    if (s.W) {
+        free_alloc(ctx, s.W);
+        s.W = nullptr;
+    }
+    if (s.Wp) free_alloc(ctx, s.Wp);
+    if (s.Wp3) free_alloc(ctx, s.Wp3);
+    s.Wp = nullptr;
+    s.Wp3 = nullptr;
+    s.interp = true;
+    upload_interp(ctx, s);
     API_END
 }
 

@@ -111,6 +111,7 @@ struct PairBand {
 // ---------------------------------------------------------------------------
 struct SchemeK {
     int N, LK, Nsym, NP, ND, M, mbits, despread, real_detect;
+    int noise_slot;               // AWGN sub-stream group (include/dsce.h NOISE)
     double inv_sqrt_kappa, data_div;
     const int* pilot_pos;
     const int* data_pos;
@@ -163,8 +164,10 @@ struct ChannelK {
     int N, ntap;                  // ntap = number of non-zero taps
     int tap_delay[DSCE_MAX_TAPS];
     double sqrt_pdp[DSCE_MAX_TAPS];
-    double fD, dt;
-    int paths, model;
+    double fD, dt;                // fD == 0: time-invariant block fading (FastFading.m:241-246)
+    int paths, model;             // model: 0 Jakes, 1 Uniform, 2 Discrete-Jakes, 3 Discrete-Uniform
+    int nd;                       // discrete models: Doppler bins f = -nd..nd (FastFading.m:161)
+    const double* sqrt_dspec;     // discrete models: sqrt(DiscreteDopplerSpectrum), 2 nd + 1 (device)
 };
 
 // host-side launch helpers (defined in the .hip translation units)

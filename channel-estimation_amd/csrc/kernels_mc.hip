@@ -245,7 +245,91 @@ static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uin
                        ir);
 }
 
+// Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
+// u2 = u53(w2,w3), (re, im) = sqrt(-2 log(1-u1)) (cos, sin)(2 pi u2).
+__device__ __forceinline__ double2 normal_pair(uint4 w) {
+    const double u1 = u53(w.x, w.y), u2 = u53(w.z, w.w);
+    const double rad = sqrt(-2.0 * log(1.0 - u1));
+    const double2 cz = cis_turns(u2);                         // u2 in [0, 1)
+    return make_double2(rad * cz.x, rad * cz.y);
+}
+
+// ---------------------------------------------------------------------------
+// a2 (MaximumDopplerShift == 0): time-invariant block fading, FastFading.m:241-246:
+// IR[tap] = 1/sqrt(2) sqrt(PDPn[tap]) (randn + j randn), one value per
+// realisation that GetConvolutionMatrix repeats over all N samples
+// (FastFading.m:288-291).  With the 'Flat' PDP this is the doubly-flat
+// h = sqrt(1/2) (randn + j randn) of SimpleVersion_DoublyFlat.m:123.
+// RNG: THETA stream, sub 0, counter = non-zero tap index.  grid (R/64,
+// ceil(N/64), ntap), lane = realisation.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_static(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+                                               double2* __restrict__ ir) {
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const int q = blockIdx.z;
+    const double2 z = normal_pair(stream_block(seed, rep0 + (uint64_t)rl, STREAM_THETA, 0, (uint32_t)q));
+    const double c = (1.0 / sqrt(2.0)) * ch.sqrt_pdp[q];
+    const double2 v = make_double2(c * z.x, c * z.y);
+    const int n0 = blockIdx.y * 64;
+    for (int n = n0; n < n0 + 64 && n < ch.N; ++n) ir[((size_t)q * ch.N + n) * R + rl] = v;
+}
+
+// ---------------------------------------------------------------------------
+// a2, 'Discrete-Jakes' / 'Discrete-Uniform' (FastFading.m:203-221): the IFFT of
+// [sqrt(S(nd+1:end)) .* G1; zeros; sqrt(S(1:nd)) .* G2] with
+// G = N/sqrt(2) (randn + j randn) sqrt(PDPn) has only the 2 nd + 1 Doppler bins
+// f = -nd..nd non-zero, so it is evaluated directly:
+//   IR[n, tap] = sum_f c_f exp(j 2 pi f n / N),
+//   c_f = sqrt(S_f) sqrt(PDPn[tap]) / sqrt(2) (re_f + j im_f)
+// (the ifft's 1/N cancels the N of G).  RNG: THETA stream, sub 1, counter
+// (f + nd) + (2 nd + 1) tap, Box-Muller pair.  Lane = realisation, DCH samples
+// per lane: exact phase (f n mod N in integers) at the chunk start, then
+// rotations.  grid (R/64, ceil(N/DCH), ntap).
+// ---------------------------------------------------------------------------
+static constexpr int DCH = 16;
+__global__ void __launch_bounds__(64) k_discrete(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+                                                 double2* __restrict__ ir) {
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const int q = blockIdx.z;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    const int n0 = blockIdx.y * DCH;
+    const int nb = 2 * ch.nd + 1;
+    double2 acc[DCH];
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) acc[i] = make_double2(0.0, 0.0);
+    const double g = ch.sqrt_pdp[q] / sqrt(2.0);
+    for (int b = 0; b < nb; ++b) {
+        const int f = b - ch.nd;
+        const double2 z0 = normal_pair(stream_block(seed, rep, STREAM_THETA, 1, (uint32_t)(b + nb * q)));
+        const double a = ch.sqrt_dspec[b] * g;
+        const double2 cf = make_double2(a * z0.x, a * z0.y);
+        const long long m = (((long long)f * n0) % ch.N + ch.N) % ch.N;
+        double2 z = c_mul(cf, cis_turns((double)m / (double)ch.N));
+        const double2 w = cis_turns((double)f / (double)ch.N);
+#pragma unroll
+        for (int i = 0; i < DCH; ++i) {
+            acc[i].x += z.x;
+            acc[i].y += z.y;
+            if (i + 1 < DCH) z = c_mul_fma(z, w);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < DCH; ++i) {
+        const int n = n0 + i;
+        if (n < ch.N) ir[((size_t)q * ch.N + n) * R + rl] = acc[i];
+    }
+}
+
 void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+    if (ch.fD == 0.0) {
+        hipLaunchKernelGGL(k_static, dim3(R / WAVE, (ch.N + 63) / 64, ch.ntap), dim3(WAVE), 0, s, ch, seed, rep0, R, ir);
+        return;
+    }
+    if (ch.model >= 2) {
+        hipLaunchKernelGGL(k_discrete, dim3(R / WAVE, (ch.N + DCH - 1) / DCH, ch.ntap), dim3(WAVE), 0, s, ch, seed,
+                           rep0, R, ir);
+        return;
+    }
     int jch = (ch.N + WAVE - 1) / WAVE;           // samples per lane: one wave covers N when N <= 1024
     if (jch > JCH_MAX) jch = JCH_MAX;
     switch (jch) {
@@ -649,8 +733,10 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 
 // ---------------------------------------------------------------------------
 // a12: r = r0 + noise (script:397-403), lane = unit; grid (U/64, ceil(N/64)).
+// Noise sub-stream snr + 256 * slot (slot: schemes drawing separate noise, e.g.
+// n_FBMC / n_OFDM of SimpleVersion_DoublyFlat.m:125-126).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, const double* __restrict__ pn, uint64_t seed,
+__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int slot, const double* __restrict__ pn, uint64_t seed,
                                               uint64_t rep0, const double2* __restrict__ r0,
                                               double2* __restrict__ rbuf) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
@@ -659,18 +745,15 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, con
     const double sc = sqrt(pn[snr] / 2.0);
     const int n0 = blockIdx.y * 64;
     for (int n = n0; n < n0 + 64 && n < N; ++n) {
-        const uint4 w = stream_block(seed, rep, STREAM_NOISE, (uint32_t)snr, (uint32_t)n);
-        const double u1 = u53(w.x, w.y), u2 = u53(w.z, w.w);
-        const double rad = sqrt(-2.0 * log(1.0 - u1));
-        const double2 cz = cis_turns(u2);                     // (cos, sin)(2 pi u2), u2 in [0, 1)
+        const double2 z = normal_pair(stream_block(seed, rep, STREAM_NOISE, (uint32_t)(snr + 256 * slot), (uint32_t)n));
         const double2 r = r0[(size_t)n * R + rl];
-        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * (rad * cz.x), r.y + sc * (rad * cz.y));
+        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * z.x, r.y + sc * z.y);
     }
 }
 
 void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
                      uint64_t rep0, McBuffers& b) {
-    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, pn, seed, rep0,
+    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, sk.noise_slot, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)
     launch_band(s, sk.QH, b.U, nullptr, LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});

@@ -20,6 +20,10 @@ __global__ void k_time_correlation(int N, double fD, double dt, int model, doubl
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 2 * N - 1) return;
     const double t = dt * (double)(i - (N - 1));
+    if (fD == 0.0) {                       // time-invariant channel: FastFading.m:338-339
+        tab[i] = 1.0;
+        return;
+    }
     tab[i] = model == 0 ? j0(((M_PI * 2.0) * fD) * t) : (t == 0.0 ? 1.0 : sin(M_PI * (2.0 * fD * t)) / (M_PI * (2.0 * fD * t)));
 }
 

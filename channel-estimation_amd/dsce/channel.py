@@ -75,8 +75,14 @@ def quantise_pdp(pdp, sampling_rate):
 
 class FastFading:
     """``Channel.FastFading(SR, PDP, N, fD, DopplerModel, Paths, nTx, nRx, warn)``
-    (FastFading.m:25-192).  Single-antenna (1x1) and the continuous Doppler
-    models 'Jakes' / 'Uniform' are the engine-backed configurations."""
+    (FastFading.m:25-192), single antenna (1x1).  Engine-backed Doppler models:
+    'Jakes' / 'Uniform' (sum of sinusoids, FastFading.m:222-238),
+    'Discrete-Jakes' / 'Discrete-Uniform' (IFFT of the discrete Doppler
+    spectrum, FastFading.m:158-177, :203-221) and MaximumDopplerShift == 0
+    (time-invariant block fading, FastFading.m:241-246; with the 'Flat' PDP the
+    doubly-flat channel of SimpleVersion_DoublyFlat.m:123)."""
+
+    MODELS = {"Jakes": 0, "Uniform": 1, "Discrete-Jakes": 2, "Discrete-Uniform": 3}
 
     def __init__(self, SamplingRate, PowerDelayProfile, SamplesTotal, MaximumDopplerShift,
                  DopplerModel, Paths, nTxAntennas=1, nRxAntennas=1, WarningIfSampleRateDoesNotMatch=False):
@@ -92,8 +98,23 @@ class FastFading:
             self.MaximumDopplerShift = 0.0
         self.PowerDelayProfile, self.PowerDelayProfileNormalized = quantise_pdp(PowerDelayProfile, self.SamplingRate)
         self.IndexDelayTaps = np.flatnonzero(self.PowerDelayProfile)   # FastFading.m:131 (0-based)
-        if DopplerModel not in ("Jakes", "Uniform"):
-            raise ValueError("Doppler spectrum not supported by the engine: %s" % DopplerModel)
+        if DopplerModel not in self.MODELS:
+            raise ValueError("Doppler spectrum not supported: %s" % DopplerModel)
+        self.UseDiscreteDopplerSpectrum = False
+        if DopplerModel.startswith("Discrete") and self.MaximumDopplerShift > 0:
+            df = self.SamplingRate / self.SamplesTotal
+            if self.MaximumDopplerShift / df <= 0.5:               # FastFading.m:153-156
+                self.MaximumDopplerShift = 0.0
+            else:                                                  # FastFading.m:158-177
+                self.UseDiscreteDopplerSpectrum = True
+                nd = int(np.ceil(self.MaximumDopplerShift / df))
+                ip = df * (np.arange(-nd - 1, nd + 1) + 0.5)
+                ip = np.clip(ip, -self.MaximumDopplerShift, self.MaximumDopplerShift)
+                if DopplerModel == "Discrete-Jakes":
+                    S = np.arcsin(ip[1:] / self.MaximumDopplerShift) - np.arcsin(ip[:-1] / self.MaximumDopplerShift)
+                else:
+                    S = ip[1:] - ip[:-1]
+                self.DiscreteDopplerSpectrum = S / S.sum()
         self._engine = None
         self._rep = 0
         self._seed = 0
@@ -103,12 +124,16 @@ class FastFading:
         return self.PowerDelayProfile.size
 
     def GetTimeCorrelation(self):
-        """FastFading.m:321-340 (Jakes: J0, Uniform: sinc)."""
+        """FastFading.m:321-340 (Jakes: J0, Uniform: sinc).  For a discrete
+        Doppler spectrum the reference assigns no TimeCorrelation (its switch
+        only knows 'Jakes' / 'Uniform', :331-336), so this raises like MATLAB."""
         from scipy.special import j0
         N = self.SamplesTotal
         t = self.dt * np.arange(-(N - 1), N)
         if self.MaximumDopplerShift <= 0:
             return np.ones(2 * N - 1), t
+        if self.DopplerModel.startswith("Discrete"):
+            raise ValueError("TimeCorrelation is not defined for a discrete Doppler spectrum (FastFading.m:321-336)")
         if self.DopplerModel == "Jakes":
             return j0(np.pi * 2 * self.MaximumDopplerShift * t), t
         return np.sinc(2 * self.MaximumDopplerShift * t), t

@@ -212,3 +212,80 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
     return Setup(name=name, N=N, L=L, F=F, SR=SR, snr_db=snr, pn_time=pn, n_iter=n_iter,
                  zero_threshold=1e-8, channel=chan, schemes=out, n_repetitions=cfg["reps"],
                  plot_snr_db=cfg["plot"])
+
+
+# ---------------------------------------------------------------------------
+# SimpleVersion_DoublyFlat.m (BASELINE config 1): doubly-flat channel, pilot
+# interpolation instead of the MMSE estimator, no interference cancellation.
+# ---------------------------------------------------------------------------
+def build_doubly_flat_setup(qam_order=16, snr_db=None, n_repetitions=1000):
+    """Setup of ``SimpleVersion_DoublyFlat.m`` (:12-82).
+
+    Schemes 'fbmc_aux', 'fbmc_cod', 'ofdm' with their interpolation weights
+    (``extras['interp']``, PSACE 'linear' on the Diamond patterns, :47-66) and
+    noise slots (``extras['noise_slot']``: n_FBMC shared by the two FBMC
+    schemes, n_OFDM separate, :125-126).  The channel is the time-invariant
+    'Flat' FastFading (fD = 0, FastFading.m:241-246), i.e. the script's
+    h = sqrt(1/2) (randn + j randn) (:123).  The script draws everything —
+    bits, pilots, h, noise — inside its SNR loop (:90-126); the engine runs one
+    SNR point per call with the key ``snr_seed(seed, k)`` (dsce.doubly_flat).
+    """
+    from .estimation import PilotSymbolAidedChannelEstimation as PSACE
+    L = 12
+    F = 15e3
+    SR = 15e3 * 14 * 12
+    snr = np.asarray(np.arange(0, 31, 5) if snr_db is None else snr_db, dtype=float)
+    fbmc = FBMC(L, 30, F, SR, 15e3 * 20, False, "Hermite-OQAM", 8, 0, True)          # :17-28
+    ofdm = OFDM(L, 15, F, SR, 15e3 * 20, False, 0, (8 - 1 / 2) * 1 / 15e3 * 1 / 2)   # :31-40
+    N = ofdm.Nr.SamplesTotal
+    if fbmc.Nr.SamplesTotal != N:
+        raise ValueError("Total number of samples must be the same for OFDM and FBMC.")
+    pam = SignalConstellation(int(np.sqrt(qam_order)), "PAM")                       # :43-44
+    qam = SignalConstellation(qam_order, "QAM")
+    ce_ofdm = PSACE("Diamond", [[ofdm.Nr.Subcarriers, 6], [ofdm.Nr.MCSymbols, 4]], "linear")   # :47-56
+    ce_fbmc = PSACE("Diamond", [[fbmc.Nr.Subcarriers, 6], [fbmc.Nr.MCSymbols, 8]], "linear")   # :57-66
+    Dfbmc = fbmc.GetFBMCMatrix()
+    aux_pm = ce_fbmc.GetAuxiliaryMatrix(1)
+    aux = IIC("Auxiliary", aux_pm, Dfbmc, 16, 2)                                      # :69-75
+    cod = IIC("Coding", ce_fbmc.PilotMatrix, Dfbmc, 16, 2)                            # :76-82
+    G_fbmc = fbmc.GetTXMatrix()
+    Q_fbmc = fbmc.GetRXMatrix().conj().T
+    G_ofdm = ofdm.GetTXMatrix()
+    Q_ofdm = ofdm.GetRXMatrix().conj().T
+    W_fbmc = ce_fbmc.GetInterpolationWeights()
+    W_ofdm = ce_ofdm.GetInterpolationWeights()
+    NPf = ce_fbmc.NrPilotSymbols
+    pil_f = np.flatnonzero(_col(ce_fbmc.PilotMatrix) == 1)
+    out = {}
+    out["fbmc_aux"] = Scheme(                                                         # :138, :148, :156
+        name="fbmc_aux", kind="fbmc_aux", G=G_fbmc, Q=Q_fbmc, P=aux.PrecodingMatrix, pilot_pos=pil_f,
+        data_pos=np.flatnonzero(_col(aux.PilotMatrix) == 0), despread=False, real_detect=True,
+        data_div=float(np.sqrt(aux.DataPowerReduction)),
+        kappa=float(aux.PilotToDataPowerOffset * aux.DataPowerReduction), dpr=aux.DataPowerReduction, const=pam,
+        considered_symbols=np.ones(aux.NrDataSymbols, dtype=bool), n_pilots=NPf, n_data=aux.NrDataSymbols,
+        bits_slot=0, pilot_slot=0,
+        extras=dict(iic=aux, pilot_matrix=aux_pm, modulation=fbmc, interp=W_fbmc, noise_slot=0, psace=ce_fbmc))
+    out["fbmc_cod"] = Scheme(                                                         # :139, :149-150, :157-158
+        name="fbmc_cod", kind="fbmc_cod", G=G_fbmc, Q=Q_fbmc, P=cod.PrecodingMatrix, pilot_pos=pil_f,
+        data_pos=np.arange(NPf, cod.PrecodingMatrix.shape[1]), despread=True, real_detect=True, data_div=1.0,
+        kappa=float(cod.PilotToDataPowerOffset), dpr=cod.DataPowerReduction, const=pam,
+        considered_symbols=np.ones(cod.NrDataSymbols, dtype=bool), n_pilots=NPf, n_data=cod.NrDataSymbols,
+        bits_slot=1, pilot_slot=0,
+        extras=dict(iic=cod, pilot_matrix=ce_fbmc.PilotMatrix, modulation=fbmc, interp=W_fbmc, noise_slot=0,
+                    psace=ce_fbmc))
+    pmv = _col(ce_ofdm.PilotMatrix)
+    NPo = ce_ofdm.NrPilotSymbols
+    LKo = pmv.size
+    Pm = np.zeros((LKo, LKo))                                                          # :113-115
+    Pm[np.flatnonzero(pmv == 1), np.arange(NPo)] = 1.0
+    Pm[np.flatnonzero(pmv == 0), np.arange(NPo, LKo)] = 1.0
+    out["ofdm"] = Scheme(                                                             # :140, :152-153, :160-161
+        name="ofdm", kind="ofdm", G=G_ofdm, Q=Q_ofdm, P=Pm.astype(complex), pilot_pos=np.flatnonzero(pmv == 1),
+        data_pos=np.flatnonzero(pmv == 0), despread=False, real_detect=False, data_div=1.0, kappa=1.0, dpr=1.0,
+        const=qam, considered_symbols=np.ones(LKo - NPo, dtype=bool), n_pilots=NPo, n_data=LKo - NPo,
+        bits_slot=2, pilot_slot=1,
+        extras=dict(pilot_matrix=ce_ofdm.PilotMatrix, modulation=ofdm, interp=W_ofdm, noise_slot=1, psace=ce_ofdm))
+    chan = FastFading(SR, "Flat", N, 0.0, "Jakes", 1, 1, 1, 0)
+    pn = SR / (F * L) * 10.0 ** (-snr / 10)                                            # :92
+    return Setup(name="doubly_flat", N=N, L=L, F=F, SR=SR, snr_db=snr, pn_time=pn, n_iter=0, zero_threshold=1e-8,
+                 channel=chan, schemes=out, n_repetitions=n_repetitions, plot_snr_db=float(snr[-1]))

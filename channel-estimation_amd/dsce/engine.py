@@ -21,6 +21,7 @@ EXPORTED = [
     "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
     "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
     "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
+    "dsce_set_noise_slot", "dsce_set_interpolation",
 ]
 
 
@@ -88,6 +89,8 @@ def load_library(path=None):
     lib.dsce_work_model.argtypes = [vp, C.c_int32, dp, dp]
     lib.dsce_mmse_onetap.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, dp, C.c_int32, dp]
     lib.dsce_tx_matrices.argtypes = [vp, C.POINTER(TxDesc), dp, dp]
+    lib.dsce_set_noise_slot.argtypes = [vp, C.c_int32, C.c_int32]
+    lib.dsce_set_interpolation.argtypes = [vp, C.c_int32, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -148,7 +151,7 @@ class Engine:
         pdp = np.ascontiguousarray(ff.PowerDelayProfileNormalized, dtype=np.float64)
         self._keep.append(pdp)
         d = ChannelDesc(ff.SamplesTotal, pdp.size, ff.SamplingRate, ff.MaximumDopplerShift, ff.Paths,
-                        0 if ff.DopplerModel == "Jakes" else 1, _dptr(pdp))
+                        ff.MODELS[ff.DopplerModel], _dptr(pdp))
         self._chk(self.lib.dsce_set_channel(self.h, C.byref(d)), "dsce_set_channel")
         self.N = ff.SamplesTotal
         self.ntaps = pdp.size
@@ -178,6 +181,18 @@ class Engine:
         self._chk(self.lib.dsce_add_scheme(self.h, C.byref(d), C.byref(sid)), "dsce_add_scheme")
         self.schemes.append(sc)
         return sid.value
+
+    def set_noise_slot(self, sid, slot):
+        """Schemes of one slot share the AWGN draw (dsce_set_noise_slot)."""
+        self._chk(self.lib.dsce_set_noise_slot(self.h, int(sid), int(slot)), "dsce_set_noise_slot")
+
+    def set_interpolation(self, sid, interp):
+        """One-tap estimate h_hat = interp @ hP (LK x NP) instead of the MMSE W
+        (dsce_set_interpolation; PSACE ChannelInterpolation weights)."""
+        sc = self.schemes[sid]
+        I = _cplx(np.asarray(interp).reshape(sc.LK, sc.n_pilots))
+        self._keep.append(I)
+        self._chk(self.lib.dsce_set_interpolation(self.h, int(sid), _dptr(I)), "dsce_set_interpolation")
 
     def build_mmse(self, zero_threshold=1e-8):
         self._chk(self.lib.dsce_build_mmse(self.h, float(zero_threshold)), "dsce_build_mmse")

@@ -190,8 +190,7 @@ class PilotSymbolAidedChannelEstimation:
 
     Supported interpolation methods: 'FullAverage', 'MovingBlockAverage',
     'linear'/'nearest' (MATLAB ``scatteredInterpolant`` semantics with
-    extrapolation restated on the host: CPU-only, config 1 plumbing,
-    ``_scattered``), and
+    extrapolation restated on the host, ``_scattered_weights``), and
     'MMSE' — the slot the reference leaves as ``error('Needs to be
     implemented')``.  For 'MMSE' the object carries the engine handle
     (``set_mmse_engine``) and ``ChannelInterpolation`` returns the MMSE
@@ -282,7 +281,7 @@ class PilotSymbolAidedChannelEstimation:
         if m == "MovingBlockAverage":
             return (self.InterpolationMatrix @ LS).reshape(self.PilotMatrix.shape, order="F")
         if m in ("linear", "nearest"):
-            return self._scattered(LS, m)
+            return (self._scattered_weights(m) @ LS).reshape(self.PilotMatrix.shape, order="F")
         if m == "natural":
             raise NotImplementedError("natural-neighbour interpolation is not provided")
         if m == "MMSE":
@@ -291,54 +290,75 @@ class PilotSymbolAidedChannelEstimation:
             return self._mmse(LS)
         raise ValueError("Interpolation method not implemented")
 
-    def _scattered(self, LS, method):
-        """``scatteredInterpolant(x_pilot, y_pilot, v, method)`` evaluated on the
-        full grid (PSACE.m:75-77, :119-121), config-1 CPU plumbing (SURVEY §8f
-        f4).  'linear': barycentric on the Delaunay triangulation of the pilot
-        positions; outside the convex hull the affine function of the boundary
-        triangle nearest to the query point (MATLAB's default linear
-        extrapolation; exact for affine fields).  'nearest': value of the
-        closest pilot (its default extrapolation too)."""
+    def _scattered_weights(self, method):
+        """Weights of the scatteredInterpolant on the grid, rows in MATLAB's
+        ``meshgrid`` query order (column-major L x K).  'linear': barycentric on
+        the Delaunay triangulation of the pilot positions; outside the convex
+        hull the affine function of the boundary triangle nearest to the query
+        point (MATLAB's default linear extrapolation; exact for affine fields).
+        'nearest': the closest pilot (its default extrapolation too)."""
+        key = "_w_" + method
+        if getattr(self, key, None) is not None:
+            return getattr(self, key)
         from scipy.spatial import Delaunay, cKDTree
         PM = self.PilotMatrix
         # [x, y] = find(PilotMatrix): column-major, 1-based (row, column)
         rows, cols = np.nonzero(PM.T)
         pts = np.stack([cols + 1.0, rows + 1.0], axis=1)
+        NP = pts.shape[0]
         nL, nK = PM.shape
         gx, gy = np.meshgrid(np.arange(1, nL + 1.0), np.arange(1, nK + 1.0), indexing="ij")
         q = np.stack([gx.ravel(), gy.ravel()], axis=1)
+        Wt = np.zeros((q.shape[0], NP))
         if method == "nearest":
             _, idx = cKDTree(pts).query(q)
-            return LS[idx].reshape(nL, nK)
-        tri = Delaunay(pts)
-        simp = tri.find_simplex(q)
-        out = np.empty(q.shape[0], dtype=complex)
+            Wt[np.arange(q.shape[0]), idx] = 1.0
+        else:
+            tri = Delaunay(pts)
+            simp = tri.find_simplex(q)
+            # boundary edges of the hull and the triangle owning each
+            hull_edges = []
+            for si, nb in enumerate(tri.neighbors):
+                for k in range(3):
+                    if nb[k] == -1:
+                        e = [tri.simplices[si][j] for j in range(3) if j != k]
+                        hull_edges.append((e[0], e[1], si))
+            for i, xy in enumerate(q):
+                si = simp[i]
+                if si < 0:
+                    best, bd = None, np.inf
+                    for a, b, s_ in hull_edges:
+                        pa, pb = pts[a], pts[b]
+                        t = np.clip(np.dot(xy - pa, pb - pa) / np.dot(pb - pa, pb - pa), 0.0, 1.0)
+                        d = np.sum((pa + t * (pb - pa) - xy) ** 2)
+                        if d < bd - 1e-12:
+                            best, bd = s_, d
+                    si = best
+                T = tri.transform[si]
+                b = T[:2].dot(xy - T[2])
+                for v, w in zip(tri.simplices[si], (b[0], b[1], 1.0 - b[0] - b[1])):
+                    Wt[i, v] += w
+        # the grid is enumerated (row, column) with the row fastest = column-major
+        order = np.arange(nL * nK).reshape(nL, nK).reshape(-1, order="F")
+        Wc = Wt[order]
+        setattr(self, key, Wc)
+        return Wc
 
-        def affine_eval(si, xy):
-            T = tri.transform[si]
-            b = T[:2].dot(xy - T[2])
-            w = np.array([b[0], b[1], 1.0 - b[0] - b[1]])
-            return w.dot(LS[tri.simplices[si]])
-        # boundary edges of the hull and the triangle owning each
-        hull_edges = []
-        for si, nb in enumerate(tri.neighbors):
-            for k in range(3):
-                if nb[k] == -1:
-                    e = [tri.simplices[si][j] for j in range(3) if j != k]
-                    hull_edges.append((e[0], e[1], si))
-        for i, xy in enumerate(q):
-            si = simp[i]
-            if si < 0:
-                best, bd = None, np.inf
-                for a, b, s_ in hull_edges:
-                    pa, pb = pts[a], pts[b]
-                    t = np.clip(np.dot(xy - pa, pb - pa) / np.dot(pb - pa, pb - pa), 0.0, 1.0)
-                    d = np.sum((pa + t * (pb - pa) - xy) ** 2)
-                    if d < bd - 1e-12:
-                        best, bd = s_, d
-                si = best
-            out[i] = affine_eval(si, xy)
-        return out.reshape(nL, nK)
+    def GetInterpolationWeights(self):
+        """LK x NP matrix I with ChannelInterpolation(LS) = reshape(I @ LS) for
+        every method the reference implements (all are linear in the LS
+        estimates, PSACE.m:115-133); this is what crosses the C-ABI as
+        dsce_set_interpolation."""
+        m = self.InterpolationMethod
+        NP = self.NrPilotSymbols
+        LK = self.PilotMatrix.size
+        if m == "FullAverage":
+            return np.full((LK, NP), 1.0 / NP)
+        if m == "MovingBlockAverage":
+            return self.InterpolationMatrix.copy()
+        if m in ("linear", "nearest"):
+            return self._scattered_weights(m).copy()
+        raise ValueError("no fixed interpolation weights for method %r" % m)
 
     def GetAuxiliaryMatrix(self, NrAuxiliarySymbols):
         """PSACE.m:137-169."""

@@ -131,3 +131,45 @@ def figures(result, outdir, theory=None, fmt="png"):
         plt.close()
         out.append(name)
     return out
+
+
+def doubly_flat_result(sim, counts, n_rep, seed, theory, extra=None):
+    """Result object of the doubly-flat script (SimpleVersion_DoublyFlat.m):
+    its five BER curves (mean over realisations, :186-191) and the closed-form
+    perfect-CSI BEP it plots (:180-181, ``theory`` on a 0.5 dB grid)."""
+    S = sim.setup
+    res = {
+        "config": "doubly_flat",
+        "N": int(S.N),
+        "snr_db": [float(x) for x in S.snr_db],
+        "n_repetitions": int(n_rep),
+        "seed": int(seed),
+        "bits_per_rep": [int(x) for x in sim.bits_per_rep()],
+        "counts": np.asarray(counts, dtype=np.int64).tolist(),
+        "ber": {k: [float(x) for x in v] for k, v in sim.ber(counts, n_rep).items()},
+        "theory": {"snr_db": [float(x) for x in theory[0]], "bep": [float(x) for x in theory[1]]},
+    }
+    if extra:
+        res.update(extra)
+    return res
+
+
+def doubly_flat_figure(result, path):
+    """The BER/BEP figure of SimpleVersion_DoublyFlat.m:185-195."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    snr = np.asarray(result["snr_db"])
+    plt.figure(figsize=(5, 4))
+    for label, f, col in (("FBMC Auxiliary", "-o", "red"), ("FBMC Coding", "-o", "blue"), ("OFDM", "-o", "black"),
+                          ("FBMC perfect CSI", "-x", "blue"), ("OFDM perfect CSI", "-x", "black")):
+        plt.semilogy(snr, result["ber"][label], f, color=col, markersize=4, label="Simulation: " + label)
+    plt.semilogy(result["theory"]["snr_db"], result["theory"]["bep"], color="black", label="Theory perfect CSI")
+    plt.xlabel("SNR for OFDM (dB)")
+    plt.ylabel("BER, BEP")
+    plt.title("Doubly-flat, %d realisations" % result["n_repetitions"])
+    plt.legend(fontsize=7, loc="lower left")
+    plt.savefig(path, dpi=120, bbox_inches="tight")
+    plt.close()
+    return path

@@ -25,6 +25,10 @@
  *                            script:417-428
  *   dsce_get_correlation / dsce_get_W <- R_hP*, W_MMSE_*          script:210-313 (parity probes)
  *   dsce_tx_matrices      <- OFDM/FBMC.GetTXMatrix / GetRXMatrix OFDM.m:184-218, FBMC.m:318-354
+ *   dsce_set_interpolation <- PilotSymbolAidedChannelEstimation.ChannelInterpolation,
+ *                            'linear'/'nearest'/'FullAverage'/'MovingBlockAverage'
+ *                            (PSACE.m:73-107, :115-133) as its LK x NP weight matrix
+ *   dsce_set_noise_slot   <- separate n_FBMC / n_OFDM draws     SimpleVersion_DoublyFlat.m:125-126
  *
  * Conventions
  *  - Return 0 on success, a negative DSCE_E* code on failure; the message is
@@ -49,9 +53,17 @@
  *                    (i & 31) of word ((i>>5) & 3) of counter i>>7.
  *    PILOTS (4, s)   pilot symbol indices (script:365-367): pilot j is word
  *                    (j & 3) of counter j>>2, masked to log2(M) bits.
- *    NOISE  (5, k)   AWGN of SNR index k, shared by all schemes (script:399):
- *                    sample e: u1=u53(w0,w1), u2=u53(w2,w3);
+ *    NOISE  (5, k + 256 g)  AWGN of SNR index k, shared by all schemes of
+ *                    noise slot g (default 0: all schemes, script:399):
+ *                    sample e: normal pair of counter e, where a normal pair is
+ *                    u1=u53(w0,w1), u2=u53(w2,w3);
  *                    re = sqrt(-2 log(1-u1)) cos(2 pi u2), im = ... sin(2 pi u2).
+ *    THETA  (1, 0)   max_doppler == 0: tap q (q-th non-zero tap) is
+ *                    1/sqrt(2) sqrt(PDPn) (re + j im) of the normal pair of
+ *                    counter q (FastFading.m:244).
+ *    THETA  (1, 1)   discrete Doppler models: Doppler bin f = -nd..nd of tap q is
+ *                    the normal pair of counter (f + nd) + (2 nd + 1) q
+ *                    (GaussUncorr1 / GaussUncorr2, FastFading.m:207-211).
  *
  * Error counters (dsce_run): int64 array of shape
  *   [n_schemes][2 csi: 0 = MMSE estimate, 1 = perfect CSI][2 edge: 0 = all bits,
@@ -67,7 +79,7 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 1
+#define DSCE_ABI_VERSION 2
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
@@ -81,9 +93,14 @@ typedef struct {
     int32_t n_samples;          /* N                                          */
     int32_t n_taps;             /* length of the sampled PDP (incl. zero taps) */
     double sampling_rate;       /* Hz                                         */
-    double max_doppler;         /* Hz (FastFading.m:42)                        */
+    double max_doppler;         /* Hz (FastFading.m:42); 0 = time-invariant    */
+                                /* block fading (FastFading.m:241-246)         */
     int32_t n_paths;            /* sum-of-sinusoids paths (FastFading.m:179)   */
-    int32_t doppler_model;      /* 0 = 'Jakes', 1 = 'Uniform'                  */
+    int32_t doppler_model;      /* 0 = 'Jakes', 1 = 'Uniform' (sum of sinusoids, */
+                                /* FastFading.m:222-238), 2 = 'Discrete-Jakes', */
+                                /* 3 = 'Discrete-Uniform' (IFFT of the discrete */
+                                /* Doppler spectrum, FastFading.m:158-177,      */
+                                /* :203-221; fD/df <= 0.5 sets fD = 0, :153-156) */
     const double* pdp_norm;     /* n_taps, PowerDelayProfileNormalized (:129) */
 } dsce_channel_desc;
 
@@ -168,6 +185,21 @@ int dsce_mmse_onetap(dsce_ctx* ctx, int32_t scheme_id, int32_t snr_index, int32_
 
 /* G (and Q, each optional) as N x LK complex column-major host buffers. */
 int dsce_tx_matrices(dsce_ctx* ctx, const dsce_tx_desc* desc, double* G_out, double* Q_out);
+
+/* Noise slot of a scheme (0..255, default 0): schemes of one slot share the AWGN
+ * draw of an SNR point (script:399-403); SimpleVersion_DoublyFlat.m:125-126
+ * draws n_FBMC and n_OFDM separately (two slots). */
+int dsce_set_noise_slot(dsce_ctx* ctx, int32_t scheme_id, int32_t slot);
+
+/* One-tap channel estimate by a fixed linear interpolation of the LS pilot
+ * estimates, h_hat = I hP, instead of the MMSE estimator: the non-'MMSE'
+ * methods of PilotSymbolAidedChannelEstimation.ChannelInterpolation
+ * (PSACE.m:115-133: 'linear' / 'nearest' scatteredInterpolant weights,
+ * 'FullAverage', 'MovingBlockAverage' — all linear in the LS values).
+ * I is LK x NP complex, column-major.  The scheme then needs no
+ * dsce_build_mmse, and dsce_run requires n_iter == 0 (no W for the IC
+ * iterations).  Used by the doubly-flat script, SimpleVersion_DoublyFlat.m:143-145. */
+int dsce_set_interpolation(dsce_ctx* ctx, int32_t scheme_id, const double* interp);
 
 /* ---- parity probes (same kernels as dsce_run) ---------------------------- */
 /* ImpulseResponse of realisation `rep`: N x n_taps complex, column-major. */

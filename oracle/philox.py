@@ -104,3 +104,15 @@ def complex_normals(seed, rep, snr_index, n):
     rad = np.sqrt(-2.0 * np.log(1.0 - u1))
     ang = (2.0 * np.pi) * u2
     return rad * np.cos(ang), rad * np.sin(ang)
+
+
+def normal_pairs(seed, rep, stream, sub, counters):
+    """Normal pairs (re, im) of the given counters, same Box-Muller as
+    :func:`complex_normals` (time-invariant and discrete-Doppler channels)."""
+    e = np.asarray(counters, dtype=np.uint32)
+    w0, w1, w2, w3 = _block(seed, rep, stream, sub, e)
+    u1 = u53(w0, w1)
+    u2 = u53(w2, w3)
+    rad = np.sqrt(-2.0 * np.log(1.0 - u1))
+    ang = (2.0 * np.pi) * u2
+    return rad * np.cos(ang), rad * np.sin(ang)

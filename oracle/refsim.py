@@ -6,6 +6,8 @@ path, written to follow the MATLAB line by line — including its explicit-matri
 formulation, which is also what makes it the CPU baseline:
 
 * Jakes channel realisation          FastFading.m:222-238
+* discrete-Doppler / time-invariant  FastFading.m:153-177, :203-221, :241-246
+* doubly-flat loop (config 1)        SimpleVersion_DoublyFlat.m:89-170
 * time-variant convolution matrix    FastFading.m:133-144, :186-190, :276-295
 * R_vecH = E{vec(H) vec(H)^H}         FastFading.m:321-340, :366-407 (literal
   sparse build, including the tau>=2 wrap-around quirk of :377)
@@ -58,6 +60,60 @@ def jakes_ir(seed, rep, N, dt, pdp_norm, idx_taps, fD, paths, model="Jakes"):
         x = ph[i][:, None] + ds[i][:, None] * t[None, :]          # Paths x N
         ir_tmp[tap, :] = np.exp(1j * (2 * np.pi * x)).sum(axis=0) / np.sqrt(paths)
     return (np.sqrt(np.asarray(pdp_norm))[:, None] * ir_tmp).T
+
+
+def static_ir(seed, rep, N, pdp_norm, idx_taps):
+    """MaximumDopplerShift == 0 (FastFading.m:241-246): one impulse response
+    1/sqrt(2) sqrt(PDPn) (randn + j randn) per realisation; returned repeated
+    over the N samples as GetConvolutionMatrix uses it (:288-291)."""
+    pdp_norm = np.asarray(pdp_norm, dtype=float)
+    taps = np.asarray(idx_taps)
+    re, im = philox.normal_pairs(seed, rep, philox.STREAM_THETA, 0, np.arange(taps.size))
+    row = np.zeros(pdp_norm.size, dtype=complex)
+    row[taps] = 1 / np.sqrt(2) * np.sqrt(pdp_norm[taps]) * (re + 1j * im)
+    return np.repeat(row[None, :], N, axis=0)
+
+
+def discrete_doppler_spectrum(N, SR, fD, model):
+    """FastFading.m:158-177; returns (nd, S) with S over the bins f = -nd..nd,
+    or (0, None) when fD/df <= 0.5 sets the velocity to zero (:153-156)."""
+    df = SR / N
+    if fD / df <= 0.5:
+        return 0, None
+    nd = int(np.ceil(fD / df))
+    ip = df * (np.arange(-nd - 1, nd + 1) + 0.5)
+    ip[ip <= -fD] = -fD
+    ip[ip >= fD] = fD
+    if model == "Discrete-Jakes":
+        S = np.arcsin(ip[1:] / fD) - np.arcsin(ip[:-1] / fD)
+    else:
+        S = ip[1:] - ip[:-1]
+    return nd, S / S.sum()
+
+
+def discrete_ir(seed, rep, N, SR, pdp_norm, idx_taps, fD, model):
+    """UseDiscreteDopplerSpectrum branch of NewRealization (FastFading.m:203-221),
+    literally: ifft of [sqrt(S(nd+1:end)).*G1; zeros; sqrt(S(1:nd)).*G2] with
+    G = N/sqrt(2) (randn + j randn) sqrt(PDPn)."""
+    pdp_norm = np.asarray(pdp_norm, dtype=float)
+    taps = np.asarray(idx_taps)
+    nt = taps.size
+    nd, S = discrete_doppler_spectrum(N, SR, fD, model)
+    if S is None:
+        return static_ir(seed, rep, N, pdp_norm, idx_taps)
+    nb = 2 * nd + 1
+    re, im = philox.normal_pairs(seed, rep, philox.STREAM_THETA, 1, np.arange(nb * nt))
+    Z = (re + 1j * im).reshape(nb, nt, order="F")                 # row = f + nd
+    g1 = N / np.sqrt(2) * Z[nd:, :]                                # f = 0..nd
+    g2 = N / np.sqrt(2) * Z[:nd, :]                                # f = -nd..-1
+    sp_ = np.sqrt(pdp_norm[taps])[None, :]
+    g1 = g1 * sp_
+    g2 = g2 * sp_
+    Sm = np.repeat(S[:, None], nt, axis=1)
+    X = np.concatenate([np.sqrt(Sm[nd:, :]) * g1, np.zeros((N - 2 * nd - 1, nt)), np.sqrt(Sm[:nd, :]) * g2])
+    ir = np.zeros((N, pdp_norm.size), dtype=complex)
+    ir[:, taps] = np.fft.ifft(X, axis=0)
+    return ir
 
 
 def conv_matrix(ir, pdp, N):
@@ -295,6 +351,67 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                         trace["hp_stages"][-1].append(hPt)
                         trace["hest_stages"][-1].append(ht)
     return dict(err=err, borderline=border, nbits=nbits)
+
+
+# ---------------------------------------------------------------------------
+# SimpleVersion_DoublyFlat.m:89-170 (BASELINE config 1)
+# ---------------------------------------------------------------------------
+def snr_seed(seed, k):
+    """Philox key of SNR point k of the doubly-flat loop: seed + k * 2^32."""
+    return (int(seed) + (int(k) << 32)) & ((1 << 64) - 1)
+
+
+def simulate_doubly_flat(seed, first_rep, n_rep, N, schemes, pn_time, margin_eps=1e-9):
+    """Literal restatement of the doubly-flat Monte-Carlo loop.
+
+    ``schemes``: oracle scheme dicts (see :func:`simulate`) plus ``noise_slot``
+    and ``interp`` (the LK x NP PilotSymbolAidedChannelEstimation weights,
+    ChannelInterpolation = interp @ LS, PSACE.m:115-121).  Every random
+    quantity is drawn per (realisation, SNR point) with key snr_seed(seed, k)
+    (:90-126).  Returns dict(err=int64[ns, 2 csi, nsnr], borderline=int64[ns]).
+    """
+    ns = len(schemes)
+    err = np.zeros((ns, 2, len(pn_time)), dtype=np.int64)
+    border = np.zeros(ns, dtype=np.int64)
+    for rep in range(first_rep, first_rep + n_rep):
+        for k, pn in enumerate(pn_time):
+            sk = snr_seed(seed, k)
+            h = static_ir(sk, rep, N, [1.0], [0])[0, 0]                     # :123
+            noise = {}
+            for si, sc in enumerate(schemes):
+                P, G, Q = sc["P"], sc["G"], sc["Q"]
+                symbols, bitmap = sc["symbols"], sc["bitmap"]
+                M = symbols.size
+                mbit = sc["bits_per_symbol"]
+                nd = sc["n_data"]
+                NP = len(sc["pilot_pos"])
+                b = philox.bits(sk, rep, sc["bits_slot"], nd * mbit)          # :95-97
+                xD = symbols[(b.reshape(nd, mbit).astype(np.int64) << np.arange(mbit)).sum(axis=1)]   # :100-102
+                xP = symbols[philox.indices(sk, rep, sc["pilot_slot"], NP, M)]   # :105-108
+                xP = xP / np.abs(xP)
+                x = P @ np.concatenate([xP, xD])                               # :111-115
+                s = G @ x                                                      # :118-120
+                slot = sc["noise_slot"]
+                if slot not in noise:                                          # :125-126
+                    nre, nim = philox.complex_normals(sk, rep, 256 * slot, N)
+                    noise[slot] = np.sqrt(pn / 2) * (nre + 1j * nim)
+                r = h * s + noise[slot]                                        # :128-130
+                y = Q.conj().T @ r                                             # :133-135
+                LS = y[sc["pilot_pos"]] / xP / np.sqrt(sc["kappa"])            # :138-140
+                hest = sc["interp"] @ LS                                       # :143-145
+                for csi, hh in ((0, hest), (1, h)):                            # :148-161
+                    xhat = y / hh
+                    if sc["despread"]:
+                        z = np.real(P[:, NP:].conj().T @ xhat) / sc["data_div"]
+                    elif sc["real_detect"]:
+                        z = np.real(xhat[sc["data_pos"]] / sc["data_div"])
+                    else:
+                        z = xhat[sc["data_pos"]] / sc["data_div"]
+                    idx, margin = nearest(z, symbols)
+                    det = bitmap[idx, :].reshape(-1)
+                    err[si, csi, k] += int(np.sum(det != b))                   # :164-169
+                    border[si] += int(np.sum(margin < margin_eps))
+    return dict(err=err, borderline=border)
 
 
 # ---------------------------------------------------------------------------

@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     from dsce import engine
     lib = engine.load_library()
-    assert lib.dsce_abi_version() == 1
+    assert lib.dsce_abi_version() == 2
 
 
 def test_struct_layout_matches_c(tmp_path):

@@ -111,3 +111,58 @@ def test_psace_scattered_interpolation():
             d = (pr - r) ** 2 + (pc - c) ** 2
             assert np.isclose(d[np.argmin(d)], ((pr - r) ** 2 + (pc - c) ** 2)[
                 np.argmin(np.abs(H[pr, pc] - near[r, c]))])
+
+
+def test_psace_linear_weights_match_scipy_inside_hull():
+    """PSACE 'linear' weights equal scipy's LinearNDInterpolator (an independent
+    Delaunay/barycentric implementation) at every grid point inside the pilot
+    hull; every row sums to one (affine fields are reproduced)."""
+    from scipy.interpolate import LinearNDInterpolator
+
+    from dsce.estimation import PilotSymbolAidedChannelEstimation as PSACE
+    ce = PSACE("Diamond", [[12, 6], [30, 8]], "linear")
+    W = ce.GetInterpolationWeights()
+    NP = ce.NrPilotSymbols
+    assert W.shape == (12 * 30, NP) and np.allclose(W.sum(axis=1), 1.0)
+    rows, cols = np.nonzero(ce.PilotMatrix.T)
+    pts = np.stack([cols + 1.0, rows + 1.0], axis=1)
+    rng = np.random.default_rng(0)
+    v = rng.standard_normal(NP) + 1j * rng.standard_normal(NP)
+    f = LinearNDInterpolator(pts, v)
+    ll, kk = np.meshgrid(np.arange(1, 13.0), np.arange(1, 31.0), indexing="ij")
+    ref = f(ll.reshape(-1, order="F"), kk.reshape(-1, order="F"))
+    inside = ~np.isnan(ref)
+    assert inside.sum() > 100
+    assert np.max(np.abs((W @ v)[inside] - ref[inside])) < 1e-12
+    got = ce.ChannelInterpolation(v)
+    assert np.allclose(got.reshape(-1, order="F"), W @ v)
+
+
+def test_doubly_flat_setup_matches_script():
+    """SimpleVersion_DoublyFlat.m:16-82: sizes, pilots, kappa, noise slots."""
+    from dsce.configs import build_doubly_flat_setup
+    S = build_doubly_flat_setup()
+    assert S.N == 3780 and S.n_iter == 0 and S.channel.MaximumDopplerShift == 0
+    assert np.allclose(S.pn_time, 14 * 10 ** (-np.arange(0, 31, 5) / 10))
+    a, c, o = (S.schemes[k] for k in ("fbmc_aux", "fbmc_cod", "ofdm"))
+    assert (a.LK, c.LK, o.LK) == (360, 360, 180) and a.n_pilots == c.n_pilots == o.n_pilots == 8
+    assert o.n_data == 172 and o.kappa == 1.0 and c.kappa == 2.0
+    assert (a.extras["noise_slot"], c.extras["noise_slot"], o.extras["noise_slot"]) == (0, 0, 1)
+    assert (a.pilot_slot, c.pilot_slot, o.pilot_slot) == (0, 0, 1)
+    assert len({a.bits_slot, c.bits_slot, o.bits_slot}) == 3
+    # OFDM pilots / data mapped by a permutation (:113-115)
+    assert np.allclose(np.abs(o.P).sum(axis=0), 1) and np.allclose(np.abs(o.P).sum(axis=1), 1)
+
+
+@pytest.mark.parametrize("M,kind", [(4, "QAM"), (16, "QAM"), (256, "QAM"), (4, "PAM"), (16, "PAM")])
+def test_theory_module_matches_oracle(M, kind):
+    """dsce.theory (vectorised, plotted by the doubly-flat run) against the
+    oracle's literal restatement of Theory/BitErrorProbabilityDoublyFlatRayleigh.m."""
+    from dsce.modulation import SignalConstellation
+    from dsce.theory import bit_error_probability_doubly_flat_rayleigh as bep
+    from oracle import refsim
+    c = SignalConstellation(M, kind)
+    snr = np.arange(-5, 41, 2.5)
+    a = bep(snr, c.SymbolMapping, c.BitMapping)
+    b = refsim.bit_error_probability_doubly_flat_rayleigh(snr, c.SymbolMapping, c.BitMapping)
+    assert np.max(np.abs(a / b - 1)) < 1e-10
