@@ -339,6 +339,40 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
             s.k.pic_goff = dupload(c, goff);
             s.k.pic_g = dupload(c, gtab);
         }
+        // MFMA operand tables of k_pic_mfma (SchemeK::pm_ok)
+        int ksq = 0;
+        bool mok = s.k.pic_ok && md <= 1;
+        for (int b = 0; b < nb && mok; ++b) {
+            const int klo = s.qband.klo[b], khi = s.qband.khi[b];
+            if (khi - s0v[b] > 32 || khi - klo > 28 || s.qband.nrows[b] > DSCE_RB) mok = false;
+            ksq = std::max(ksq, (khi - klo + 3) / 4);
+        }
+        s.k.pm_ok = mok ? 1 : 0;
+        if (mok) {
+            const long long stride = (long long)(2 * 6 + 2 * ksq) * 64;
+            std::vector<double2> pa((size_t)stride * nb, make_double2(0, 0));
+            for (int b = 0; b < nb; ++b) {
+                const int r0 = s.qband.row0[b], nr = s.qband.nrows[b], klo = s.qband.klo[b], khi = s.qband.khi[b];
+                double2* g = pa.data() + (size_t)stride * b;
+                double2* q = g + 2 * 6 * 64;
+                for (int t = 0; t < 2; ++t)
+                    for (int l = 0; l < 64; ++l) {
+                        for (int k = 0; k < 6; ++k) {            // G[s0 + 16t + (l&15)][r0 + 4k + (l>>4)]
+                            const int n = s0v[b] + 16 * t + (l & 15), col = r0 + 4 * k + (l >> 4);
+                            if (n < khi && col < r0 + DSCE_RB && col < LK)
+                                g[((size_t)t * 6 + k) * 64 + l] = s.G[(size_t)col * N + n];
+                        }
+                        for (int k = 0; k < ksq; ++k) {          // Q^H[r0 + 16t + (l&15)][klo + 4k + (l>>4)]
+                            const int r = 16 * t + (l & 15), n = klo + 4 * k + (l >> 4);
+                            if (r < nr && n < khi)
+                                q[((size_t)t * ksq + k) * 64 + l] = s.qband.vals[s.qband.off[b] + (size_t)(n - klo) * DSCE_RB + r];
+                        }
+                    }
+            }
+            s.k.pm_ksq = ksq;
+            s.k.pm_stride = stride;
+            s.k.pm_a = dupload(c, pa);
+        }
     }
     // W band: rows r, k = (c, p); c overlaps where Q-support(r) meets (H G)-support(c)
     int maxd = 0;
@@ -823,24 +857,36 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
             // stage, MFMA-bound) on the main stream and perfect CSI (perfect_ic,
             // HBM-bound) on stream2, overlapping; joined before the next chunk.
             const bool two = pfuse && c->streams2;
+            // pic_ok schemes (OFDM): the whole perfect-CSI chain is one kernel
+            // (k_pic_chain, u in registers across the iterations)
+            const bool chain = pfuse && perfect_chain_ok(s.k, c->ch, b);
             for (int it = 0; it <= c->niter; ++it) {
-                if (it == 1 && two) {
-                    DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
-                    DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-                    for (int jt = 1; jt <= c->niter; ++jt) {
-                        Timed t(c, "perfect_ic", c->stream2);
-                        PerfectDetectArgs pd{c->d_counters, (int)si, jt, c->niter + 1, c->nsnr, jt == c->niter,
-                                             s.k.slI, s.k.slQ};
-                        launch_perfect_ic(c->stream2, s.k, c->ch, b, &pd);
+                if (it == 1 && (two || chain)) {
+                    hipStream_t ps = two ? c->stream2 : c->stream;
+                    if (two) {
+                        DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
+                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
                     }
-                    DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
+                    if (chain) {
+                        Timed t(c, "perfect_ic", ps);
+                        PerfectDetectArgs pd{c->d_counters, (int)si, 1, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
+                        launch_perfect_chain(ps, s.k, c->ch, b, &pd, c->niter);
+                    } else {
+                        for (int jt = 1; jt <= c->niter; ++jt) {
+                            Timed t(c, "perfect_ic", ps);
+                            PerfectDetectArgs pd{c->d_counters, (int)si, jt, c->niter + 1, c->nsnr, jt == c->niter,
+                                                 s.k.slI, s.k.slQ};
+                            launch_perfect_ic(ps, s.k, c->ch, b, &pd);
+                        }
+                    }
+                    if (two) DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
                 }
                 if (it > 0) {
                     {
                         Timed t(c, "k_wcontract");
                         launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
                     }
-                    if (!two) {
+                    if (!two && !chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
                                              s.k.slI, s.k.slQ};

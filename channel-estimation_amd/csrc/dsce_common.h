@@ -158,6 +158,15 @@ struct SchemeK {
     const int* pic_s0;
     const long long* pic_goff;
     const double2* pic_g;
+    // MFMA form of the perfect-CSI chain (k_pic_mfma; pic_ok blocks with at most
+    // 32 window samples, 28 FFT-window samples, 24 rows, max tap delay <= 1):
+    // per Q^H block the A operands of v_mfma_f64_16x16x4 in lane order,
+    // [tile 2][k-step 6][lane 64] of G (rows = window samples s0.., k = the
+    // block's 24 columns) then [tile 2][k-step pm_ksq][lane 64] of Q^H (rows =
+    // the block's rows, k = samples klo..); block stride pm_stride elements
+    int pm_ok, pm_ksq;
+    long long pm_stride;
+    const double2* pm_a;
 };
 
 struct ChannelK {

@@ -65,6 +65,11 @@ struct PerfectDetectArgs {
     double sI, sQ;   // 1 / slicer step (I, Q)
 };
 void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd);
+// The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
+// registers (pic_ok schemes with 1-3 taps); perfect_chain_ok tells when it applies.
+bool perfect_chain_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
+void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                          const PerfectDetectArgs* pd, int niter);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)

@@ -15,6 +15,7 @@
 #include "dsce_kernels.h"
 
 #include <math.h>
+#include <algorithm>
 #include <type_traits>
 #include <stdlib.h>
 #include <string.h>
@@ -848,6 +849,351 @@ __global__ void __launch_bounds__(64) k_pic(SchemeK sk, BandOrder ord, const dou
     o.finish(lane);
 }
 
+// The whole perfect-CSI IC chain (iterations 1..n_iter, script:541-561) in one
+// kernel for pic_ok schemes (OFDM): D = Q'HG is block-diagonal there, so the
+// chain of a (unit, Q^H block) never needs another block, and u (the block's
+// re-precoded perfect-CSI decisions) stays in registers across the iterations.
+// A lane PAIR owns a unit: lane h of the pair holds u and the accumulators of
+// the block's rows 12h..12h+11 (48 + 48 VGPRs instead of 96 + 96 for one lane
+// per unit, so 3 waves/SIMD instead of 1).  Per iteration and sample n of the
+// block window [s0, khi): t[n] = G[n, :] u (each lane its 12 columns, the pair
+// adds the halves with one DPP swap; kept in a sliding window of DMAX + 1
+// samples for the tap delays), (H t)[n] = sum_q IR[q][n] t[n - d_q], and
+// acc += Q^H[rows, n] (H t)[n]; then per row y_perf = y - acc + h u, one-tap
+// equalisation by h, slicer, error counts of stage `it`, and the new decision
+// replaces u.  Only y, h, the taps and the transmitted symbol indices are read
+// (L2-shared by the SNR points of a realisation); nothing but the counters is
+// written.  Replaces n_iter x (G u pass + k_band<LoadChannelApplied,
+// StorePerfectDetect>), which moved t, u and y through HBM every iteration.
+// Block = 256 threads = 128 units of one Q^H block (the block's G rows and
+// Q^H columns staged once in LDS); grid: Q^H blocks x units/128, SNR-fastest
+// XCD-aware order (BandOrder with 128-unit groups).
+static constexpr int PCH_UNITS = 128;
+static constexpr int PCH_HALF = DSCE_RB / 2;
+
+__device__ __forceinline__ double swap_pair(double v) {
+    // exchange with the neighbouring lane (quad_perm [1, 0, 3, 2])
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0xb1, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(lo, 0xb1, 0xf, 0xf, false));
+}
+
+template <int NT, int DMAX>
+__global__ void __launch_bounds__(256) k_pic_chain(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
+                                                   TapDelays dl, StorePerfectDetect o, int niter) {
+    extern __shared__ double2 pic_lds[];
+    __shared__ int pc_cnt[8];
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int tid = threadIdx.x, half = tid & 1;
+    const int lane = ug * PCH_UNITS + (tid >> 1);             // unit
+    const int U = o.U, R = o.R, rl = lane % R;
+    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk], khi = sk.QH.khi[blk];
+    const int s0 = sk.pic_s0[blk];
+    const int rh = PCH_HALF * half;                           // first row / column of this lane's half
+    // LDS: constellation (256) + slicer tables, then the block's G rows [s0, khi)
+    // x 24 and Q^H columns [klo, khi) x 24 (read as broadcasts)
+    double2* sym = pic_lds;
+    SlicerLds* slt = (SlicerLds*)(pic_lds + 256);
+    double2* sg = pic_lds + 256 + (sizeof(SlicerLds) + 15) / 16;
+    const int ng = (khi - s0) * DSCE_RB, nq = (khi - klo) * DSCE_RB;
+    double2* sq = sg + ng;
+    {
+        const double2* __restrict__ gsrc = sk.pic_g + sk.pic_goff[blk];
+        const double2* __restrict__ qsrc = sk.QH.vals + sk.QH.off[blk];
+        const double2 sv = tid < o.M ? o.symbols[tid] : make_double2(0.0, 0.0);
+        const int gv = tid < o.nI * o.nQ ? o.grid_sym[tid] : 0;
+        const double li = tid < o.nI && tid < 16 ? o.lvI[tid] : 0.0;
+        const double lq = tid < o.nQ && tid < 16 ? o.lvQ[tid] : 0.0;
+        for (int i = tid; i < ng; i += 256) sg[i] = gsrc[i];
+        for (int i = tid; i < nq; i += 256) sq[i] = qsrc[i];
+        sym[tid] = sv;
+        slt->grid[tid] = gv;
+        if (tid < 16) {
+            slt->lvI[tid] = li;
+            slt->lvQ[tid] = lq;
+        }
+    }
+    double2 ur[PCH_HALF];
+#pragma unroll
+    for (int c = 0; c < PCH_HALF; ++c)
+        ur[c] = rh + c < nrows ? o.u[(size_t)(row0 + rh + c) * U + lane] : make_double2(0.0, 0.0);
+    __syncthreads();
+    int dsel[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) dsel[q] = dl.d[q];
+    const int snr = o.snr0 + (ug * PCH_UNITS) / R;
+    for (int it = 1; it <= niter; ++it) {
+        int oz = 0;                                           // opaque zero: no hoisting of the
+        asm volatile("" : "+v"(oz));                          // per-iteration loads out of the loop
+        double2 acc[PCH_HALF];
+#pragma unroll
+        for (int r = 0; r < PCH_HALF; ++r) acc[r] = make_double2(0.0, 0.0);
+        double2 tw[DMAX + 1];
+#pragma unroll
+        for (int j = 0; j <= DMAX; ++j) tw[j] = make_double2(0.0, 0.0);
+        double2 hcur[NT], hnxt[NT];
+#pragma unroll
+        for (int q = 0; q < NT; ++q) hcur[q] = ir[((size_t)q * N + klo + oz) * R + rl];
+        for (int n = s0 + oz; n < khi; ++n) {
+            const bool out_row = n >= klo;
+            if (out_row) {
+                const int nn = n + 1 < khi ? n + 1 : n;
+#pragma unroll
+                for (int q = 0; q < NT; ++q) hnxt[q] = ir[((size_t)q * N + nn) * R + rl];
+            }
+            // t[n] = G[n, :] u: this lane's 12 columns in 3 chains, pair sum by DPP
+            const double2* gr = sg + (n - s0) * DSCE_RB + rh;
+            double2 t0 = make_double2(0.0, 0.0), t1 = t0, t2 = t0;
+#pragma unroll
+            for (int c = 0; c < PCH_HALF; c += 3) {
+                c_fma(t0, gr[c], ur[c]);
+                c_fma(t1, gr[c + 1], ur[c + 1]);
+                c_fma(t2, gr[c + 2], ur[c + 2]);
+            }
+            const double2 tp = c_add(c_add(t0, t1), t2);
+#pragma unroll
+            for (int j = DMAX; j > 0; --j) tw[j] = tw[j - 1];
+            tw[0] = make_double2(tp.x + swap_pair(tp.x), tp.y + swap_pair(tp.y));   // a + b == b + a: same on both lanes
+            if (out_row) {
+                double2 x = make_double2(0.0, 0.0);
+#pragma unroll
+                for (int q = 0; q < NT; ++q) {
+                    double2 tq = tw[0];
+#pragma unroll
+                    for (int j = 1; j <= DMAX; ++j)
+                        if (dsel[q] == j) tq = tw[j];
+                    c_fma(x, hcur[q], tq);
+                }
+                const double2* qk = sq + (n - klo) * DSCE_RB + rh;
+#pragma unroll
+                for (int r = 0; r < PCH_HALF; ++r) c_fma(acc[r], qk[r], x);
+#pragma unroll
+                for (int q = 0; q < NT; ++q) hcur[q] = hnxt[q];
+            }
+        }
+        // epilogue: this lane's 12 rows in groups of 4, every input of a group first
+        int c0 = 0, c1 = 0;
+        const bool last = it == niter;
+#pragma unroll
+        for (int g0 = 0; g0 < PCH_HALF; g0 += 4) {
+            double2 yv[4], hv[4], pv[4];
+            int tx[4], dd[4], cn[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = rh + g0 + k;
+                const int row = row0 + (r < nrows ? r : 0) + oz;
+                dd[k] = r < nrows ? o.row_data[row] : -1;
+                cn[k] = o.row_cons[row];
+                pv[k] = o.row_pval[row];
+                yv[k] = o.y[(size_t)row * U + lane];
+                hv[k] = o.h[(size_t)row * R + rl];
+                tx[k] = o.sidx[(size_t)(dd[k] > 0 ? dd[k] : 0) * R + rl];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = g0 + k;
+                if (dd[k] < 0) continue;
+                double2 rr = c_sub(yv[k], acc[r]);
+                rr = c_add(rr, c_mul(hv[k], ur[r]));
+                const double2 z = c_div1(rr, hv[k]);
+                const int dp = slice_fast(*slt, o.nI, o.nQ,
+                                          o.real_detect ? make_double2(z.x * o.idd, 0.0)
+                                                        : make_double2(z.x * o.idd, z.y * o.idd),
+                                          o.sI, o.sQ);
+                const int ne = __popc((unsigned)(dp ^ tx[k]));
+                c0 += ne;
+                c1 += cn[k] ? ne : 0;
+                if (!last) {
+                    double2 av = make_double2(0.0, 0.0);
+                    c_fma(av, pv[k], sym[dp]);
+                    ur[r] = av;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const int s_0 = wave_sum(c0), s_1 = wave_sum(c1);
+        if ((tid & 63) < 2) {
+            const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + ((tid & 1) ? (size_t)o.cstride_edge : 0);
+            const int v = (tid & 1) ? s_1 : s_0;
+            if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+        }
+    }
+    (void)pc_cnt;
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+
+// ---------------------------------------------------------------------------
+// The perfect-CSI IC chain on the matrix cores (k_pic_mfma, SchemeK::pm_ok: OFDM
+// at C2).  Per Q^H block and IC iteration the chain is two small GEMMs whose A
+// operands are shared by every unit and whose B operands are the units:
+//   T   (window samples x units) = G_blk (samples x 24 columns) U (24 x units)
+//   acc (24 rows x units)        = Q^H_blk (rows x KW samples)  X (KW x units),
+//   X[j][u] = sum_q IR_q[klo + j][u] T[j + maxd - d_q][u]      (H, per unit)
+// on v_mfma_f64_16x16x4_f64 (complex = 4 real MFMAs).  A wave owns 16 units;
+// the D layout (row (lane>>4) + 4 reg, col lane&15) of a 16-row tile register
+// r is exactly the B operand of k-step 4 tile + r, so U (decisions, kept in
+// registers across the iterations) and T feed the next GEMM without data
+// movement; the one-sample shift of the delayed tap is one lane shuffle.  The
+// epilogue (y_perf = y - acc + h u, one-tap by h, slicer, counts, re-precoded
+// decision into U) runs on the D layout of acc, 8 rows per lane.  Only y, h,
+// the taps and the transmitted symbol indices are read; nothing but the
+// counters is written.  Block = 4 waves = 64 units of one Q^H block (its A
+// tables staged in LDS once); grid: Q^H blocks x units/64, SNR-fastest
+// XCD-aware order.
+template <int KSQ>
+__global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
+                                                  int d0, int d1, int ntap, StorePerfectDetect o, int niter) {
+    extern __shared__ double2 pm_lds[];
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const int U = o.U, R = o.R;
+    const int unit = ug * WAVE + w * 16 + (l & 15);
+    const int rl = unit % R;
+    const int kq = l >> 4;
+    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk];
+    constexpr int NA = (2 * 6 + 2 * KSQ) * 64;
+    double2* sa = pm_lds;                                       // A tables
+    double2* sym = pm_lds + NA;
+    SlicerLds* slt = (SlicerLds*)(sym + 256);
+    {
+        const double2* __restrict__ src = sk.pm_a + (size_t)sk.pm_stride * blk;
+        for (int i = tid; i < NA; i += 256) sa[i] = src[i];
+        sym[tid] = tid < o.M ? o.symbols[tid] : make_double2(0.0, 0.0);
+        slt->grid[tid] = tid < o.nI * o.nQ ? o.grid_sym[tid] : 0;
+        if (tid < 16) {
+            slt->lvI[tid] = tid < o.nI ? o.lvI[tid] : 0.0;
+            slt->lvQ[tid] = tid < o.nQ ? o.lvQ[tid] : 0.0;
+        }
+    }
+    const double2* ga = sa;
+    const double2* qa = sa + 2 * 6 * 64;
+    // U in D layout: ur[t][r] = u[row0 + 16 t + kq + 4 r][unit]
+    double2 ur[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = 16 * t + kq + 4 * r;
+            ur[t][r] = row < nrows ? o.u[(size_t)(row0 + row) * U + unit] : make_double2(0.0, 0.0);
+        }
+    __syncthreads();
+    // tap delay offsets into T: X[j] uses T[j + maxd - d_q] (maxd <= 1)
+    const int maxd = max(d0, ntap > 1 ? d1 : 0);
+    const int c0 = maxd - d0, c1 = maxd - d1;
+    const int src_lane = (l + 16) & 63;
+    const int snr = o.snr0 + (ug * WAVE) / R;
+    for (int it = 1; it <= niter; ++it) {
+        // the loads below are the same every iteration: an opaque zero keeps the
+        // compiler from hoisting them out of the loop (they would stay live
+        // across it and triple the register footprint)
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+        // GEMM1: T = G U (2 row tiles x 6 k-steps)
+        d4 tre[2], tim[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            tre[t] = (d4){0.0, 0.0, 0.0, 0.0};
+            tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double2 b = ur[k >> 2][k & 3];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const double2 a = ga[(t * 6 + k) * 64 + l];
+                tre[t] = MFMA64(a.x, b.x, tre[t]);
+                tre[t] = MFMA64(-a.y, b.y, tre[t]);
+                tim[t] = MFMA64(a.x, b.y, tim[t]);
+                tim[t] = MFMA64(a.y, b.x, tim[t]);
+            }
+        }
+        // X in B layout (k-step s: sample klo + 4 s + kq) and GEMM2: acc = Q^H X
+        d4 are[2], aim[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            are[t] = (d4){0.0, 0.0, 0.0, 0.0};
+            aim[t] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int k = 0; k < KSQ; ++k) {
+            // T row j = 4k + kq is register (k&3) of tile k>>2 in this lane; row
+            // j + 1 comes from lane l + 16 (register k), or for kq == 3 from lane
+            // l - 48 (register k + 1)
+            const double2 tc = make_double2(tre[k >> 2][k & 3], tim[k >> 2][k & 3]);
+            const int kn = k + 1 < 8 ? k + 1 : 7;
+            const double2 tn = make_double2(tre[kn >> 2][kn & 3], tim[kn >> 2][kn & 3]);
+            const double2 sv = l >= 16 ? tc : tn;
+            const double2 t1 = make_double2(__shfl(sv.x, src_lane), __shfl(sv.y, src_lane));
+            const int n = klo + 4 * k + kq + oz;
+            const int nc = n < N ? n : N - 1;
+            const double2 h0 = ir[(size_t)nc * R + rl];
+            double2 x = make_double2(0.0, 0.0);
+            c_fma(x, h0, c0 ? t1 : tc);
+            if (ntap > 1) {
+                const double2 h1 = ir[((size_t)N + nc) * R + rl];
+                c_fma(x, h1, c1 ? t1 : tc);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const double2 a = qa[(t * KSQ + k) * 64 + l];
+                are[t] = MFMA64(a.x, x.x, are[t]);
+                are[t] = MFMA64(-a.y, x.y, are[t]);
+                aim[t] = MFMA64(a.x, x.y, aim[t]);
+                aim[t] = MFMA64(a.y, x.x, aim[t]);
+            }
+        }
+        // epilogue on the D layout of acc: 8 rows per lane, one tile at a time
+        int e0 = 0, e1 = 0;
+        const bool last = it == niter;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            double2 yv[4], hv[4], pv[4];
+            int tx[4], dd[4], cn[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int rr = 16 * t + kq + 4 * r;
+                const int row = row0 + (rr < nrows ? rr : 0) + oz;
+                dd[r] = rr < nrows ? o.row_data[row] : -1;
+                cn[r] = o.row_cons[row];
+                pv[r] = o.row_pval[row];
+                yv[r] = o.y[(size_t)row * U + unit];
+                hv[r] = o.h[(size_t)row * R + rl];
+                tx[r] = o.sidx[(size_t)(dd[r] > 0 ? dd[r] : 0) * R + rl];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (dd[r] < 0) continue;
+                double2 yp = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
+                yp = c_add(yp, c_mul(hv[r], ur[t][r]));
+                const double2 z = c_div1(yp, hv[r]);
+                const int dp = slice_fast(*slt, o.nI, o.nQ,
+                                          o.real_detect ? make_double2(z.x * o.idd, 0.0)
+                                                        : make_double2(z.x * o.idd, z.y * o.idd),
+                                          o.sI, o.sQ);
+                const int ne = __popc((unsigned)(dp ^ tx[r]));
+                e0 += ne;
+                e1 += cn[r] ? ne : 0;
+                if (!last) {
+                    double2 av = make_double2(0.0, 0.0);
+                    c_fma(av, pv[r], sym[dp]);
+                    ur[t][r] = av;
+                }
+            }
+        }
+        const int s_0 = wave_sum(e0), s_1 = wave_sum(e1);
+        if (l < 2) {
+            const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (l ? (size_t)o.cstride_edge : 0);
+            const int v = l ? s_1 : s_0;
+            if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+        }
+    }
+}
+
 template <int NT, class Out>
 static void launch_pass2(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
                          const Out& o, size_t lds) {
@@ -873,6 +1219,87 @@ static void launch_pass2_nt(hipStream_t s, const SchemeK& sk, const ChannelK& ch
         case 5: launch_pass2<5>(s, sk, ch, b, ord, o, lds); break;
         case 6: launch_pass2<6>(s, sk, ch, b, ord, o, lds); break;
         default: launch_pass2<0>(s, sk, ch, b, ord, o, lds); break;
+    }
+}
+
+// (ntap, max delay) pairs with a k_pic_chain instance
+static int pic_chain_variant(const ChannelK& ch) {
+    int md = 0;
+    for (int q = 0; q < ch.ntap; ++q) md = std::max(md, ch.tap_delay[q]);
+    if (ch.ntap == 1 && md == 0) return 1;
+    if (ch.ntap == 2 && md == 1) return 2;
+    if (ch.ntap == 3 && md == 2) return 3;
+    return 0;
+}
+
+// DSCE_PIC_CHAIN: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 (default) =
+// k_pic_mfma where the scheme allows it, else k_pic_chain
+static int pic_chain_mode() {
+    const char* e = getenv("DSCE_PIC_CHAIN");
+    return e ? atoi(e) : 2;
+}
+
+static bool pic_mfma_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    return sk.pm_ok && pic_chain_mode() == 2 && ch.ntap <= 2 && (sk.pm_ksq == 6 || sk.pm_ksq == 7) &&
+           ((size_t)(b.U / WAVE) * sk.QH.nblk) % 8 == 0;
+}
+
+bool perfect_chain_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    if (pic_mfma_ok(sk, ch, b)) return true;
+    return sk.pic_ok && pic_chain_variant(ch) && pic_chain_mode() != 0 && b.R % PCH_UNITS == 0 &&
+           ((size_t)(b.U / PCH_UNITS) * sk.QH.nblk) % 8 == 0;
+}
+
+void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                          const PerfectDetectArgs* pd, int niter) {
+    StorePerfectDetect o{};
+    o.y = b.y;
+    o.h = b.h;
+    o.u = b.u;
+    o.sidx = b.sidx;
+    o.row_data = sk.row_data;
+    o.row_cons = sk.row_cons;
+    o.row_pval = sk.row_pval;
+    o.symbols = sk.symbols;
+    o.lvI = sk.lvI;
+    o.lvQ = sk.lvQ;
+    o.grid_sym = sk.grid_sym;
+    o.counters = pd->counters;
+    o.cidx0 = ((((size_t)pd->scheme * 2 + 1) * 2 + 0) * pd->nsnr) * pd->nstage;   // stage added per iteration
+    o.cstride_edge = pd->nsnr * pd->nstage;
+    o.cstride_snr = pd->nstage;
+    o.U = b.U;
+    o.R = b.R;
+    o.snr0 = b.snr0;
+    o.M = sk.M;
+    o.nI = sk.nI;
+    o.nQ = sk.nQ;
+    o.real_detect = sk.real_detect;
+    o.idd = 1.0 / sk.data_div;
+    o.sI = pd->sI;
+    o.sQ = pd->sQ;
+    TapDelays dl{};
+    for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
+    const char* xe = getenv("DSCE_XCD");
+    if (pic_mfma_ok(sk, ch, b)) {
+        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, (!xe || xe[0] != '0') ? 1 : 0};
+        const size_t lds = ((size_t)(2 * 6 + 2 * sk.pm_ksq) * 64 + 256) * sizeof(double2) + sizeof(SlicerLds);
+        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+        const int d1 = ch.ntap > 1 ? ch.tap_delay[1] : 0;
+        if (sk.pm_ksq == 6)
+            hipLaunchKernelGGL(k_pic_mfma<6>, grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, ch.ntap, o, niter);
+        else
+            hipLaunchKernelGGL(k_pic_mfma<7>, grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, ch.ntap, o, niter);
+        return;
+    }
+    const BandOrder ord{b.U / PCH_UNITS, b.U / b.R, b.R / PCH_UNITS, (!xe || xe[0] != '0') ? 1 : 0};
+    const size_t plds = 256 * sizeof(double2) + sizeof(SlicerLds) + 16 + (size_t)sk.pic_rows * DSCE_RB * sizeof(double2);
+    const dim3 grid((b.U / PCH_UNITS) * sk.QH.nblk), blk(256);
+    switch (pic_chain_variant(ch)) {
+        case 1: hipLaunchKernelGGL((k_pic_chain<1, 0>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
+        case 2: hipLaunchKernelGGL((k_pic_chain<2, 1>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
+        case 3: hipLaunchKernelGGL((k_pic_chain<3, 2>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
+        default: break;
     }
 }
 
@@ -952,9 +1379,6 @@ void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McB
 // tiles) -> 32 MFMAs per 4-deep k step.  Block = 4 waves = 256 units.
 // grid (U/256, nblk).
 // ---------------------------------------------------------------------------
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 // one complex 16x16x4 tile: (re, im) += W (16 rows x 4 k) * Z (4 k x 16 units)
 #define CTILE(RE, IM, W, Z)                 \
     RE = MFMA64((W).x, (Z).x, RE);          \
