@@ -138,6 +138,18 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
                                (int32_t)mxGetScalar(prhs[3]), cplx(prhs[4], &t), n,
                                (double*)mxGetComplexDoubles(plhs[0])), "dsce_mmse_onetap");
         if (t) mxDestroyArray(t);
+    } else if (!strcmp(cmd, "set_noise_slot")) {
+        /* dsce_mex('set_noise_slot', id, slot)  (SimpleVersion_DoublyFlat.m:125-126) */
+        check(dsce_set_noise_slot(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, (int32_t)mxGetScalar(prhs[2])),
+              "dsce_set_noise_slot");
+    } else if (!strcmp(cmd, "set_interpolation")) {
+        /* dsce_mex('set_interpolation', id, I): I = LK x NP weights of a
+           PilotSymbolAidedChannelEstimation ('linear', 'MovingBlockAverage', ...),
+           e.g. obtained by applying ChannelInterpolation to the NP unit vectors */
+        mxArray* t = NULL;
+        check(dsce_set_interpolation(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, cplx(prhs[2], &t)),
+              "dsce_set_interpolation");
+        if (t) mxDestroyArray(t);
     } else {
         mexErrMsgIdAndTxt("dsce:usage", "unknown command '%s'", cmd);
     }
