@@ -130,6 +130,12 @@ struct dsce_ctx {
     std::vector<void*> buf_allocs;
     unsigned long long* d_counters = nullptr;
     size_t counters_n = 0;
+    // channel-estimation MSE (dsce_enable_mse): device sums of the current
+    // dsce_run, host totals since the last enable
+    bool mse = false;
+    double* d_mse = nullptr;                 // [err: ns * nsnr * nstage][pow: ns * nsnr]
+    size_t mse_n = 0;
+    std::vector<double> mse_host;
     std::vector<void*> allocs;
     bool timing = false;
     std::map<std::string, std::pair<int64_t, double>> ktime;
@@ -1132,6 +1138,32 @@ static void prepare_run(dsce_ctx* ctx) {
         ctx->counters_n = n;
     }
     DSCE_HIP_CHECK(hipMemsetAsync(ctx->d_counters, 0, n * sizeof(unsigned long long), ctx->stream));
+    ctx->buf.mse_err = ctx->buf.mse_pow = nullptr;
+    if (ctx->mse) {
+        const size_t ns = ctx->schemes.size(), ne = ns * ctx->nsnr * (ctx->niter + 1), np = ns * ctx->nsnr;
+        if (ctx->mse_n != ne + np) {
+            if (ctx->d_mse) free_alloc(ctx, ctx->d_mse);
+            ctx->d_mse = dalloc<double>(ctx, ne + np);
+            ctx->mse_n = ne + np;
+        }
+        if (ctx->mse_host.size() != ne + np) ctx->mse_host.assign(ne + np, 0.0);
+        DSCE_HIP_CHECK(hipMemsetAsync(ctx->d_mse, 0, (ne + np) * sizeof(double), ctx->stream));
+    }
+}
+
+static void set_mse_buffers(dsce_ctx* ctx) {
+    if (!ctx->mse) return;
+    const size_t ne = ctx->schemes.size() * ctx->nsnr * (ctx->niter + 1);
+    ctx->buf.mse_err = ctx->d_mse;
+    ctx->buf.mse_pow = ctx->d_mse + ne;
+}
+
+static void collect_mse(dsce_ctx* ctx) {
+    if (!ctx->mse) return;
+    std::vector<double> h(ctx->mse_n);
+    DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_mse, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < h.size(); ++i) ctx->mse_host[i] += h[i];
 }
 
 int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
@@ -1145,6 +1177,7 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
         const uint64_t left = n_rep - done;
         const int R = (int)std::min<uint64_t>((uint64_t)ctx->batch, left);
         ensure_buffers(ctx, R <= ctx->batch ? ctx->batch : R);
+        set_mse_buffers(ctx);
         run_batch(ctx, seed, first_rep + done, R, R, nullptr);
         done += (uint64_t)R;
     }
@@ -1154,6 +1187,7 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->timing) collect_timing(ctx);
     for (size_t i = 0; i < h.size(); ++i) err_counts[i] += (int64_t)h[i];
+    collect_mse(ctx);
     API_END
 }
 
@@ -1367,6 +1401,28 @@ int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
     s.Wp3 = nullptr;
     s.interp = true;
     upload_interp(ctx, s);
+    API_END
+}
+
+int dsce_enable_mse(dsce_ctx* ctx, int32_t enable) {
+    API_BEGIN
+    check_ctx(ctx);
+    ctx->mse = enable != 0;
+    ctx->mse_host.clear();
+    API_END
+}
+
+int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!ctx->mse) throw ApiError(DSCE_ESTATE, "dsce_enable_mse first");
+    const size_t ns = ctx->schemes.size(), ne = ns * ctx->nsnr * (ctx->niter + 1), np = ns * ctx->nsnr;
+    for (size_t i = 0; i < ne; ++i) {
+        if (err_sum) err_sum[i] = ctx->mse_host.size() == ne + np ? ctx->mse_host[i] : 0.0;
+    }
+    for (size_t i = 0; i < np; ++i) {
+        if (pow_sum) pow_sum[i] = ctx->mse_host.size() == ne + np ? ctx->mse_host[ne + i] : 0.0;
+    }
     API_END
 }
 

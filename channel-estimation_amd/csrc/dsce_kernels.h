@@ -32,6 +32,8 @@ struct McBuffers {
     double2* e2;      // [LK][U]   y_perf ./ h     (one-tap quotient, perfect CSI)
     uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
+    double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
+    double* mse_pow;  // [scheme][snr] sums of |h|^2
 };
 
 struct MmseK {

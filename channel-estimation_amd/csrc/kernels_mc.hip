@@ -33,6 +33,24 @@ __device__ __forceinline__ int wave_sum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Channel-estimation MSE of one stage (build-defined; the reference computes no
+// MSE): sum over units and rows of |h_hat - h|^2 (h = diag(D), the perfect-CSI
+// one-tap channel) into err[(scheme * nsnr + snr) * nstage + stage], and of
+// |h|^2 into pow[scheme * nsnr + snr] at stage 0.  One fp64 atomic per wave.
+__device__ __forceinline__ void flush_mse(double e, double pw, double* err, double* pow, int scheme, int nsnr, int snr,
+                                          int nstage, int stage) {
+    const double te = wave_sum_d(e), tp = wave_sum_d(pw);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&err[((size_t)scheme * nsnr + snr) * nstage + stage], te);
+        if (stage == 0) atomicAdd(&pow[(size_t)scheme * nsnr + snr], tp);
+    }
+}
 
 // Slicer tables staged in LDS (levels and the level-grid -> symbol map are
 // gathered per lane; from global memory these gathers were the stage's latency
@@ -1863,6 +1881,8 @@ struct StageArgs {
     int stage, var, nsnr, nstage, scheme, last, trace, perfect, R, U, snr0, xcd_order;
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
+    double* mse_err;           // null: no MSE accumulation (see flush_mse)
+    double* mse_pow;
 };
 
 // (1) LS pilot estimates, h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p and the
@@ -1888,14 +1908,22 @@ __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const 
     const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP;
     const int r0 = blockIdx.y * DSCE_RB;
     const int r1 = min(sk.LK, r0 + DSCE_RB);
+    double me = 0.0, mp = 0.0;
     for (int c = r0; c < r1; ++c) {
         double2 acc = make_double2(0.0, 0.0);
         for (int p = 0; p < sk.NP; ++p) c_fma(acc, wd[(size_t)c * sk.NP + p], shp[p * WAVE + threadIdx.x]);
         const size_t i = (size_t)c * U + unit;
+        const double2 hv = h[(size_t)c * R + rl];
         hest[i] = acc;
         e_est[i] = c_div(st.ysrc_e[i], acc);
-        e_perf[i] = c_div(st.ysrc_p[i], h[(size_t)c * R + rl]);
+        e_perf[i] = c_div(st.ysrc_p[i], hv);
+        if (st.mse_err) {
+            const double dx = acc.x - hv.x, dy = acc.y - hv.y;
+            me += dx * dx + dy * dy;
+            mp += hv.x * hv.x + hv.y * hv.y;
+        }
     }
+    if (st.mse_err) flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage);
 }
 
 // (2) data-symbol decisions and bit-error counts, grid (U/64, ceil(ND/32)).
@@ -1998,7 +2026,7 @@ __global__ void __launch_bounds__(64) k_ls(SchemeK sk, StageArgs st, const doubl
 // decisions for k_precode.  diag(D_hat) is written only for traces; the
 // contraction uses a W band with a zero diagonal, so nothing else reads it.
 // Flat grid, row block fastest (the blocks of one unit group share hP in L2).
-template <int NPT, int RB, bool PERF>
+template <int NPT, int RB, bool PERF, bool MSE>
 __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, int nrb, const double2* __restrict__ Wd,
                                                      const double2* __restrict__ xp,
                                                      const uint16_t* __restrict__ sidx,
@@ -2045,10 +2073,8 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
         const size_t ix = (size_t)row * U + unit;
         ye[r] = st.ysrc_e[ix];
         tx[r] = sidx[(size_t)(i > 0 ? i : 0) * R + rl];
-        if (PERF) {
-            yp[r] = same_y ? ye[r] : st.ysrc_p[ix];
-            hh[r] = h[(size_t)row * R + rl];
-        }
+        if (PERF) yp[r] = same_y ? ye[r] : st.ysrc_p[ix];
+        if (PERF || MSE) hh[r] = h[(size_t)row * R + rl];
     }
     // per-row scalars of the wave's rows, requested together (no dependent chains)
     int rdat[RB], rcons[RB], rpcol[RB];
@@ -2098,6 +2124,17 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
 #pragma unroll
         for (int r = 0; r < RB; ++r)
             if (r < nr) c_fma(acc[r], wds[r * NPT + p], hv);
+    }
+    if (MSE) {
+        double me = 0.0, mp = 0.0;
+#pragma unroll
+        for (int r = 0; r < RB; ++r)
+            if (r < nr) {
+                const double dx = acc[r].x - hh[r].x, dy = acc[r].y - hh[r].y;
+                me += dx * dx + dy * dy;
+                mp += hh[r].x * hh[r].x + hh[r].y * hh[r].y;
+            }
+        flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage);
     }
     const double idd = 1.0 / sk.data_div;
     const double sI = sk.slI, sQ = sk.slQ;
@@ -2165,12 +2202,20 @@ static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageA
         const int nrb = (sk.LK + 4 * (RBV) - 1) / (4 * (RBV));                                                  \
         StageArgs sa = st;                                                                                      \
         sa.xcd_order = xcd && ((ug * nrb) % 8) == 0;                                                            \
-        if (st.perfect)                                                                                         \
-            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb, mm.Wd, \
-                               b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);                 \
+        if (st.mse_err) {                                                                                       \
+            if (st.perfect)                                                                                     \
+                hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, true>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, \
+                                   nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters); \
+            else                                                                                                \
+                hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, true>), dim3(ug * nrb), dim3(256), 0, s, sk,  \
+                                   sa, nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u,       \
+                                   counters);                                                                   \
+        } else if (st.perfect)                                                                                  \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa,   \
+                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
         else                                                                                                    \
-            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, nrb,      \
-                               mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);          \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa,  \
+                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
         return true;                                                                                            \
     }
     if (rb == 4) LAUNCH_SF(4)
@@ -2208,6 +2253,8 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     st.xcd_order = 0;
     st.ysrc_e = stage == 0 ? b.y : b.yest;
     st.ysrc_p = stage == 0 ? b.y : b.yperf;
+    st.mse_err = b.mse_err;
+    st.mse_pow = b.mse_pow;
     const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
     // select-mode schemes: k_ls + one fused pass (DSCE_STAGE=split keeps the
     // 3-kernel path for A/B; DSCE_STAGE_RB = rows per fused block, 4 | 8 | 16)

@@ -21,7 +21,7 @@ EXPORTED = [
     "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
     "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
     "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
-    "dsce_set_noise_slot", "dsce_set_interpolation",
+    "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse",
 ]
 
 
@@ -91,6 +91,8 @@ def load_library(path=None):
     lib.dsce_tx_matrices.argtypes = [vp, C.POINTER(TxDesc), dp, dp]
     lib.dsce_set_noise_slot.argtypes = [vp, C.c_int32, C.c_int32]
     lib.dsce_set_interpolation.argtypes = [vp, C.c_int32, dp]
+    lib.dsce_enable_mse.argtypes = [vp, C.c_int32]
+    lib.dsce_get_mse.argtypes = [vp, dp, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -294,6 +296,20 @@ class Engine:
                   "dsce_mmse_onetap")
         h = out.view(np.complex128).reshape(n, sc.LK).T
         return h[:, 0] if one else h
+
+    # -- channel-estimation MSE (build-defined) ---------------------------------
+    def enable_mse(self, on=True):
+        """Start (and reset) the MSE sums of dsce_run (dsce_enable_mse)."""
+        self._chk(self.lib.dsce_enable_mse(self.h, int(bool(on))), "dsce_enable_mse")
+
+    def mse(self):
+        """(err [scheme][snr][stage] = sum |h_hat - h|^2, pow [scheme][snr] = sum |h|^2)
+        since enable_mse(); NMSE = err / pow[..., None]."""
+        ns = len(self.schemes)
+        err = np.zeros((ns, self.nsnr, 1 + self.niter))
+        pw = np.zeros((ns, self.nsnr))
+        self._chk(self.lib.dsce_get_mse(self.h, _dptr(err), _dptr(pw)), "dsce_get_mse")
+        return err, pw
 
     # -- measurement -----------------------------------------------------------
     def enable_timing(self, on=True):

@@ -8,7 +8,9 @@ realisation carries the same number of bits, so that mean equals total
 errors / total bits, which is what `ber()` returns.
 
 File format (JSON, one object): configuration, SNR grid, per-scheme bit counts,
-realisation count, the raw counters and the BER arrays; `save(..., npz=True)`
+realisation count, the raw counters and the BER arrays (plus, with
+`simulate --mse`, "nmse": [scheme][snr][stage] channel-estimation NMSE, a
+build-defined output the reference does not compute); `save(..., npz=True)`
 also writes the arrays to a sibling .npz.  `figures()` draws Figures 2-5 with
 the script's curve set, colours and markers (matplotlib, optional).
 """

@@ -26,6 +26,7 @@ def main(argv=None):
     ap.add_argument("--out", default=None, help="result JSON")
     ap.add_argument("--npz", action="store_true")
     ap.add_argument("--figures", default=None, help="directory for Figure2-5.png")
+    ap.add_argument("--mse", action="store_true", help="also accumulate the channel-estimation NMSE per stage")
     a = ap.parse_args(argv)
 
     from dsce import results
@@ -43,6 +44,8 @@ def main(argv=None):
     eng = build_engine(S, batch=min(a.batch, reps))
     setup_s = time.perf_counter() - t0
     counts = np.zeros(eng.counter_shape(), dtype=np.int64)
+    if a.mse:
+        eng.enable_mse()
     done, t0 = 0, time.perf_counter()
     step = min(a.batch, reps)
     while done < reps:
@@ -52,8 +55,11 @@ def main(argv=None):
         el = time.perf_counter() - t0
         print("%d%% Completed! Time Left: %.1f s" % (100 * done // reps, el / done * (reps - done)), flush=True)
     bits = np.array([eng.bits_per_rep(i) for i in range(len(names))])
-    res = results.make(S, names, counts, bits, reps, a.seed,
-                       extra={"setup_s": setup_s, "seconds": time.perf_counter() - t0})
+    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0}
+    if a.mse:
+        err, pw = eng.mse()
+        extra["nmse"] = {s: (err[i] / pw[i][:, None]).tolist() for i, s in enumerate(names)}
+    res = results.make(S, names, counts, bits, reps, a.seed, extra=extra)
     if a.out:
         results.save(a.out, res, npz=a.npz)
     if a.figures:

@@ -215,6 +215,18 @@ int dsce_get_W(dsce_ctx* ctx, int32_t scheme_id, int32_t snr_index, int32_t vari
 int dsce_trace_unit(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t rep, int32_t snr_index,
                     double* y, double* hp_stages, double* hest_stages, double* h_perfect);
 
+/* Channel-estimation MSE (build-defined: the reference computes no MSE, so
+ * this output is parity-unpinned against MATLAB and checked against the
+ * oracle only).  While enabled, every dsce_run adds, per scheme, SNR point and
+ * stage (0 = one-tap, i = IC iteration i), the sum over realisations and the
+ * LK positions of |h_hat - h|^2, h_hat = diag(D_hat) the stage's MMSE (or
+ * interpolation) estimate and h = diag(D) the perfect-CSI one-tap channel of
+ * script:450-466; and per scheme and SNR point the sum of |h|^2 (NMSE =
+ * err / pow).  err_sum [n_schemes][n_snr][1 + n_iter], pow_sum
+ * [n_schemes][n_snr], totals since the last dsce_enable_mse(ctx, 1). */
+int dsce_enable_mse(dsce_ctx* ctx, int32_t enable);
+int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum);
+
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, dsce_run records HIP events around every launch of each kernel
  * on the context's stream; dsce_kernel_time returns (launches, total ms). */

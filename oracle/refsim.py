@@ -237,12 +237,16 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
     ``mmse``: per scheme the dict from :func:`mmse_setup`.
 
     Returns dict(err=int64[ns, 2 csi, 2 edge, nsnr, 1+n_iter], borderline=int64[ns],
-    nbits=int64[ns, 2 edge]).
+    nbits=int64[ns, 2 edge], mse_err=float[ns, nsnr, 1+n_iter], mse_pow=float[ns, nsnr]).
+    The MSE sums (|h_hat - h|^2 per stage, |h|^2, h = diag(D)) are build-defined
+    (the reference computes none): the checker of dsce_get_mse.
     """
     ns = len(schemes)
     nsnr = len(pn_time)
     N = chan["N"]
     err = np.zeros((ns, 2, 2, nsnr, 1 + n_iter), dtype=np.int64)
+    mse_err = np.zeros((ns, nsnr, 1 + n_iter))
+    mse_pow = np.zeros((ns, nsnr))
     border = np.zeros(ns, dtype=np.int64)
     nbits = np.zeros((ns, 2), dtype=np.int64)
     for si, sc in enumerate(schemes):
@@ -306,6 +310,8 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                 hP = y[sc["pilot_pos"]] / xP / np.sqrt(sc["kappa"])              # script:412-414
                 Dest = (W[:, isnr].reshape(LK, LK, NP, order="F") * hP[None, None, :]).sum(axis=2)
                 hest = np.diag(Dest).copy()
+                mse_err[si, isnr, 0] += np.sum(np.abs(hest - h) ** 2)
+                mse_pow[si, isnr] += np.sum(np.abs(h) ** 2)
                 # one-tap, estimated (script:428-447)
                 _, idx, mg = detect(y / hest)
                 e = count(idx, mg)
@@ -333,6 +339,7 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                     Wv = W if it <= n_iter / 2 else W0                              # script:492
                     Dt = (Wv[:, isnr].reshape(LK, LK, NP, order="F") * hPt[None, None, :]).sum(axis=2)
                     ht = np.diag(Dt).copy()
+                    mse_err[si, isnr, it] += np.sum(np.abs(ht - h) ** 2)
                     _, idx, mg = detect(yic / ht)                                  # script:519-537
                     e = count(idx, mg)
                     err[si, 0, 0, isnr, it] += e[0]
@@ -350,7 +357,7 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                         trace.setdefault("ypc", []).append(ypc)
                         trace["hp_stages"][-1].append(hPt)
                         trace["hest_stages"][-1].append(ht)
-    return dict(err=err, borderline=border, nbits=nbits)
+    return dict(err=err, borderline=border, nbits=nbits, mse_err=mse_err, mse_pow=mse_pow)
 
 
 # ---------------------------------------------------------------------------

@@ -85,11 +85,14 @@ def test_error_counts_match_oracle(ofdm):
     S, eng, mm = ofdm
     sc = S.schemes["ofdm"]
     n = 64
+    eng.enable_mse()
     cg = eng.run(SEED, 0, n)
     res = refsim.simulate(SEED, 0, n, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm])
     co = res["err"]
     diff = np.abs(cg - co).sum()
     assert diff <= 8 * res["borderline"].sum(), (cg - co)
+    _check_mse(eng, res)
+    eng.enable_mse(False)
     b = eng.bits_per_rep(0)
     assert b[0] == sc.n_bits and b[1] == sc.considered_symbols.sum() * sc.bits_per_symbol
 
@@ -133,10 +136,24 @@ def test_fbmc_estimator_and_trace(fbmc):
 def test_fbmc_error_counts(fbmc):
     name, S, eng, mm = fbmc
     sc = S.schemes[name]
+    eng.enable_mse()
     cg = eng.run(SEED, 64, 64)
     res = refsim.simulate(SEED, 64, 64, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
                           [mm])
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
+    _check_mse(eng, res)
+    eng.enable_mse(False)
+
+
+def _check_mse(eng, res):
+    """dsce_get_mse (build-defined channel-estimation MSE, parity unpinned vs
+    MATLAB) against the oracle's sums: fp64 sums of O(1e4) terms, 1e-9
+    relative; and a sane NMSE (below 1, decreasing with SNR at stage 0)."""
+    err, pw = eng.mse()
+    np.testing.assert_allclose(err, res["mse_err"], rtol=1e-9, atol=0)
+    np.testing.assert_allclose(pw, res["mse_pow"], rtol=1e-12, atol=0)
+    nmse = err[..., 0] / pw
+    assert np.all(nmse < 1) and np.all(np.diff(nmse, axis=-1) < 0)
 
 
 def test_three_schemes_share_channel_and_noise():
