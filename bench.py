@@ -162,7 +162,7 @@ def main():
     bits = eng.bits_per_rep(0)
     ber = counts[0, :, 0, :, :] / float(bits[0] * total_reps)
     kernels = {}
-    for k in ("k_jakes", "tx", "rx_front", "k_wcontract", "perfect_ic", "k_stage"):
+    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
         kernels[k] = {"launches": n, "ms": round(ms, 3)}
 
@@ -192,7 +192,8 @@ def main():
         "config": {"workload": "C2: OFDM 24sc x 14sym, N=540, Jakes 500 km/h VehA, 256-QAM, 16 pilots, "
                                "7 SNR (10:5:40 dB) x (one-tap + 4 IC) x (MMSE + perfect CSI)",
                    "reps_per_step_per_gpu": B, "engine_batch": args.batch, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "kernel": "k_wpair3 (pair-tile MMSE contraction, 3M; timed as k_wcontract)",
+        "roofline": {"bound": "mfma", "kernel": "k_wpair3<24,4,fused> (pair-tile MMSE contraction, 3M, with the "
+                               "next stage's diag(D_hat) + detection in its epilogue; timed as k_wcontract)",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
                      "traffic": traffic, "launches": launches,

@@ -92,6 +92,9 @@ struct Scheme {
     double2* Wd = nullptr;
     double2* Wp = nullptr;          // pair-tile copy of W for k_wpair (null: not eligible)
     double* Wp3 = nullptr;          // its Re / Im / Re+Im planes (3M complex products)
+    double2* Wpil = nullptr;        // fused MMSE stage operands (null: not eligible)
+    double2* WdA = nullptr;
+    int* pil_c0 = nullptr;
     long long wp_elems = 0, wp_exec = 0;
     PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
@@ -603,8 +606,35 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
     s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
     s.Wp3 = dalloc<double>(c, (size_t)nsl * 3 * s.wp_elems);
     setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3);
-    DSCE_HIP_CHECK(hipStreamSynchronize(c->stream));
-    DSCE_HIP_CHECK(hipGetLastError());
+    // fused MMSE stage: block-diagonal W (every block's columns are its own 24
+    // rows, OFDM), row-local precoder, select-mode detection, NP = 16
+    bool fuse = rbp == 24 && NP == 16 && s.k.p_diag && !s.d.despread;
+    for (int b = 0; b < nblk && fuse; ++b)
+        if (nrows[b] != 24 || s.wband.klo[b] / NP < row0[b] || s.wband.khi[b] / NP > row0[b] + 24) fuse = false;
+    if (fuse) {
+        std::vector<int> pblk(NP), pc0(NP);
+        for (int i = 0; i < NP; ++i) {
+            const int r = s.pilot_pos[i];
+            int bb = -1;
+            for (int b = 0; b < nblk; ++b)
+                if (r >= row0[b] && r < row0[b] + nrows[b]) bb = b;
+            if (bb < 0) fuse = false;
+            pblk[i] = bb;
+            pc0[i] = bb < 0 ? 0 : row0[bb];
+        }
+        if (fuse) {
+            int* dpb = dupload(c, pblk);
+            int* dpp = dupload(c, s.pilot_pos);
+            s.pil_c0 = dupload(c, pc0);
+            s.Wpil = dalloc<double2>(c, (size_t)nsl * NP * 24 * NP);
+            s.WdA = dalloc<double2>(c, (size_t)nsl * nblk * 2 * (NP / 4) * 64);
+            setup_fused_stage(c->stream, s.Wb, s.LK, NP, s.W, s.w_elems, s.Wd, nsl, dpb, dpp, 24, s.Wpil, s.WdA);
+            DSCE_HIP_CHECK(hipStreamSynchronize(c->stream));
+            DSCE_HIP_CHECK(hipGetLastError());
+            free_alloc(c, dpb);
+            free_alloc(c, dpp);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -637,8 +667,13 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         free_alloc(c, s.Wd);
         if (s.Wp) free_alloc(c, s.Wp);
         if (s.Wp3) free_alloc(c, s.Wp3);
+        if (s.Wpil) free_alloc(c, s.Wpil);
+        if (s.WdA) free_alloc(c, s.WdA);
+        if (s.pil_c0) free_alloc(c, s.pil_c0);
         s.W = s.Wd = s.Wp = nullptr;
         s.Wp3 = nullptr;
+        s.Wpil = s.WdA = nullptr;
+        s.pil_c0 = nullptr;
         s.wband = s.wband_struct;
         s.w_elems = s.wband.elems;
         s.Wb = upload_band(c, s.wband, false);
@@ -787,6 +822,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.yest = dalloc<double2>(c, LK * U, L);
     b.yperf = dalloc<double2>(c, LK * U, L);
     b.hp = dalloc<double2>(c, NP * U, L);
+    b.hp2 = dalloc<double2>(c, NP * U, L);
     b.hest = dalloc<double2>(c, LK * U, L);
     b.v = dalloc<double2>(c, LK * U, L);
     b.u = dalloc<double2>(c, LK * U, L);
@@ -840,6 +876,9 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.Wp3 = s.Wp3;
         mm.wp_elems = s.wp_elems;
         mm.Pb = s.Pb;
+        mm.Wpil = s.Wpil;
+        mm.WdA = s.WdA;
+        mm.pil_c0 = s.pil_c0;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
@@ -866,6 +905,12 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
             // pic_ok schemes (OFDM): the whole perfect-CSI chain is one kernel
             // (k_pic_chain, u in registers across the iterations)
             const bool chain = pfuse && perfect_chain_ok(s.k, c->ch, b);
+            // block-diagonal W + row-local P (OFDM): the MMSE stage of every IC
+            // iteration rides in the contraction's epilogue (k_pilot_pre +
+            // k_wpair3<..., true>); hP alternates between hp and hp2
+            const bool mfuse = pfuse && !tracing && mmse_fused_ok(s.k, mm, b);
+            double2* hp_prev = b.hp;
+            double2* hp_cur = b.hp2;
             for (int it = 0; it <= c->niter; ++it) {
                 if (it == 1 && (two || chain)) {
                     hipStream_t ps = two ? c->stream2 : c->stream;
@@ -886,6 +931,26 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
                         }
                     }
                     if (two) DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
+                }
+                if (it > 0 && mfuse) {
+                    {
+                        Timed t(c, "k_pilot_pre");
+                        launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur);
+                    }
+                    {
+                        // the contraction with the stage in its epilogue (bench's roofline kernel)
+                        Timed t(c, "k_wcontract");
+                        launch_mmse_fused(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), var_of_stage(it, c->niter),
+                                          it, c->niter, it == c->niter, b, hp_prev, hp_cur, c->d_counters, (int)si);
+                    }
+                    std::swap(hp_prev, hp_cur);
+                    if (!two && !chain) {
+                        Timed t(c, "perfect_ic");
+                        PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
+                                             s.k.slI, s.k.slQ};
+                        launch_perfect_ic(c->stream, s.k, c->ch, b, pfuse ? &pd : nullptr);
+                    }
+                    continue;
                 }
                 if (it > 0) {
                     {
@@ -1447,7 +1512,11 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
     API_BEGIN
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
-    if (cmac) *cmac = (double)s.w_struct * ctx->nsnr * ctx->niter;
+    // contraction CMACs; with the fused MMSE stage (OFDM) the same kernel also
+    // forms diag(D_hat) = Wd hP of the next stage (LK x NP CMACs per unit)
+    const char* fe = getenv("DSCE_FUSE_STAGE");
+    const double fused = s.Wpil && !(fe && fe[0] == '0') ? (double)s.LK * s.d.n_pilots : 0.0;
+    if (cmac) *cmac = ((double)s.w_struct + fused) * ctx->nsnr * ctx->niter;
     if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
     API_END
 }

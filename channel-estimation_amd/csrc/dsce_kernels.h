@@ -24,6 +24,7 @@ struct McBuffers {
     double2* yest;    // [LK][U]
     double2* yperf;   // [LK][U]
     double2* hp;      // [NP][U]   LS pilot estimates of the current stage
+    double2* hp2;     // [NP][U]   second buffer (fused MMSE stage: previous / current stage)
     double2* hest;    // [LK][U]   diag(D_hat) of the current stage
     double2* v;       // [LK][U]   P [xP; Q(x_est)]
     double2* u;       // [LK][U]   P [xP; Q(x_perfect)]
@@ -46,6 +47,10 @@ struct MmseK {
     const double* Wp3;    // [var][snr][3 wp_elems] Re / Im / Re+Im planes (3M form), or null
     long long wp_elems;
     PairBand Pb;
+    // fused MMSE stage (block-diagonal W, row-local P): null when not eligible
+    const double2* Wpil;  // [var][snr][NP pilots][24 columns][NP]
+    const double2* WdA;   // [var][snr][blk][2][NP/4][64] diag(W) rows, MFMA A layout
+    const int* pil_c0;    // NP: first column of each pilot row's block
 };
 
 // Monte-Carlo pipeline
@@ -60,6 +65,15 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
 // row-local, so the perfect-CSI branch of IC iterations can ride on perfect_ic
 bool perfect_fusable(const SchemeK& sk);
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
+// Fused MMSE stage of IC iteration `stage` (block-diagonal W, row-local P):
+// k_pilot_pre (pilot rows + LS into hp_new) then the contraction with the
+// stage's detection in its epilogue (no y_est, no separate stage kernel).
+bool mmse_fused_ok(const SchemeK& sk, const MmseK& mm, const McBuffers& b);
+void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
+                      const double2* hp_prev, double2* hp_new);
+void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, int var_cur, int stage,
+                       int n_iter, bool last, McBuffers& b, const double2* hp_prev, double2* hp_new,
+                       unsigned long long* counters, int scheme_index);
 // Perfect-CSI detection fused into the perfect IC pass (select mode, row-local P)
 struct PerfectDetectArgs {
     unsigned long long* counters;
@@ -103,6 +117,9 @@ struct TxDesc {
     double norm, phase0, rx_scale;
 };
 void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q);
+void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const double2* w, long long w_elems,
+                       const double2* wd, int nslices, const int* pil_blk, const int* pilot_pos, int ncol,
+                       double2* wpil, double2* wda);
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
                  double2* wp, long long wp_elems, int nslices, double* w3);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);

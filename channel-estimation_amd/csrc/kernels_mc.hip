@@ -1654,11 +1654,32 @@ __global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __rest
 //   P1 += Wr hr,  P2 += Wi hi,  P3 += (Wr + Wi)(hr + hi);  Re = P1 - P2, Im = P3 - P1 - P2
 // instead of four (-25 % matrix-core work); W arrives as three 64-double planes
 // per (tile, k-step) (k_wpair_pack3), hP as Re / Im / Re+Im registers.
-template <int RBP, int NKS>
+// Fused MMSE stage (FUSE, block-diagonal W, row-local P): after the
+// contraction the tile's rows go straight through the stage of IC iteration
+// `stage` instead of being written as y_est and re-read by k_ls + k_stage_fused:
+// diag(D_hat) = Wd hP_new on the matrix cores (A = diag(W) rows in MFMA layout,
+// B = this stage's LS pilot estimates from k_pilot_pre; its D layout is the
+// epilogue's row layout, rows g + 4 k), one-tap y_est ./ h_hat, slicer, error
+// counts, and the re-precoded decision written over v (safe in place: with a
+// block-diagonal W only this wave reads these rows of v).
+struct FuseArgs {
+    const double2* WdA;            // [var][snr][blk][2][NKS][64]
+    const double2* hp_new;         // this stage's hP [NP][U]
+    const uint16_t* sidx;          // transmitted symbol indices [ND][R]
+    const double2* h;              // perfect diag(D) [LK][R] (MSE only)
+    double2* vout;                 // = v (the re-precoded decisions, in place)
+    unsigned long long* counters;
+    double* mse_err;
+    double* mse_pow;
+    int var, stage, nstage, last, scheme;
+};
+
+template <int RBP, int NKS, bool FUSE>
 __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems,
                                                 int var, int nsnr, int snr0, int R, int U,
-                                                const double2* __restrict__ hp, const double2* __restrict__ v,
-                                                const double2* __restrict__ y, double2* __restrict__ yest) {
+                                                const double2* __restrict__ hp, const double2* v,
+                                                const double2* __restrict__ y, double2* __restrict__ yest,
+                                                SchemeK sk, FuseArgs fa) {
     constexpr int PER = RBP == 24 ? 3 : 2;
     constexpr int CPP = RBP == 24 ? 2 : 1;
     constexpr int NACC = RBP / 4;
@@ -1667,6 +1688,12 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     const int unit = blockIdx.x * 64 + wv * 16 + j;
     const int snr = snr0 + (blockIdx.x * 64) / R;
     const int blk = blockIdx.y;
+    __shared__ double2 fsym[FUSE ? 256 : 1];
+    __shared__ SlicerLds fslt[1];
+    if (FUSE) {
+        stage_tables<256>(fsym, fslt[0], sk, threadIdx.x);
+        __syncthreads();
+    }
     double br[NKS], bi[NKS], bs[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -1772,14 +1799,148 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     }
 #undef WSTEP
     const int row0 = P.row0[blk], nrows = P.nrows[blk];
+    if (!FUSE) {
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) {
+            const int r = g + 4 * k;
+            if (r < nrows) {
+                const size_t i = (size_t)(row0 + r) * U + unit;
+                yest[i] = c_sub(y[i], acc[k]);
+            }
+        }
+        return;
+    }
+    // ---- fused stage epilogue -------------------------------------------
+    double hr[NKS], hi[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        const double2 hv = fa.hp_new[(size_t)(4 * ks + g) * U + unit];
+        hr[ks] = hv.x;
+        hi[ks] = hv.y;
+    }
+    const double2* __restrict__ wa = fa.WdA + (((size_t)fa.var * nsnr + snr) * P.nblk + blk) * 2 * NKS * 64 + lane;
+    d4 er[2], ei[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        er[t] = d4{0.0, 0.0, 0.0, 0.0};
+        ei[t] = er[t];
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const double2 a = wa[(t * NKS + ks) * 64];
+            er[t] = MFMA64(a.x, hr[ks], er[t]);
+            er[t] = MFMA64(-a.y, hi[ks], er[t]);
+            ei[t] = MFMA64(a.x, hi[ks], ei[t]);
+            ei[t] = MFMA64(a.y, hr[ks], ei[t]);
+        }
+    }
+    const int rl = unit % R;
+    const double idd = 1.0 / sk.data_div;
+    int cnt[4] = {0, 0, 0, 0};
+    double me = 0.0, mp = 0.0;
 #pragma unroll
     for (int k = 0; k < NACC; ++k) {
         const int r = g + 4 * k;
-        if (r < nrows) {
-            const size_t i = (size_t)(row0 + r) * U + unit;
-            yest[i] = c_sub(y[i], acc[k]);
+        if (r >= nrows) continue;
+        const int row = row0 + r;
+        const size_t ix = (size_t)row * U + unit;
+        const double2 ye = c_sub(y[ix], acc[k]);
+        const double2 he = make_double2(er[k >> 2][k & 3], ei[k >> 2][k & 3]);
+        if (fa.mse_err) {
+            const double2 hv = fa.h[(size_t)row * R + rl];
+            const double dx = he.x - hv.x, dy = he.y - hv.y;
+            me += dx * dx + dy * dy;
+        }
+        const int d = sk.row_data[row];
+        if (d < 0) continue;
+        const double2 z = c_div1(ye, he);
+        const int de = slice_fast(fslt[0], sk.nI, sk.nQ,
+                                  sk.real_detect ? make_double2(z.x * idd, 0.0) : make_double2(z.x * idd, z.y * idd),
+                                  sk.slI, sk.slQ);
+        const int ne = __popc((unsigned)(de ^ (int)fa.sidx[(size_t)d * R + rl]));
+        cnt[0] += ne;
+        cnt[1] += sk.row_cons[row] ? ne : 0;
+        if (!fa.last) {
+            double2 av = make_double2(0.0, 0.0);
+            if (sk.row_pcol[row] >= 0) c_fma(av, sk.row_pval[row], fsym[de]);
+            fa.vout[ix] = av;
         }
     }
+    flush_counts(cnt, fa.counters, (((size_t)fa.scheme * 4) * nsnr + snr) * fa.nstage + fa.stage,
+                 (size_t)nsnr * fa.nstage, 1);
+    if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage);
+}
+
+// Pre-pass of the fused MMSE stage of IC iteration `stage` (script:482-489):
+// y_est at the NP pilot rows with the previous stage's D_hat (W of var_prev,
+// the contraction's), then the LS estimates hP = y_est(pilots) ./ xP /
+// sqrt(kappa) into hp_new, which the fused contraction's epilogue needs
+// before any row can be detected.  Lane = unit; the pilot rows of W stream
+// with wave-uniform (scalar) loads.  NP x 24 x (NP + 1) CMACs per unit, 5 % of
+// the contraction.
+template <int NP>
+__global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __restrict__ Wpil,
+                                                  const int* __restrict__ pil_c0, int var_prev, int nsnr, int snr0,
+                                                  int R, int U, const double2* __restrict__ hp_prev,
+                                                  const double2* __restrict__ v, const double2* __restrict__ y,
+                                                  const double2* __restrict__ xp, double2* __restrict__ hp_new) {
+    const int unit = blockIdx.x * WAVE + threadIdx.x;
+    const int rl = unit % R;
+    const int snr = snr0 + (blockIdx.x * WAVE) / R;
+    double2 hq[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) hq[p] = hp_prev[(size_t)p * U + unit];
+    const double2* __restrict__ wb = Wpil + ((size_t)var_prev * nsnr + snr) * (size_t)NP * 24 * NP;
+    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    for (int i = 0; i < NP; ++i) {
+        const int r = sk.pilot_pos[i], c0 = pil_c0[i];
+        const double2* __restrict__ wi = wb + (size_t)i * 24 * NP;
+        double2 acc = make_double2(0.0, 0.0);
+        for (int cc = 0; cc < 24; ++cc) {
+            const double2 vc = v[(size_t)(c0 + cc) * U + unit];
+            double2 d = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) c_fma(d, wi[cc * NP + p], hq[p]);
+            c_fma(acc, d, vc);
+        }
+        const double2 ye = c_sub(y[(size_t)r * U + unit], acc);
+        const double2 q = c_div(ye, xp[(size_t)i * R + rl]);
+        hp_new[(size_t)i * U + unit] = make_double2(q.x / sqk, q.y / sqk);
+    }
+}
+
+bool mmse_fused_ok(const SchemeK& sk, const MmseK& mm, const McBuffers& b) {
+    const char* e = getenv("DSCE_FUSE_STAGE");
+    const char* m3e = getenv("DSCE_WPAIR_3M");
+    const char* we = getenv("DSCE_WCONTRACT");
+    return mm.Wpil && mm.WdA && mm.Wp3 && mm.Pb.rbp == 24 && mm.Pb.nks == 4 && sk.NP == 16 && !(e && e[0] == '0') &&
+           !(m3e && m3e[0] == '0') && !(we && we[0] != 'p') && (b.U % 64) == 0 && (b.R % 64) == 0;
+}
+
+void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
+                      const double2* hp_prev, double2* hp_new) {
+    hipLaunchKernelGGL(k_pilot_pre<16>, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev, mm.nsnr,
+                       b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.xp, hp_new);
+}
+
+void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, int var_cur, int stage,
+                       int n_iter, bool last, McBuffers& b, const double2* hp_prev, double2* hp_new,
+                       unsigned long long* counters, int scheme_index) {
+    FuseArgs fa{};
+    fa.WdA = mm.WdA;
+    fa.hp_new = hp_new;
+    fa.sidx = b.sidx;
+    fa.h = b.h;
+    fa.vout = b.v;
+    fa.counters = counters;
+    fa.mse_err = b.mse_err;
+    fa.mse_pow = b.mse_pow;
+    fa.var = var_cur;
+    fa.stage = stage;
+    fa.nstage = n_iter + 1;
+    fa.last = last ? 1 : 0;
+    fa.scheme = scheme_index;
+    hipLaunchKernelGGL((k_wpair3<24, 4, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems,
+                       var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
 }
 
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
@@ -1798,8 +1959,8 @@ void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
         if (mm.Wp3 && m3) {
 #define LAUNCH_W3(RBPV, NKSV)                                                                                    \
     {                                                                                                            \
-        hipLaunchKernelGGL((k_wpair3<RBPV, NKSV>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,           \
-                           mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                                   \
+        hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,    \
+                           mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{});                   \
     }
             if (mm.Pb.rbp == 24) {
                 if (mm.Pb.nks == 2) LAUNCH_W3(24, 2)

@@ -371,6 +371,48 @@ __global__ void k_wpair_pack3(long long wp_elems, const double2* __restrict__ wp
     }
 }
 
+// Operands of the fused MMSE stage (k_pilot_pre + k_wpair3<..., true>), block-
+// diagonal schemes only.  Wpil[slice][pilot i][cc][p] = W[(pilot row, c0_i + cc), p]
+// from the packed band (the pilot rows of W, row-major: the pre-pass streams
+// them with wave-uniform loads); c0_i = first column of the pilot row's block.
+__global__ void k_wpil_pack(Band Wb, int NP, const double2* __restrict__ w, long long w_elems,
+                            const int* __restrict__ pil_blk, const int* __restrict__ pilot_pos, int ncol,
+                            double2* __restrict__ out) {
+    const int i = blockIdx.x, sl = blockIdx.y;
+    const int b = pil_blk[i], r = pilot_pos[i];
+    const int clo = Wb.klo[b] / NP, chi = Wb.khi[b] / NP;
+    const int c0 = Wb.row0[b];
+    for (int e = threadIdx.x; e < ncol * NP; e += blockDim.x) {
+        const int cc = e / NP, p = e % NP, c = c0 + cc;
+        double2 v = make_double2(0.0, 0.0);
+        if (c >= clo && c < chi)
+            v = w[(size_t)sl * w_elems + Wb.off[b] + ((size_t)(c - clo) * NP + p) * Wb.rb + (r - Wb.row0[b])];
+        out[(((size_t)sl * NP + i) * ncol + cc) * NP + p] = v;
+    }
+}
+
+// WdA[slice][blk][t][ks][lane] = Wd[slice][row0_blk + 16 t + (lane & 15)][4 ks + (lane >> 4)]:
+// diag(W) rows as the A operand of v_mfma_f64_16x16x4 (diag(D_hat) = Wd hP on the matrix cores)
+__global__ void k_wda_pack(Band Wb, int LK, int NP, const double2* __restrict__ wd, double2* __restrict__ out) {
+    const int b = blockIdx.x, sl = blockIdx.y, nks = NP / 4;
+    const int row0 = Wb.row0[b], nrows = Wb.nrows[b];
+    for (int e = threadIdx.x; e < 2 * nks * 64; e += blockDim.x) {
+        const int l = e & 63, ks = (e >> 6) % nks, t = (e >> 6) / nks;
+        const int r = 16 * t + (l & 15);
+        const double2 v = r < nrows ? wd[(size_t)sl * LK * NP + (size_t)(row0 + r) * NP + 4 * ks + (l >> 4)]
+                                    : make_double2(0.0, 0.0);
+        out[((size_t)sl * Wb.nblk + b) * 2 * nks * 64 + e] = v;
+    }
+}
+
+void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const double2* w, long long w_elems,
+                       const double2* wd, int nslices, const int* pil_blk, const int* pilot_pos, int ncol,
+                       double2* wpil, double2* wda) {
+    hipLaunchKernelGGL(k_wpil_pack, dim3(NP, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, pil_blk, pilot_pos, ncol,
+                       wpil);
+    hipLaunchKernelGGL(k_wda_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, LK, NP, wd, wda);
+}
+
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
                  double2* wp, long long wp_elems, int nslices, double* w3) {
     hipLaunchKernelGGL(k_wpair_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, P, wp, wp_elems);

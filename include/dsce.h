@@ -233,8 +233,9 @@ int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum);
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
 /* Algorithmic work of one realisation of a scheme (support-aware): complex
- * multiply-accumulates of the MMSE contraction and the number of W bytes
- * streamed per contraction launch. */
+ * multiply-accumulates of the MMSE contraction kernel (including, when the MMSE
+ * stage is fused into it, the diag(D_hat) = Wd hP products) and the number of W
+ * bytes streamed per contraction launch. */
 int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per_rep, double* w_bytes_per_snr);
 
 #ifdef __cplusplus
