@@ -1811,26 +1811,32 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
         return;
     }
     // ---- fused stage epilogue -------------------------------------------
-    double hr[NKS], hi[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-        const double2 hv = fa.hp_new[(size_t)(4 * ks + g) * U + unit];
-        hr[ks] = hv.x;
-        hi[ks] = hv.y;
-    }
-    const double2* __restrict__ wa = fa.WdA + (((size_t)fa.var * nsnr + snr) * P.nblk + blk) * 2 * NKS * 64 + lane;
+    // diag(D_hat) of this stage = Wd hP_new on the matrix cores: B = hP_new in
+    // B layout (pilot 4 ks + g, unit j), D rows g + 4 reg + 16 t = this lane's
+    // rows g + 4 k of the block.  (Forming it before the tile loop and parking
+    // it in LDS measured no faster.)
     d4 er[2], ei[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        er[t] = d4{0.0, 0.0, 0.0, 0.0};
-        ei[t] = er[t];
+    {
+        double hr[NKS], hi[NKS];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-            const double2 a = wa[(t * NKS + ks) * 64];
-            er[t] = MFMA64(a.x, hr[ks], er[t]);
-            er[t] = MFMA64(-a.y, hi[ks], er[t]);
-            ei[t] = MFMA64(a.x, hi[ks], ei[t]);
-            ei[t] = MFMA64(a.y, hr[ks], ei[t]);
+            const double2 hv = fa.hp_new[(size_t)(4 * ks + g) * U + unit];
+            hr[ks] = hv.x;
+            hi[ks] = hv.y;
+        }
+        const double2* __restrict__ wa = fa.WdA + (((size_t)fa.var * nsnr + snr) * P.nblk + blk) * 2 * NKS * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            er[t] = d4{0.0, 0.0, 0.0, 0.0};
+            ei[t] = er[t];
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const double2 a = wa[(t * NKS + ks) * 64];
+                er[t] = MFMA64(a.x, hr[ks], er[t]);
+                er[t] = MFMA64(-a.y, hi[ks], er[t]);
+                ei[t] = MFMA64(a.x, hi[ks], ei[t]);
+                ei[t] = MFMA64(a.y, hr[ks], ei[t]);
+            }
         }
     }
     const int rl = unit % R;
@@ -1894,13 +1900,22 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
     for (int i = 0; i < NP; ++i) {
         const int r = sk.pilot_pos[i], c0 = pil_c0[i];
         const double2* __restrict__ wi = wb + (size_t)i * 24 * NP;
+        // D_hat[r, c] = sum_p W hP_p in 4 partial sums (independent FMA chains),
+        // two columns per step
         double2 acc = make_double2(0.0, 0.0);
-        for (int cc = 0; cc < 24; ++cc) {
-            const double2 vc = v[(size_t)(c0 + cc) * U + unit];
-            double2 d = make_double2(0.0, 0.0);
+        for (int cc = 0; cc < 24; cc += 2) {
+            const double2 va = v[(size_t)(c0 + cc) * U + unit];
+            const double2 vb = v[(size_t)(c0 + cc + 1) * U + unit];
+            double2 d[8];
 #pragma unroll
-            for (int p = 0; p < NP; ++p) c_fma(d, wi[cc * NP + p], hq[p]);
-            c_fma(acc, d, vc);
+            for (int k = 0; k < 8; ++k) d[k] = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                c_fma(d[p & 3], wi[cc * NP + p], hq[p]);
+                c_fma(d[4 + (p & 3)], wi[(cc + 1) * NP + p], hq[p]);
+            }
+            c_fma(acc, c_add(c_add(d[0], d[1]), c_add(d[2], d[3])), va);
+            c_fma(acc, c_add(c_add(d[4], d[5]), c_add(d[6], d[7])), vb);
         }
         const double2 ye = c_sub(y[(size_t)r * U + unit], acc);
         const double2 q = c_div(ye, xp[(size_t)i * R + rl]);
