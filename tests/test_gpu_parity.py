@@ -236,12 +236,19 @@ def test_stage_variants_agree(monkeypatch, name):
     # perfect-CSI detection fused into perfect_ic (OFDM) on/off, XCD-aware
     # work order on/off, SNR-chunked receiver, two streams instead of one, the
     # one-pass perfect-CSI IC (k_pic) instead of the two passes, 4-MFMA instead of
-    # 3M complex products, 32-row contraction tiles instead of pairs
-    for var, val in (("DSCE_PFUSE", "0"), ("DSCE_XCD", "0"), ("DSCE_SNR_CHUNK", "2"), ("DSCE_STREAMS", "2"),
-                     ("DSCE_PIC", "1"), ("DSCE_WPAIR_3M", "0"), ("DSCE_WCONTRACT", "mfma")):
-        monkeypatch.setenv(var, val)
-        np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=var)
-        monkeypatch.delenv(var)
+    # 3M complex products, 32-row contraction tiles instead of pairs, the MMSE
+    # stage as its own kernels instead of fused into the contraction, the
+    # perfect-CSI chain as per-iteration passes / VALU chain instead of k_pic_mfma
+    variants = ({"DSCE_PFUSE": "0"}, {"DSCE_XCD": "0"}, {"DSCE_SNR_CHUNK": "2"}, {"DSCE_STREAMS": "2"},
+                {"DSCE_PIC": "1", "DSCE_PIC_CHAIN": "0"}, {"DSCE_WPAIR_3M": "0"}, {"DSCE_WCONTRACT": "mfma"},
+                {"DSCE_FUSE_STAGE": "0"}, {"DSCE_PIC_CHAIN": "0"}, {"DSCE_PIC_CHAIN": "1"},
+                {"DSCE_STREAMS": "2", "DSCE_FUSE_STAGE": "0"})
+    for env in variants:
+        for var, val in env.items():
+            monkeypatch.setenv(var, val)
+        np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(env))
+        for var in env:
+            monkeypatch.delenv(var)
     eng.close()
 
 
