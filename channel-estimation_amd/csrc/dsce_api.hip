@@ -318,6 +318,16 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
                 }
             }
     }
+    // Q^H row blocks with disjoint sample ranges (OFDM): the noise can be drawn
+    // inside the Q^H pass (LoadNoisy) without drawing a sample twice
+    {
+        std::vector<int> seen(N, 0);
+        bool disj = true;
+        for (size_t b = 0; b < s.qband.row0.size() && disj; ++b)
+            for (int n = s.qband.klo[b]; n < s.qband.khi[b]; ++n)
+                if (seen[n]++) disj = false;
+        s.k.qh_disjoint = disj ? 1 : 0;
+    }
     // fused perfect-CSI IC tables (see SchemeK::pic_ok)
     {
         int md = 0;

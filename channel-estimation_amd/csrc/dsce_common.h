@@ -112,6 +112,7 @@ struct PairBand {
 struct SchemeK {
     int N, LK, Nsym, NP, ND, M, mbits, despread, real_detect;
     int noise_slot;               // AWGN sub-stream group (include/dsce.h NOISE)
+    int qh_disjoint;              // every sample lies in at most one Q^H row block's k-range
     double inv_sqrt_kappa, data_div;
     const int* pilot_pos;
     const int* data_pos;

@@ -790,8 +790,35 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int
     }
 }
 
+// r = r0 + noise generated on the fly as the column operand of the Q^H band
+// (the noise of k_noise, bit for bit, but only for the samples Q^H reads — the
+// OFDM cyclic prefixes and zero guards are never drawn — and r never touches
+// memory).  Used when every sample feeds at most one Q^H row block.
+struct LoadNoisy {
+    const double2* __restrict__ r0;    // [N][R]
+    const double* __restrict__ pn;
+    uint64_t seed, rep0;
+    int R, snr0, slot;
+    typedef double2 Regs;
+    __device__ __forceinline__ Regs load(int n, int lane) const {
+        const int snr = snr0 + lane / R, rl = lane % R;
+        const double sc = sqrt(pn[snr] / 2.0);
+        const double2 z = normal_pair(stream_block(seed, rep0 + (uint64_t)rl, STREAM_NOISE,
+                                                   (uint32_t)(snr + 256 * slot), (uint32_t)n));
+        const double2 r = r0[(size_t)n * R + rl];
+        return make_double2(r.x + sc * z.x, r.y + sc * z.y);
+    }
+    __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
+};
+
 void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
                      uint64_t rep0, McBuffers& b) {
+    const char* e = getenv("DSCE_NOISE_FUSE");
+    if (sk.qh_disjoint && !(e && e[0] == '0')) {
+        launch_band(s, sk.QH, b.U, nullptr, LoadNoisy{b.r0, pn, seed, rep0, b.R, b.snr0, sk.noise_slot},
+                    StoreSoA{b.y, b.U});
+        return;
+    }
     hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, sk.noise_slot, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)

@@ -242,7 +242,7 @@ def test_stage_variants_agree(monkeypatch, name):
     variants = ({"DSCE_PFUSE": "0"}, {"DSCE_XCD": "0"}, {"DSCE_SNR_CHUNK": "2"}, {"DSCE_STREAMS": "2"},
                 {"DSCE_PIC": "1", "DSCE_PIC_CHAIN": "0"}, {"DSCE_WPAIR_3M": "0"}, {"DSCE_WCONTRACT": "mfma"},
                 {"DSCE_FUSE_STAGE": "0"}, {"DSCE_PIC_CHAIN": "0"}, {"DSCE_PIC_CHAIN": "1"},
-                {"DSCE_STREAMS": "2", "DSCE_FUSE_STAGE": "0"})
+                {"DSCE_STREAMS": "2", "DSCE_FUSE_STAGE": "0"}, {"DSCE_NOISE_FUSE": "0"})
     for env in variants:
         for var, val in env.items():
             monkeypatch.setenv(var, val)
