@@ -1,7 +1,12 @@
 """Command-line Monte-Carlo run: the reference script's loop and plots
-(DoublySelectiveChannelEstimation.m:350-631) on one MI355X.
+(DoublySelectiveChannelEstimation.m:350-631) on one MI355X, or sharded over the
+GPUs of a node (one process per GPU, realisations split contiguously, one
+all-reduce of the counters and MSE sums — SURVEY §8e; bit-identical counts for
+any number of ranks):
 
     python -m dsce.simulate --config default --reps 4096 --out run.json --figures figs/
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m dsce.simulate --config c5 --reps 10048 --out c5.json     # BASELINE config 5
 
 Progress lines mirror the script's `disp` (script:567); results go through
 dsce.results (JSON [+ NPZ], Figures 2-5)."""
@@ -36,30 +41,64 @@ def main(argv=None):
     if a.config == "doubly_flat":
         return _doubly_flat(a)
 
+    from dsce.parallel import allreduce_counts, shard_range
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    device = 0
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        # DSCE_DIST_BACKEND=gloo rehearses on a one-GPU box (ranks share the device)
+        device = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        dist.init_process_group(os.environ.get("DSCE_DIST_BACKEND", "nccl"))
     names = tuple(a.schemes.split(","))
     S = build_setup(a.config, schemes=names)
     reps = a.reps if a.reps is not None else S.n_repetitions
-    reps = max(64, (reps + 63) // 64 * 64)
+    reps = max(64 * world, (reps + 64 * world - 1) // (64 * world) * (64 * world))
+    first, mine = shard_range(0, reps, world, rank)
     t0 = time.perf_counter()
-    eng = build_engine(S, batch=min(a.batch, reps))
+    eng = build_engine(S, device=device, batch=min(a.batch, mine))
     setup_s = time.perf_counter() - t0
     counts = np.zeros(eng.counter_shape(), dtype=np.int64)
     if a.mse:
         eng.enable_mse()
     done, t0 = 0, time.perf_counter()
-    step = min(a.batch, reps)
-    while done < reps:
-        n = min(step, reps - done)
-        eng.run(a.seed, done, n, counts)
+    step = min(a.batch, mine)
+    while done < mine:
+        n = min(step, mine - done)
+        eng.run(a.seed, first + done, n, counts)
         done += n
         el = time.perf_counter() - t0
-        print("%d%% Completed! Time Left: %.1f s" % (100 * done // reps, el / done * (reps - done)), flush=True)
+        if rank == 0:
+            print("%d%% Completed! Time Left: %.1f s" % (100 * done // mine, el / done * (mine - done)), flush=True)
     bits = np.array([eng.bits_per_rep(i) for i in range(len(names))])
-    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0}
+    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world}
     if a.mse:
         err, pw = eng.mse()
+    if world > 1:
+        dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else None
+        counts = allreduce_counts(counts, dev)                    # the one exchange
+        if a.mse:
+            err = allreduce_counts(err, dev)
+            pw = allreduce_counts(pw, dev)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([extra["seconds"]], dtype=torch.float64)
+        if dev:
+            t = t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra["seconds"] = float(t.item())
+    if a.mse:
         extra["nmse"] = {s: (err[i] / pw[i][:, None]).tolist() for i, s in enumerate(names)}
+    extra["realisations_per_s"] = reps / extra["seconds"]
     res = results.make(S, names, counts, bits, reps, a.seed, extra=extra)
+    if rank != 0:
+        eng.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
     if a.out:
         results.save(a.out, res, npz=a.npz)
     if a.figures:
@@ -72,6 +111,8 @@ def main(argv=None):
                    "ber_onetap_mmse": float(res["ber"][s]["mmse"]["all"][k][0])} for s in names}
     print(json.dumps(summary))
     eng.close()
+    if world > 1:
+        dist.destroy_process_group()
     return 0
 
 
