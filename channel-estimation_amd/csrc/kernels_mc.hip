@@ -947,7 +947,6 @@ template <int NT, int DMAX>
 __global__ void __launch_bounds__(256) k_pic_chain(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
                                                    TapDelays dl, StorePerfectDetect o, int niter) {
     extern __shared__ double2 pic_lds[];
-    __shared__ int pc_cnt[8];
     int ug, blk;
     band_block(ord, sk.QH.nblk, ug, blk);
     const int tid = threadIdx.x, half = tid & 1;
@@ -1084,7 +1083,6 @@ __global__ void __launch_bounds__(256) k_pic_chain(SchemeK sk, BandOrder ord, co
             if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
         }
     }
-    (void)pc_cnt;
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));
