@@ -94,7 +94,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--reps-per-step", type=int, default=65536)
-    ap.add_argument("--batch", type=int, default=32768, help="realisations per device batch")
+    ap.add_argument("--batch", type=int, default=65536, help="realisations per device batch")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-leg", action="store_true", help=argparse.SUPPRESS)
