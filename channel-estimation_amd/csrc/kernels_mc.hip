@@ -1107,9 +1107,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // counters is written.  Block = 4 waves = 64 units of one Q^H block (its A
 // tables staged in LDS once); grid: Q^H blocks x units/64, SNR-fastest
 // XCD-aware order.
-template <int KSQ>
+template <int KSQ, int NT>
 __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
-                                                  int d0, int d1, int ntap, StorePerfectDetect o, int niter) {
+                                                  int d0, int d1, StorePerfectDetect o, int niter) {
     extern __shared__ double2 pm_lds[];
     int ug, blk;
     band_block(ord, sk.QH.nblk, ug, blk);
@@ -1123,6 +1123,10 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
     double2* sa = pm_lds;                                       // A tables
     double2* sym = pm_lds + NA;
     SlicerLds* slt = (SlicerLds*)(sym + 256);
+    // the block's 32 (padded) rows: re-precoding value, data index (-1: pilot or
+    // padding), no-edge flag — read by the epilogue every iteration
+    __shared__ double2 rpv[32];
+    __shared__ int rdc[32];
     {
         const double2* __restrict__ src = sk.pm_a + (size_t)sk.pm_stride * blk;
         for (int i = tid; i < NA; i += 256) sa[i] = src[i];
@@ -1131,6 +1135,12 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
         if (tid < 16) {
             slt->lvI[tid] = tid < o.nI ? o.lvI[tid] : 0.0;
             slt->lvQ[tid] = tid < o.nQ ? o.lvQ[tid] : 0.0;
+        }
+        if (tid < 32) {
+            const int row = row0 + (tid < nrows ? tid : 0);
+            rpv[tid] = o.row_pval[row];
+            // data index << 1 | no-edge flag, or -1
+            rdc[tid] = tid < nrows && o.row_data[row] >= 0 ? (o.row_data[row] << 1) | (o.row_cons[row] ? 1 : 0) : -1;
         }
     }
     const double2* ga = sa;
@@ -1145,8 +1155,19 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
             ur[t][r] = row < nrows ? o.u[(size_t)(row0 + row) * U + unit] : make_double2(0.0, 0.0);
         }
     __syncthreads();
+    // transmitted symbol indices of the lane's 8 rows, fixed for the whole chain:
+    // loaded once, 8 bits each, packed 4 per register (M <= 256)
+    unsigned txp[2] = {0u, 0u};
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int dc = rdc[16 * t + kq + 4 * r];
+            const unsigned tx = dc >= 0 ? (unsigned)o.sidx[(size_t)(dc >> 1) * R + rl] : 0u;
+            txp[t] |= (tx & 0xffu) << (8 * r);
+        }
     // tap delay offsets into T: X[j] uses T[j + maxd - d_q] (maxd <= 1)
-    const int maxd = max(d0, ntap > 1 ? d1 : 0);
+    const int maxd = max(d0, NT > 1 ? d1 : 0);
     const int c0 = maxd - d0, c1 = maxd - d1;
     const int src_lane = (l + 16) & 63;
     const int snr = o.snr0 + (ug * WAVE) / R;
@@ -1156,6 +1177,16 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
         // across it and triple the register footprint)
         int oz = 0;
         asm volatile("" : "+v"(oz));
+        // taps of GEMM2's first k-step, requested now so GEMM1 covers their latency;
+        // every later k-step's taps are requested one step ahead
+        auto ld_taps = [&](int k, double2 (&hv)[NT]) {
+            const int n = klo + 4 * k + kq + oz;
+            const int nc = n < N ? n : N - 1;
+#pragma unroll
+            for (int q = 0; q < NT; ++q) hv[q] = ir[((size_t)q * N + nc) * R + rl];
+        };
+        double2 hnext[NT];
+        ld_taps(0, hnext);
         // GEMM1: T = G U (2 row tiles x 6 k-steps)
         d4 tre[2], tim[2];
 #pragma unroll
@@ -1192,15 +1223,13 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
             const double2 tn = make_double2(tre[kn >> 2][kn & 3], tim[kn >> 2][kn & 3]);
             const double2 sv = l >= 16 ? tc : tn;
             const double2 t1 = make_double2(__shfl(sv.x, src_lane), __shfl(sv.y, src_lane));
-            const int n = klo + 4 * k + kq + oz;
-            const int nc = n < N ? n : N - 1;
-            const double2 h0 = ir[(size_t)nc * R + rl];
+            double2 hcur[NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) hcur[q] = hnext[q];
+            if (k + 1 < KSQ) ld_taps(k + 1, hnext);
             double2 x = make_double2(0.0, 0.0);
-            c_fma(x, h0, c0 ? t1 : tc);
-            if (ntap > 1) {
-                const double2 h1 = ir[((size_t)N + nc) * R + rl];
-                c_fma(x, h1, c1 ? t1 : tc);
-            }
+            c_fma(x, hcur[0], c0 ? t1 : tc);
+            if (NT > 1) c_fma(x, hcur[NT > 1 ? 1 : 0], c1 ? t1 : tc);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const double2 a = qa[(t * KSQ + k) * 64 + l];
@@ -1215,22 +1244,19 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
         const bool last = it == niter;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-            double2 yv[4], hv[4], pv[4];
-            int tx[4], dd[4], cn[4];
+            double2 yv[4], hv[4];
+            int dc[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int rr = 16 * t + kq + 4 * r;
                 const int row = row0 + (rr < nrows ? rr : 0) + oz;
-                dd[r] = rr < nrows ? o.row_data[row] : -1;
-                cn[r] = o.row_cons[row];
-                pv[r] = o.row_pval[row];
+                dc[r] = rdc[rr];
                 yv[r] = o.y[(size_t)row * U + unit];
                 hv[r] = o.h[(size_t)row * R + rl];
-                tx[r] = o.sidx[(size_t)(dd[r] > 0 ? dd[r] : 0) * R + rl];
             }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (dd[r] < 0) continue;
+                if (dc[r] < 0) continue;
                 double2 yp = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
                 yp = c_add(yp, c_mul(hv[r], ur[t][r]));
                 const double2 z = c_div1(yp, hv[r]);
@@ -1238,12 +1264,12 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
                                           o.real_detect ? make_double2(z.x * o.idd, 0.0)
                                                         : make_double2(z.x * o.idd, z.y * o.idd),
                                           o.sI, o.sQ);
-                const int ne = __popc((unsigned)(dp ^ tx[r]));
+                const int ne = __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu)));
                 e0 += ne;
-                e1 += cn[r] ? ne : 0;
+                e1 += (dc[r] & 1) ? ne : 0;
                 if (!last) {
                     double2 av = make_double2(0.0, 0.0);
-                    c_fma(av, pv[r], sym[dp]);
+                    c_fma(av, rpv[16 * t + kq + 4 * r], sym[dp]);
                     ur[t][r] = av;
                 }
             }
@@ -1349,10 +1375,16 @@ void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, 
         const size_t lds = ((size_t)(2 * 6 + 2 * sk.pm_ksq) * 64 + 256) * sizeof(double2) + sizeof(SlicerLds);
         const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
         const int d1 = ch.ntap > 1 ? ch.tap_delay[1] : 0;
-        if (sk.pm_ksq == 6)
-            hipLaunchKernelGGL(k_pic_mfma<6>, grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, ch.ntap, o, niter);
-        else
-            hipLaunchKernelGGL(k_pic_mfma<7>, grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, ch.ntap, o, niter);
+#define LAUNCH_PM(KS, NTV) \
+    hipLaunchKernelGGL((k_pic_mfma<KS, NTV>), grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, o, niter)
+        if (sk.pm_ksq == 6) {
+            if (ch.ntap == 2) LAUNCH_PM(6, 2);
+            else LAUNCH_PM(6, 1);
+        } else {
+            if (ch.ntap == 2) LAUNCH_PM(7, 2);
+            else LAUNCH_PM(7, 1);
+        }
+#undef LAUNCH_PM
         return;
     }
     const BandOrder ord{b.U / PCH_UNITS, b.U / b.R, b.R / PCH_UNITS, (!xe || xe[0] != '0') ? 1 : 0};
@@ -1715,9 +1747,29 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     const int blk = blockIdx.y;
     __shared__ double2 fsym[FUSE ? 256 : 1];
     __shared__ SlicerLds fslt[1];
+    // FUSE: the block's rows (re-precoding value or 0, data index << 1 | no-edge
+    // flag or -1) and, per lane, the transmitted symbol indices of its rows
+    // (8 bits each, packed) — the epilogue then has no dependent global loads
+    __shared__ double2 frpv[FUSE ? RBP : 1];
+    __shared__ int frdc[FUSE ? RBP : 1];
+    unsigned ftx[FUSE ? 2 : 1] = {0u};
     if (FUSE) {
         stage_tables<256>(fsym, fslt[0], sk, threadIdx.x);
+        const int r0b = P.row0[blk], nrb = P.nrows[blk];
+        if (threadIdx.x < RBP) {
+            const int rr = threadIdx.x, row = r0b + (rr < nrb ? rr : 0);
+            const int d = rr < nrb ? sk.row_data[row] : -1;
+            frpv[rr] = sk.row_pcol[row] >= 0 ? sk.row_pval[row] : make_double2(0.0, 0.0);
+            frdc[rr] = d >= 0 ? (d << 1) | (sk.row_cons[row] ? 1 : 0) : -1;
+        }
         __syncthreads();
+        const int rl0 = (blockIdx.x * 64 + (int)(threadIdx.x >> 6) * 16 + (int)(threadIdx.x & 15)) % R;
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) {
+            const int dc = frdc[(threadIdx.x & 63) / 16 + 4 * k < RBP ? (threadIdx.x & 63) / 16 + 4 * k : 0];
+            const unsigned tx = dc >= 0 ? (unsigned)fa.sidx[(size_t)(dc >> 1) * R + rl0] : 0u;
+            ftx[k >> 2] |= (tx & 0xffu) << (8 * (k & 3));
+        }
     }
     double br[NKS], bi[NKS], bs[NKS];
 #pragma unroll
@@ -1881,18 +1933,18 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
             const double dx = he.x - hv.x, dy = he.y - hv.y;
             me += dx * dx + dy * dy;
         }
-        const int d = sk.row_data[row];
-        if (d < 0) continue;
+        const int dc = frdc[r];
+        if (dc < 0) continue;
         const double2 z = c_div1(ye, he);
         const int de = slice_fast(fslt[0], sk.nI, sk.nQ,
                                   sk.real_detect ? make_double2(z.x * idd, 0.0) : make_double2(z.x * idd, z.y * idd),
                                   sk.slI, sk.slQ);
-        const int ne = __popc((unsigned)(de ^ (int)fa.sidx[(size_t)d * R + rl]));
+        const int ne = __popc((unsigned)(de ^ (int)((ftx[k >> 2] >> (8 * (k & 3))) & 0xffu)));
         cnt[0] += ne;
-        cnt[1] += sk.row_cons[row] ? ne : 0;
+        cnt[1] += (dc & 1) ? ne : 0;
         if (!fa.last) {
             double2 av = make_double2(0.0, 0.0);
-            if (sk.row_pcol[row] >= 0) c_fma(av, sk.row_pval[row], fsym[de]);
+            c_fma(av, frpv[r], fsym[de]);
             fa.vout[ix] = av;
         }
     }
