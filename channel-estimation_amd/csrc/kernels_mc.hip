@@ -1108,7 +1108,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // tables staged in LDS once); grid: Q^H blocks x units/64, SNR-fastest
 // XCD-aware order.
 template <int KSQ, int NT>
-__global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
                                                   int d0, int d1, StorePerfectDetect o, int niter) {
     extern __shared__ double2 pm_lds[];
     int ug, blk;
@@ -1146,26 +1146,35 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
     const double2* ga = sa;
     const double2* qa = sa + 2 * 6 * 64;
     // U in D layout: ur[t][r] = u[row0 + 16 t + kq + 4 r][unit]
+    // (loads unconditional, clamped row, then masked: a conditional load would be
+    // a branch with its own wait, eight serial round trips)
     double2 ur[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = 16 * t + kq + 4 * r;
-            ur[t][r] = row < nrows ? o.u[(size_t)(row0 + row) * U + unit] : make_double2(0.0, 0.0);
+            ur[t][r] = o.u[(size_t)(row0 + (row < nrows ? row : 0)) * U + unit];
         }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (16 * t + kq + 4 * r >= nrows) ur[t][r] = make_double2(0.0, 0.0);
     __syncthreads();
     // transmitted symbol indices of the lane's 8 rows, fixed for the whole chain:
     // loaded once, 8 bits each, packed 4 per register (M <= 256)
     unsigned txp[2] = {0u, 0u};
+    {
+        unsigned short tv[8];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int dc = rdc[16 * t + kq + 4 * r];
-            const unsigned tx = dc >= 0 ? (unsigned)o.sidx[(size_t)(dc >> 1) * R + rl] : 0u;
-            txp[t] |= (tx & 0xffu) << (8 * r);
+        for (int i = 0; i < 8; ++i) {
+            const int dc = rdc[16 * (i >> 2) + kq + 4 * (i & 3)];
+            tv[i] = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
         }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) txp[i >> 2] |= ((unsigned)tv[i] & 0xffu) << (8 * (i & 3));
+    }
     // tap delay offsets into T: X[j] uses T[j + maxd - d_q] (maxd <= 1)
     const int maxd = max(d0, NT > 1 ? d1 : 0);
     const int c0 = maxd - d0, c1 = maxd - d1;
@@ -1240,10 +1249,12 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
             }
         }
         // epilogue on the D layout of acc: 8 rows per lane, one tile at a time
+        // (a lambda per tile with a compile-time tile index: as a loop the
+        // compiler declined to unroll it and indexed ur through scratch)
         int e0 = 0, e1 = 0;
         const bool last = it == niter;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        auto epi_tile = [&](auto tcst) {
+            constexpr int t = decltype(tcst)::value;
             double2 yv[4], hv[4];
             int dc[4];
 #pragma unroll
@@ -1254,9 +1265,11 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
                 yv[r] = o.y[(size_t)row * U + unit];
                 hv[r] = o.h[(size_t)row * R + rl];
             }
+            // every row is computed and the pilot / padding rows masked out
+            // afterwards: with a per-row branch the compiler sinks each row's y
+            // and h loads into it, one serial round trip per load
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                if (dc[r] < 0) continue;
                 double2 yp = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
                 yp = c_add(yp, c_mul(hv[r], ur[t][r]));
                 const double2 z = c_div1(yp, hv[r]);
@@ -1264,16 +1277,22 @@ __global__ void __launch_bounds__(256) k_pic_mfma(SchemeK sk, BandOrder ord, con
                                           o.real_detect ? make_double2(z.x * o.idd, 0.0)
                                                         : make_double2(z.x * o.idd, z.y * o.idd),
                                           o.sI, o.sQ);
-                const int ne = __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu)));
+                const bool data = dc[r] >= 0;
+                const int ne = data ? __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu))) : 0;
                 e0 += ne;
                 e1 += (dc[r] & 1) ? ne : 0;
                 if (!last) {
                     double2 av = make_double2(0.0, 0.0);
                     c_fma(av, rpv[16 * t + kq + 4 * r], sym[dp]);
-                    ur[t][r] = av;
+                    // component-wise select (a struct-valued ?: became an
+                    // address select through scratch)
+                    ur[t][r].x = data ? av.x : ur[t][r].x;
+                    ur[t][r].y = data ? av.y : ur[t][r].y;
                 }
             }
-        }
+        };
+        epi_tile(std::integral_constant<int, 0>{});
+        epi_tile(std::integral_constant<int, 1>{});
         const int s_0 = wave_sum(e0), s_1 = wave_sum(e1);
         if (l < 2) {
             const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (l ? (size_t)o.cstride_edge : 0);
@@ -1764,12 +1783,14 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
         }
         __syncthreads();
         const int rl0 = (blockIdx.x * 64 + (int)(threadIdx.x >> 6) * 16 + (int)(threadIdx.x & 15)) % R;
+        unsigned short tv[NACC];
 #pragma unroll
         for (int k = 0; k < NACC; ++k) {
             const int dc = frdc[(threadIdx.x & 63) / 16 + 4 * k < RBP ? (threadIdx.x & 63) / 16 + 4 * k : 0];
-            const unsigned tx = dc >= 0 ? (unsigned)fa.sidx[(size_t)(dc >> 1) * R + rl0] : 0u;
-            ftx[k >> 2] |= (tx & 0xffu) << (8 * (k & 3));
+            tv[k] = fa.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl0];
         }
+#pragma unroll
+        for (int k = 0; k < NACC; ++k) ftx[k >> 2] |= ((unsigned)tv[k] & 0xffu) << (8 * (k & 3));
     }
     double br[NKS], bi[NKS], bs[NKS];
 #pragma unroll
@@ -1920,31 +1941,39 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     const double idd = 1.0 / sk.data_div;
     int cnt[4] = {0, 0, 0, 0};
     double me = 0.0, mp = 0.0;
+    // all rows' y requested first and every row computed, padding / pilot rows
+    // masked afterwards (a per-row branch lets the compiler sink each y load
+    // into it: one serial round trip per row)
+    double2 yv[NACC];
 #pragma unroll
     for (int k = 0; k < NACC; ++k) {
         const int r = g + 4 * k;
-        if (r >= nrows) continue;
-        const int row = row0 + r;
+        yv[k] = y[(size_t)(row0 + (r < nrows ? r : 0)) * U + unit];
+    }
+#pragma unroll
+    for (int k = 0; k < NACC; ++k) {
+        const int r = g + 4 * k;
+        const bool valid = r < nrows;
+        const int row = row0 + (valid ? r : 0);
         const size_t ix = (size_t)row * U + unit;
-        const double2 ye = c_sub(y[ix], acc[k]);
+        const double2 ye = c_sub(yv[k], acc[k]);
         const double2 he = make_double2(er[k >> 2][k & 3], ei[k >> 2][k & 3]);
-        if (fa.mse_err) {
+        if (fa.mse_err && valid) {
             const double2 hv = fa.h[(size_t)row * R + rl];
             const double dx = he.x - hv.x, dy = he.y - hv.y;
             me += dx * dx + dy * dy;
         }
-        const int dc = frdc[r];
-        if (dc < 0) continue;
+        const int dc = valid ? frdc[r] : -1;
         const double2 z = c_div1(ye, he);
         const int de = slice_fast(fslt[0], sk.nI, sk.nQ,
                                   sk.real_detect ? make_double2(z.x * idd, 0.0) : make_double2(z.x * idd, z.y * idd),
                                   sk.slI, sk.slQ);
-        const int ne = __popc((unsigned)(de ^ (int)((ftx[k >> 2] >> (8 * (k & 3))) & 0xffu)));
+        const int ne = dc >= 0 ? __popc((unsigned)(de ^ (int)((ftx[k >> 2] >> (8 * (k & 3))) & 0xffu))) : 0;
         cnt[0] += ne;
         cnt[1] += (dc & 1) ? ne : 0;
-        if (!fa.last) {
+        if (!fa.last && dc >= 0) {
             double2 av = make_double2(0.0, 0.0);
-            c_fma(av, frpv[r], fsym[de]);
+            c_fma(av, frpv[valid ? r : 0], fsym[de]);
             fa.vout[ix] = av;
         }
     }
