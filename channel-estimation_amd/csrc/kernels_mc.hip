@@ -77,12 +77,20 @@ __device__ __forceinline__ void stage_tables(double2* sym, SlicerLds& t, const S
     int gv[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
+        // Clamped, unconditional loads, masked afterwards: a guarded load becomes a
+        // branch with its own vmcnt(0) wait, and the table loads then serialise.
         const int i = tid + k * NTH;
-        sv[k] = i < sk.M ? sk.symbols[i] : make_double2(0.0, 0.0);
-        gv[k] = i < sk.nI * sk.nQ ? sk.grid_sym[i] : 0;
+        const double2 a = sk.symbols[min(i, sk.M - 1)];
+        const int g = sk.grid_sym[min(i, sk.nI * sk.nQ - 1)];
+        sv[k].x = i < sk.M ? a.x : 0.0;
+        sv[k].y = i < sk.M ? a.y : 0.0;
+        gv[k] = i < sk.nI * sk.nQ ? g : 0;
     }
-    const double li = tid < sk.nI && tid < 16 ? sk.lvI[tid] : 0.0;
-    const double lq = tid < sk.nQ && tid < 16 ? sk.lvQ[tid] : 0.0;
+    const int lt = min(tid, 15);
+    const double lia = sk.lvI[min(lt, sk.nI - 1)];
+    const double lqa = sk.lvQ[min(lt, sk.nQ - 1)];
+    const double li = tid < sk.nI ? lia : 0.0;
+    const double lq = tid < sk.nQ ? lqa : 0.0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         sym[tid + k * NTH] = sv[k];
@@ -94,26 +102,30 @@ __device__ __forceinline__ void stage_tables(double2* sym, SlicerLds& t, const S
     }
 }
 
+// Branch-free (selects only): with branches each row's slicer became a chain of
+// exec-mask blocks, every one ending in its own LDS wait, and the rows of an
+// epilogue could not be interleaved.
 __device__ __forceinline__ int nearest_level_fast(const double* lv, int n, double x, double istep, int& alt) {
-    alt = -1;
-    if (n == 1) return 0;
+    // n == 1 (the Q axis of a real slicer) folds in: i = i1 = 0, no alternative
     int i = (int)floor((x - lv[0]) * istep);
-    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
-    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i + 1]);
-    if (d1 < d0) return i + 1;
-    if (d1 == d0) alt = i + 1;
-    return i;
+    i = i < 0 ? 0 : (i > n - 2 ? max(n - 2, 0) : i);
+    const int i1 = min(i + 1, n - 1);
+    const double d0 = fabs(x - lv[i]), d1 = fabs(x - lv[i1]);
+    alt = d1 == d0 && i1 != i ? i1 : -1;
+    return d1 < d0 ? i1 : i;
 }
 
+// nearest grid point; on a tie the smallest symbol index (MATLAB min's first
+// index).  The alternative entries are read unconditionally at clamped indices:
+// a missing alternative reads the primary entry again, which leaves the min as is.
 __device__ __forceinline__ int slice_fast(const SlicerLds& t, int nI, int nQ, double2 z, double sI, double sQ) {
     int aI, aQ;
     const int iI = nearest_level_fast(t.lvI, nI, z.x, sI, aI);
     const int iQ = nearest_level_fast(t.lvQ, nQ, z.y, sQ, aQ);
-    int best = t.grid[iI * nQ + iQ];
-    if (aI >= 0) best = min(best, t.grid[aI * nQ + iQ]);
-    if (aQ >= 0) best = min(best, t.grid[iI * nQ + aQ]);
-    if (aI >= 0 && aQ >= 0) best = min(best, t.grid[aI * nQ + aQ]);
-    return best;
+    const int jI = aI >= 0 ? aI : iI, jQ = aQ >= 0 ? aQ : iQ;
+    const int b0 = t.grid[iI * nQ + iQ], b1 = t.grid[jI * nQ + iQ];
+    const int b2 = t.grid[iI * nQ + jQ], b3 = t.grid[jI * nQ + jQ];
+    return min(min(b0, b1), min(b2, b3));
 }
 
 // a / b with one division (rounding-level differences to c_div)
@@ -1128,19 +1140,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
     __shared__ double2 rpv[32];
     __shared__ int rdc[32];
     {
+        // every global load of the prologue is issued before the first wait
+        // (clamped indices, masked values): guarded loads would each be a branch
+        // with its own vmcnt(0), a chain of serial round trips per block
         const double2* __restrict__ src = sk.pm_a + (size_t)sk.pm_stride * blk;
-        for (int i = tid; i < NA; i += 256) sa[i] = src[i];
-        sym[tid] = tid < o.M ? o.symbols[tid] : make_double2(0.0, 0.0);
-        slt->grid[tid] = tid < o.nI * o.nQ ? o.grid_sym[tid] : 0;
+        constexpr int NIT = (NA + 255) / 256;
+        double2 av[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) av[k] = src[min(tid + 256 * k, NA - 1)];
+        const double2 sv = o.symbols[min(tid, o.M - 1)];
+        const int gv = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int lt = min(tid, 15);
+        const double li = o.lvI[min(lt, o.nI - 1)], lq = o.lvQ[min(lt, o.nQ - 1)];
+        const int rt = min(tid, 31);
+        const int row = row0 + (rt < nrows ? rt : 0);
+        const double2 pv = o.row_pval[row];
+        const int dr = o.row_data[row], cs = o.row_cons[row];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k)
+            if (tid + 256 * k < NA) sa[tid + 256 * k] = av[k];
+        sym[tid] = make_double2(tid < o.M ? sv.x : 0.0, tid < o.M ? sv.y : 0.0);
+        slt->grid[tid] = tid < o.nI * o.nQ ? gv : 0;
         if (tid < 16) {
-            slt->lvI[tid] = tid < o.nI ? o.lvI[tid] : 0.0;
-            slt->lvQ[tid] = tid < o.nQ ? o.lvQ[tid] : 0.0;
+            slt->lvI[tid] = tid < o.nI ? li : 0.0;
+            slt->lvQ[tid] = tid < o.nQ ? lq : 0.0;
         }
         if (tid < 32) {
-            const int row = row0 + (tid < nrows ? tid : 0);
-            rpv[tid] = o.row_pval[row];
+            rpv[tid] = pv;
             // data index << 1 | no-edge flag, or -1
-            rdc[tid] = tid < nrows && o.row_data[row] >= 0 ? (o.row_data[row] << 1) | (o.row_cons[row] ? 1 : 0) : -1;
+            rdc[tid] = tid < nrows && dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
         }
     }
     const double2* ga = sa;
@@ -1256,7 +1284,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
         auto epi_tile = [&](auto tcst) {
             constexpr int t = decltype(tcst)::value;
             double2 yv[4], hv[4];
-            int dc[4];
+            int dc[4], dps[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int rr = 16 * t + kq + 4 * r;
@@ -1281,11 +1309,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
                 const int ne = data ? __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu))) : 0;
                 e0 += ne;
                 e1 += (dc[r] & 1) ? ne : 0;
-                if (!last) {
+                dps[r] = dp;
+            }
+            // one uniform branch per tile, after all its rows (a branch per row
+            // splits the rows into separate blocks the scheduler cannot interleave)
+            if (!last) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
                     double2 av = make_double2(0.0, 0.0);
-                    c_fma(av, rpv[16 * t + kq + 4 * r], sym[dp]);
+                    c_fma(av, rpv[16 * t + kq + 4 * r], sym[dps[r]]);
                     // component-wise select (a struct-valued ?: became an
                     // address select through scratch)
+                    const bool data = dc[r] >= 0;
                     ur[t][r].x = data ? av.x : ur[t][r].x;
                     ur[t][r].y = data ? av.y : ur[t][r].y;
                 }
@@ -1775,11 +1810,16 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     if (FUSE) {
         stage_tables<256>(fsym, fslt[0], sk, threadIdx.x);
         const int r0b = P.row0[blk], nrb = P.nrows[blk];
-        if (threadIdx.x < RBP) {
-            const int rr = threadIdx.x, row = r0b + (rr < nrb ? rr : 0);
-            const int d = rr < nrb ? sk.row_data[row] : -1;
-            frpv[rr] = sk.row_pcol[row] >= 0 ? sk.row_pval[row] : make_double2(0.0, 0.0);
-            frdc[rr] = d >= 0 ? (d << 1) | (sk.row_cons[row] ? 1 : 0) : -1;
+        {
+            // unconditional loads (clamped row), masked after: see stage_tables
+            const int rr = min((int)threadIdx.x, RBP - 1), row = r0b + (rr < nrb ? rr : 0);
+            const int dr = sk.row_data[row], pc = sk.row_pcol[row], cs = sk.row_cons[row];
+            const double2 pv = sk.row_pval[row];
+            const int d = rr < nrb ? dr : -1;
+            if (threadIdx.x < RBP) {
+                frpv[rr] = make_double2(pc >= 0 ? pv.x : 0.0, pc >= 0 ? pv.y : 0.0);
+                frdc[rr] = d >= 0 ? (d << 1) | (cs ? 1 : 0) : -1;
+            }
         }
         __syncthreads();
         const int rl0 = (blockIdx.x * 64 + (int)(threadIdx.x >> 6) * 16 + (int)(threadIdx.x & 15)) % R;
