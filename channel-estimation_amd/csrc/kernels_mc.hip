@@ -1208,6 +1208,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
     const int c0 = maxd - d0, c1 = maxd - d1;
     const int src_lane = (l + 16) & 63;
     const int snr = o.snr0 + (ug * WAVE) / R;
+    // 1 / |h|^2 of the lane's 8 rows: iteration-invariant, computed once (the
+    // IEEE division is ~12 FP64 instructions per row); not for KSQ 7, where the
+    // 16 extra registers would cost the third wave per SIMD
+    constexpr bool HID = KSQ <= 6;
+    double hid[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int rr = 16 * t + kq + 4 * r;
+            const double2 hh = HID ? o.h[(size_t)(row0 + (rr < nrows ? rr : 0)) * R + rl] : make_double2(1.0, 0.0);
+            hid[t][r] = HID ? 1.0 / (hh.x * hh.x + hh.y * hh.y) : 1.0;
+        }
     for (int it = 1; it <= niter; ++it) {
         // the loads below are the same every iteration: an opaque zero keeps the
         // compiler from hoisting them out of the loop (they would stay live
@@ -1300,7 +1313,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
             for (int r = 0; r < 4; ++r) {
                 double2 yp = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
                 yp = c_add(yp, c_mul(hv[r], ur[t][r]));
-                const double2 z = c_div1(yp, hv[r]);
+                // = c_div1(yp, hv[r]), with the hoisted reciprocal when HID
+                const double id = HID ? hid[t][r] : 1.0 / (hv[r].x * hv[r].x + hv[r].y * hv[r].y);
+                const double2 z = make_double2((yp.x * hv[r].x + yp.y * hv[r].y) * id,
+                                               (yp.y * hv[r].x - yp.x * hv[r].y) * id);
                 const int dp = slice_fast(*slt, o.nI, o.nQ,
                                           o.real_detect ? make_double2(z.x * o.idd, 0.0)
                                                         : make_double2(z.x * o.idd, z.y * o.idd),
