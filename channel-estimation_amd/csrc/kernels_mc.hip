@@ -199,20 +199,26 @@ __device__ __forceinline__ double2 c_mul_fma(double2 z, double2 w) {
 }
 
 static constexpr int JCH_MAX = 16;
-template <int JCH>
+// RPW realisations per wave (LPR = 64 / RPW lanes each): with N = 540 two
+// realisations of 32 chunks of 17 samples keep every lane busy with twice the
+// chunk length of one realisation per wave (the per-chunk cis is amortised over
+// 17 samples instead of 9).
+template <int JCH, int RPW>
 __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
                                                double2* __restrict__ ir) {
     extern __shared__ double sm[];
+    constexpr int LPR = WAVE / RPW;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = RPW == 1 ? 0 : lane / LPR, sl = RPW == 1 ? lane : lane % LPR;
     const int P = ch.paths;
-    double* ds = sm + (size_t)wv * 4 * P;
+    double* ds = sm + (size_t)(wv * RPW + sub) * 4 * P;
     double* ph = ds + P;
     double* wr = ph + P;
     double* wi = wr + P;
     const int tap = blockIdx.z;
-    const int rl = blockIdx.y * 4 + wv;
+    const int rl = (blockIdx.y * 4 + wv) * RPW + sub;
     const uint64_t rep = rep0 + (uint64_t)rl;
-    for (int p = lane; p < P; p += WAVE) {
+    for (int p = sl; p < P; p += LPR) {
         const uint32_t e = (uint32_t)(tap + ch.ntap * p);       // rand([Ntap 1 Paths]) column-major
         const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, e >> 1);
         const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, e >> 1);
@@ -227,7 +233,7 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
         wi[p] = sn;
     }
     __syncthreads();
-    const int n0 = (blockIdx.x * WAVE + lane) * JCH;
+    const int n0 = (blockIdx.x * LPR + sl) * JCH;
     if (n0 >= ch.N) return;
     const double t0 = (double)n0 * ch.dt;
     double2 acc[JCH];
@@ -288,12 +294,13 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
     }
 }
 
-template <int JCH>
+template <int JCH, int RPW = 1>
 static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+    constexpr int LPR = WAVE / RPW;
     const int nchunk = (ch.N + JCH - 1) / JCH;
-    dim3 grid((nchunk + WAVE - 1) / WAVE, R / 4, ch.ntap);
-    hipLaunchKernelGGL(k_jakes<JCH>, grid, dim3(256), (size_t)4 * 4 * ch.paths * sizeof(double), s, ch, seed, rep0, R,
-                       ir);
+    dim3 grid((nchunk + LPR - 1) / LPR, R / (4 * RPW), ch.ntap);
+    hipLaunchKernelGGL((k_jakes<JCH, RPW>), grid, dim3(256), (size_t)4 * RPW * 4 * ch.paths * sizeof(double), s, ch,
+                       seed, rep0, R, ir);
 }
 
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
@@ -371,6 +378,15 @@ __global__ void __launch_bounds__(64) k_discrete(ChannelK ch, uint64_t seed, uin
     }
 }
 
+// DSCE_JAKES_RPW=1 keeps one realisation per wave (A/B switch)
+static bool jakes_rpw2() {
+    static const bool on = [] {
+        const char* e = getenv("DSCE_JAKES_RPW");
+        return !(e && atoi(e) == 1);
+    }();
+    return on;
+}
+
 void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
     if (ch.fD == 0.0) {
         hipLaunchKernelGGL(k_static, dim3(R / WAVE, (ch.N + 63) / 64, ch.ntap), dim3(WAVE), 0, s, ch, seed, rep0, R, ir);
@@ -380,6 +396,27 @@ void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep
         hipLaunchKernelGGL(k_discrete, dim3(R / WAVE, (ch.N + DCH - 1) / DCH, ch.ntap), dim3(WAVE), 0, s, ch, seed,
                            rep0, R, ir);
         return;
+    }
+    // two realisations per wave (32 lanes each) when that gives chunks of 9-20
+    // samples (N 257-640) and R splits into blocks of 8; the LDS path tables
+    // then take 64 P bytes per realisation, 51 KB per block at P = 200
+    const int jch2 = (ch.N + WAVE / 2 - 1) / (WAVE / 2);
+    if (jch2 >= 9 && jch2 <= 20 && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024 &&
+        jakes_rpw2()) {
+        switch (jch2) {
+            case 9: launch_jakes_t<9, 2>(s, ch, seed, rep0, R, ir); return;
+            case 10: launch_jakes_t<10, 2>(s, ch, seed, rep0, R, ir); return;
+            case 11: launch_jakes_t<11, 2>(s, ch, seed, rep0, R, ir); return;
+            case 12: launch_jakes_t<12, 2>(s, ch, seed, rep0, R, ir); return;
+            case 13: launch_jakes_t<13, 2>(s, ch, seed, rep0, R, ir); return;
+            case 14: launch_jakes_t<14, 2>(s, ch, seed, rep0, R, ir); return;
+            case 15: launch_jakes_t<15, 2>(s, ch, seed, rep0, R, ir); return;
+            case 16: launch_jakes_t<16, 2>(s, ch, seed, rep0, R, ir); return;
+            case 17: launch_jakes_t<17, 2>(s, ch, seed, rep0, R, ir); return;
+            case 18: launch_jakes_t<18, 2>(s, ch, seed, rep0, R, ir); return;
+            case 19: launch_jakes_t<19, 2>(s, ch, seed, rep0, R, ir); return;
+            default: launch_jakes_t<20, 2>(s, ch, seed, rep0, R, ir); return;
+        }
     }
     int jch = (ch.N + WAVE - 1) / WAVE;           // samples per lane: one wave covers N when N <= 1024
     if (jch > JCH_MAX) jch = JCH_MAX;
