@@ -1281,9 +1281,11 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     check_ctx(ctx);
     if (!ctx->chan_set) throw ApiError(DSCE_ESTATE, "dsce_set_channel first");
     if (!ir_out) throw ApiError(DSCE_EINVAL, "null output");
-    const int N = ctx->ch.N, R = 64;
+    // the realisation sits at lane rep % 8 of its batch, so the tests reach every
+    // position of the kernels' realisation-to-wave mapping
+    const int N = ctx->ch.N, R = 64, lane = (int)(rep % 8);
     double2* ir = dalloc<double2>(ctx, (size_t)ctx->ch.ntap * N * R);
-    launch_jakes(ctx->stream, ctx->ch, seed, rep, R, ir);
+    launch_jakes(ctx->stream, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
     std::vector<double2> h((size_t)ctx->ch.ntap * N * R);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ir, h.size() * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -1293,7 +1295,7 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     for (size_t i = 0; i < (size_t)N * ntot * 2; ++i) ir_out[i] = 0.0;
     for (int q = 0; q < ctx->ch.ntap; ++q)
         for (int n = 0; n < N; ++n) {
-            const double2 v = h[((size_t)q * N + n) * R + 0];
+            const double2 v = h[((size_t)q * N + n) * R + lane];
             const size_t o = (size_t)ctx->ch.tap_delay[q] * N + n;
             ir_out[2 * o] = v.x;
             ir_out[2 * o + 1] = v.y;
