@@ -1838,7 +1838,7 @@ struct FuseArgs {
     int var, stage, nstage, last, scheme;
 };
 
-template <int RBP, int NKS, bool FUSE>
+template <int RBP, int NKS, bool FUSE, bool WDA_3M = false>
 __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems,
                                                 int var, int nsnr, int snr0, int R, int U,
                                                 const double2* __restrict__ hp, const double2* v,
@@ -2008,25 +2008,43 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     // it in LDS measured no faster.)
     d4 er[2], ei[2];
     {
-        double hr[NKS], hi[NKS];
+        double hr[NKS], hi[NKS], hs[NKS];
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             const double2 hv = fa.hp_new[(size_t)(4 * ks + g) * U + unit];
             hr[ks] = hv.x;
             hi[ks] = hv.y;
+            hs[ks] = hv.x + hv.y;
         }
         const double2* __restrict__ wa = fa.WdA + (((size_t)fa.var * nsnr + snr) * P.nblk + blk) * 2 * NKS * 64 + lane;
+        if (WDA_3M) {
+            // 3M like the contraction: three real MFMAs per k-step instead of four
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            er[t] = d4{0.0, 0.0, 0.0, 0.0};
-            ei[t] = er[t];
+            for (int t = 0; t < 2; ++t) {
+                d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
 #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const double2 a = wa[(t * NKS + ks) * 64];
-                er[t] = MFMA64(a.x, hr[ks], er[t]);
-                er[t] = MFMA64(-a.y, hi[ks], er[t]);
-                ei[t] = MFMA64(a.x, hi[ks], ei[t]);
-                ei[t] = MFMA64(a.y, hr[ks], ei[t]);
+                for (int ks = 0; ks < NKS; ++ks) {
+                    const double2 a = wa[(t * NKS + ks) * 64];
+                    p1 = MFMA64(a.x, hr[ks], p1);
+                    p2 = MFMA64(a.y, hi[ks], p2);
+                    p3 = MFMA64(a.x + a.y, hs[ks], p3);
+                }
+                er[t] = p1 - p2;
+                ei[t] = p3 - p1 - p2;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                er[t] = d4{0.0, 0.0, 0.0, 0.0};
+                ei[t] = er[t];
+#pragma unroll
+                for (int ks = 0; ks < NKS; ++ks) {
+                    const double2 a = wa[(t * NKS + ks) * 64];
+                    er[t] = MFMA64(a.x, hr[ks], er[t]);
+                    er[t] = MFMA64(-a.y, hi[ks], er[t]);
+                    ei[t] = MFMA64(a.x, hi[ks], ei[t]);
+                    ei[t] = MFMA64(a.y, hr[ks], ei[t]);
+                }
             }
         }
     }
@@ -2153,8 +2171,14 @@ void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int va
     fa.nstage = n_iter + 1;
     fa.last = last ? 1 : 0;
     fa.scheme = scheme_index;
-    hipLaunchKernelGGL((k_wpair3<24, 4, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems,
-                       var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    // DSCE_WDA_3M=0: diag(D_hat) of the epilogue with four real MFMAs per k-step
+    const char* e3 = getenv("DSCE_WDA_3M");
+    if (e3 && e3[0] == '0')
+        hipLaunchKernelGGL((k_wpair3<24, 4, true, false>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
+                           mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    else
+        hipLaunchKernelGGL((k_wpair3<24, 4, true, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
+                           mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
 }
 
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
