@@ -95,6 +95,7 @@ struct Scheme {
     double2* Wpil = nullptr;        // fused MMSE stage operands (null: not eligible)
     double2* WdA = nullptr;
     int* pil_c0 = nullptr;
+    int w3x4 = 0;
     long long wp_elems = 0, wp_exec = 0;
     PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
@@ -615,7 +616,14 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
     const int nsl = 2 * c->nsnr;
     s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
     s.Wp3 = dalloc<double>(c, (size_t)nsl * 3 * s.wp_elems);
-    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3);
+    // W's 3M planes two k-steps per 16-byte lane load (half the load
+    // instructions of the contraction's tile loop); DSCE_W3_X4=0 at build time:
+    // one double per lane and plane
+    {
+        const char* e = getenv("DSCE_W3_X4");
+        s.w3x4 = (s.Pb.nks % 2 == 0 && !(e && e[0] == '0')) ? 1 : 0;
+    }
+    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3, s.w3x4);
     // fused MMSE stage: block-diagonal W (every block's columns are its own 24
     // rows, OFDM), row-local precoder, select-mode detection, NP = 16
     bool fuse = rbp == 24 && NP == 16 && s.k.p_diag && !s.d.despread;
@@ -889,6 +897,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.Wpil = s.Wpil;
         mm.WdA = s.WdA;
         mm.pil_c0 = s.pil_c0;
+        mm.w3x4 = s.w3x4;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);

@@ -51,6 +51,7 @@ struct MmseK {
     const double2* Wpil;  // [var][snr][NP pilots][24 columns][NP]
     const double2* WdA;   // [var][snr][blk][2][NP/4][64] diag(W) rows, MFMA A layout
     const int* pil_c0;    // NP: first column of each pilot row's block
+    int w3x4;             // Wp3 in the 16-byte layout (two k-steps per lane and plane)
 };
 
 // Monte-Carlo pipeline
@@ -121,7 +122,7 @@ void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const doub
                        const double2* wd, int nslices, const int* pil_blk, const int* pilot_pos, int ncol,
                        double2* wpil, double2* wda);
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices, double* w3);
+                 double2* wp, long long wp_elems, int nslices, double* w3, int w3x4);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);
 void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
              const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);

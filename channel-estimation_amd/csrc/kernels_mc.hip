@@ -1838,12 +1838,12 @@ struct FuseArgs {
     int var, stage, nstage, last, scheme;
 };
 
-template <int RBP, int NKS, bool FUSE, bool WDA_3M = false>
-__global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems,
-                                                int var, int nsnr, int snr0, int R, int U,
-                                                const double2* __restrict__ hp, const double2* v,
-                                                const double2* __restrict__ y, double2* __restrict__ yest,
-                                                SchemeK sk, FuseArgs fa) {
+template <int RBP, int NKS, bool FUSE, bool WDA_3M, bool X4>
+__device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __restrict__ W3, long long wp_elems,
+                                            int var, int nsnr, int snr0, int R, int U,
+                                            const double2* __restrict__ hp, const double2* v,
+                                            const double2* __restrict__ y, double2* __restrict__ yest,
+                                            const SchemeK& sk, const FuseArgs& fa) {
     constexpr int PER = RBP == 24 ? 3 : 2;
     constexpr int CPP = RBP == 24 ? 2 : 1;
     constexpr int NACC = RBP / 4;
@@ -1894,7 +1894,8 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
         bs[ks] = h.x + h.y;
     }
     const int clo = P.clo[blk], ntile = P.ntile[blk];
-    const double* __restrict__ w = W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + lane;
+    const double* __restrict__ w =
+        W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + (X4 ? 2 * lane : lane);
     double2 acc[NACC];
 #pragma unroll
     for (int k = 0; k < NACC; ++k) acc[k] = make_double2(0.0, 0.0);
@@ -1906,12 +1907,27 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
         d4 p1, p2, p3;
     };
     auto ldt = [&](int t, T3& a) {
+        if (X4) {
+            // [tile][k-step pair][plane][lane][2]: one 16-byte load per plane and pair
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const double* q = w + ((size_t)t * NKS + ks) * 192;
-            a.r[ks] = q[0];
-            a.i[ks] = q[64];
-            a.s[ks] = q[128];
+            for (int kp = 0; kp < NKS / 2; ++kp) {
+                const double2* q = reinterpret_cast<const double2*>(w + ((size_t)t * (NKS / 2) + kp) * 384);
+                const double2 r = q[0], i = q[64], sm = q[128];
+                a.r[2 * kp] = r.x;
+                a.r[2 * kp + 1] = r.y;
+                a.i[2 * kp] = i.x;
+                a.i[2 * kp + 1] = i.y;
+                a.s[2 * kp] = sm.x;
+                a.s[2 * kp + 1] = sm.y;
+            }
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const double* q = w + ((size_t)t * NKS + ks) * 192;
+                a.r[ks] = q[0];
+                a.i[ks] = q[64];
+                a.s[ks] = q[128];
+            }
         }
     };
     auto mma = [&](const T3& a, D3& d) {
@@ -2093,6 +2109,22 @@ __global__ void __launch_bounds__(256) k_wpair3(PairBand P, const double* __rest
     if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage);
 }
 
+#define WPAIR3_ARGS                                                                                          \
+    PairBand P, const double* __restrict__ W3, long long wp_elems, int var, int nsnr, int snr0, int R, int U, \
+        const double2* __restrict__ hp, const double2* v, const double2* __restrict__ y,                      \
+        double2* __restrict__ yest, SchemeK sk, FuseArgs fa
+template <int RBP, int NKS, bool FUSE, bool WDA_3M = false, bool X4 = false>
+__global__ void __launch_bounds__(256) k_wpair3(WPAIR3_ARGS) {
+    wpair3_body<RBP, NKS, FUSE, WDA_3M, X4>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
+}
+
+// the fused kernel with the 16-byte W loads held to 168 VGPRs (3 waves/SIMD)
+template <int RBP, int NKS, bool WDA_3M>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_wpair3_f3(WPAIR3_ARGS) {
+    wpair3_body<RBP, NKS, true, WDA_3M, true>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
+}
+#undef WPAIR3_ARGS
+
 // Pre-pass of the fused MMSE stage of IC iteration `stage` (script:482-489):
 // y_est at the NP pilot rows with the previous stage's D_hat (W of var_prev,
 // the contraction's), then the LS estimates hP = y_est(pilots) ./ xP /
@@ -2173,12 +2205,26 @@ void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int va
     fa.scheme = scheme_index;
     // DSCE_WDA_3M=0: diag(D_hat) of the epilogue with four real MFMAs per k-step
     const char* e3 = getenv("DSCE_WDA_3M");
-    if (e3 && e3[0] == '0')
-        hipLaunchKernelGGL((k_wpair3<24, 4, true, false>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
-                           mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
-    else
-        hipLaunchKernelGGL((k_wpair3<24, 4, true, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
-                           mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    const bool wda3 = !(e3 && e3[0] == '0');
+#define LAUNCH_FW(WDA, X4V)                                                                                        \
+    hipLaunchKernelGGL((k_wpair3<24, 4, true, WDA, X4V>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb,         \
+                       mm.Wp3, mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa)
+    const char* e3w = getenv("DSCE_WPAIR_3W");
+    if (mm.w3x4 && e3w && e3w[0] == '1') {
+        if (wda3)
+            hipLaunchKernelGGL((k_wpair3_f3<24, 4, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
+                               mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+        else
+            hipLaunchKernelGGL((k_wpair3_f3<24, 4, false>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
+                               mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    } else if (mm.w3x4) {
+        if (wda3) LAUNCH_FW(true, true);
+        else LAUNCH_FW(false, true);
+    } else {
+        if (wda3) LAUNCH_FW(true, false);
+        else LAUNCH_FW(false, false);
+    }
+#undef LAUNCH_FW
 }
 
 void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
@@ -2197,8 +2243,12 @@ void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
         if (mm.Wp3 && m3) {
 #define LAUNCH_W3(RBPV, NKSV)                                                                                    \
     {                                                                                                            \
-        hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,    \
-                           mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{});                   \
+        if (mm.w3x4)                                                                                             \
+            hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false, false, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3,   \
+                               mm.wp_elems, var, mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{}); \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems,   \
+                               var, mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{});           \
     }
             if (mm.Pb.rbp == 24) {
                 if (mm.Pb.nks == 2) LAUNCH_W3(24, 2)

@@ -11,6 +11,8 @@
 // once); see DESIGN.md §Setup.
 #include "dsce_kernels.h"
 
+#include <stdlib.h>
+
 #include <math.h>
 
 namespace dsce {
@@ -358,18 +360,28 @@ __global__ void k_wpair_pack(Band Wb, int NP, const double2* __restrict__ w, lon
 
 // 3M planes of the pair tiles: per (tile, k-step) the 64 lanes' Re, Im and
 // Re+Im as three contiguous 64-double rows (k_wpair's Gauss/Karatsuba form).
-__global__ void k_wpair_pack3(long long wp_elems, const double2* __restrict__ wp, double* __restrict__ w3) {
+// x4 (MmseK::w3x4): the planes of two consecutive k-steps interleaved per lane,
+// [tile][k-step pair][plane][lane][2], so k_wpair3 fetches them with 16-byte
+// loads — half the load instructions of one double per lane and plane.
+__global__ void k_wpair_pack3(long long wp_elems, int nks, int x4, const double2* __restrict__ wp,
+                              double* __restrict__ w3) {
     const long long n = wp_elems;
     const double2* __restrict__ src = wp + (size_t)blockIdx.y * wp_elems;
     double* __restrict__ dst = w3 + (size_t)blockIdx.y * 3 * wp_elems;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
         const double2 v = src[e];
         const long long g = e / 64, l = e % 64;
-        dst[(g * 3 + 0) * 64 + l] = v.x;
-        dst[(g * 3 + 1) * 64 + l] = v.y;
-        dst[(g * 3 + 2) * 64 + l] = v.x + v.y;
+        const double pv[3] = {v.x, v.y, v.x + v.y};
+        if (x4) {
+            const long long t = g / nks, ks = g % nks;
+            for (int pl = 0; pl < 3; ++pl)
+                dst[((t * (nks / 2) + ks / 2) * 3 + pl) * 128 + 2 * l + (ks & 1)] = pv[pl];
+        } else {
+            for (int pl = 0; pl < 3; ++pl) dst[(g * 3 + pl) * 64 + l] = pv[pl];
+        }
     }
 }
+
 
 // Operands of the fused MMSE stage (k_pilot_pre + k_wpair3<..., true>), block-
 // diagonal schemes only.  Wpil[slice][pilot i][cc][p] = W[(pilot row, c0_i + cc), p]
@@ -414,9 +426,10 @@ void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const doub
 }
 
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices, double* w3) {
+                 double2* wp, long long wp_elems, int nslices, double* w3, int w3x4) {
     hipLaunchKernelGGL(k_wpair_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, P, wp, wp_elems);
-    if (w3) hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, wp, w3);
+    if (w3)
+        hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, P.nks, w3x4, wp, w3);
 }
 
 // G[n, l + L k] in closed form (OFDM.m:153-165, :184-203; FBMC.m:255-285,

@@ -257,6 +257,23 @@ def test_stage_variants_agree(monkeypatch, name):
     eng.close()
 
 
+def test_w3_layouts_agree(monkeypatch):
+    """W's 3M planes packed two k-steps per 16-byte lane load (default) or one
+    double per lane (DSCE_W3_X4=0, chosen when the estimator is built): the
+    contraction reads the same values, counts are identical, fused and unfused."""
+    from dsce.engine import build_engine
+    S = build_setup("default", schemes=("ofdm",), snr_db=[10.0, 25.0, 40.0])
+    x4 = build_engine(S, batch=512)
+    monkeypatch.setenv("DSCE_W3_X4", "0")
+    x2 = build_engine(S, batch=512)
+    monkeypatch.delenv("DSCE_W3_X4")
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("DSCE_FUSE_STAGE", fuse)
+        np.testing.assert_array_equal(x4.run(SEED, 0, 1024), x2.run(SEED, 0, 1024), err_msg=fuse)
+    x4.close()
+    x2.close()
+
+
 @pytest.mark.parametrize("name", ["default", "c5", "paper"])
 def test_tx_matrices_on_gpu_match_host_mirror(name):
     """Row f1: G and Q = GetRXMatrix' produced on the GPU in closed form equal
