@@ -242,12 +242,13 @@ def test_stage_variants_agree(monkeypatch, name):
     # stage as its own kernels instead of fused into the contraction, the
     # perfect-CSI chain as per-iteration passes / VALU chain instead of k_pic_mfma,
     # the fused epilogue's diag(D_hat) with 4 real MFMAs instead of 3M, one
-    # realisation per Jakes wave (17- vs 9-sample recurrence chunks)
+    # realisation per Jakes wave (17- vs 9-sample recurrence chunks), the fused
+    # contraction held to 3 waves/SIMD
     variants = ({"DSCE_PFUSE": "0"}, {"DSCE_XCD": "0"}, {"DSCE_SNR_CHUNK": "2"}, {"DSCE_STREAMS": "2"},
                 {"DSCE_PIC": "1", "DSCE_PIC_CHAIN": "0"}, {"DSCE_WPAIR_3M": "0"}, {"DSCE_WCONTRACT": "mfma"},
                 {"DSCE_FUSE_STAGE": "0"}, {"DSCE_PIC_CHAIN": "0"}, {"DSCE_PIC_CHAIN": "1"},
                 {"DSCE_STREAMS": "2", "DSCE_FUSE_STAGE": "0"}, {"DSCE_NOISE_FUSE": "0"}, {"DSCE_WDA_3M": "0"},
-                {"DSCE_JAKES_RPW": "1"})
+                {"DSCE_JAKES_RPW": "1"}, {"DSCE_WPAIR_3W": "1"}, {"DSCE_WPAIR_3W": "1", "DSCE_WDA_3M": "0"})
     for env in variants:
         for var, val in env.items():
             monkeypatch.setenv(var, val)
