@@ -1,29 +1,37 @@
 #!/usr/bin/env python3
 """Headline benchmark: Monte-Carlo channel realisations/s at 24 sc x 14 sym.
 
-Workload (BASELINE.json configs[1], "C2"): OFDM 24 subcarriers x 14 symbols,
-N = 540 samples, Jakes 500 km/h @ 2.5 GHz, VehicularA, 256-QAM, 16 pilots,
-doubly-selective MMSE channel estimation + 4 interference-cancellation
-iterations, 7 SNR points (10:5:40 dB).  One realisation = one iteration of
-the Monte-Carlo loop body of DoublySelectiveChannelEstimation.m:350-564 for
-this scheme: channel draw + TX + perfect-CSI diag(D), then for every SNR point
-noise, demodulation, LS, MMSE one-tap, perfect-CSI one-tap and 4 IC iterations
-for both, with bit-error counting (with/without edges).  Setup (correlation
-matrices, W) is excluded and reported separately.
+Workload (BASELINE.json configs[1], "C2", the default): OFDM 24 subcarriers x
+14 symbols, N = 540 samples, Jakes 500 km/h @ 2.5 GHz, VehicularA, 256-QAM,
+16 pilots, doubly-selective MMSE channel estimation + 4 interference-
+cancellation iterations, 7 SNR points (10:5:40 dB).  One realisation = one
+iteration of the Monte-Carlo loop body of DoublySelectiveChannelEstimation.m:
+350-564 for this scheme: channel draw + TX + perfect-CSI diag(D), then for
+every SNR point noise, demodulation, LS, MMSE one-tap, perfect-CSI one-tap and
+4 IC iterations for both, with bit-error counting (with/without edges).  Setup
+(correlation matrices, W) is excluded and reported separately.
+``--config c3|c4|c5`` measures the other single-GPU configurations the same
+way (FBMC auxiliary / data-spreading 24 x 30; 48 x 30 at SR 720 kHz with the
+three schemes and 16 SNR points).
 
 A "step" = one pass of the hot path over --reps-per-step realisations
-(synthetic Philox inputs).  With N GPUs (torch.distributed.run, one rank per
-GPU) every rank processes its own contiguous realisation range (weak scaling,
-no collective inside the data path); the int64 error counters are summed with
-ONE all-reduce (RCCL) at the end of the timed region.
+(synthetic Philox inputs, generated on the device).  With N GPUs (one rank per
+GPU, torch.distributed) every rank processes its own contiguous realisation
+range (weak scaling, no collective inside the data path); the int64 error
+counters are summed with ONE all-reduce (RCCL) after the timed steps.
+``--gpus N`` without a launcher starts ``torch.distributed.run`` itself (as a
+child process) and forwards rank 0's line.
 
-Prints one JSON line (rank 0).  See DESIGN.md §Measurement.
+Prints one JSON line (rank 0).  See DESIGN.md §6.
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
+import statistics
 import subprocess
 import sys
 import time
@@ -32,60 +40,150 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "channel-estimation_amd")]
 
 METRIC = "Monte-Carlo channel realisations/sec at 24sc x 14sym; BER curve match vs ref"
-FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 matrix/vector peak (AMD spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 matrix peak (AMD spec) — measured value reported beside it
 HBM_PEAK_GBS = 8000.0
 SEED = 0x5EED0002
 
+# workload -> (setup name, schemes, default reps per step (= engine batch), description)
+WORKLOADS = {
+    "c2": ("default", ("ofdm",), 65536,
+           "C2: OFDM 24sc x 14sym, N=540, Jakes 500 km/h VehA, 256-QAM, 16 pilots, 7 SNR (10:5:40 dB) x "
+           "(one-tap + 4 IC) x (MMSE + perfect CSI)"),
+    "c3": ("default", ("fbmc_aux",), 32768,
+           "C3: FBMC-OQAM auxiliary-symbol pilots 24sc x 30sym, N=540, PAM-16, 16 pilots + 64 aux, 7 SNR x "
+           "(one-tap + 4 IC) x (MMSE + perfect CSI)"),
+    "c4": ("default", ("fbmc_cod",), 32768,
+           "C4: FBMC-OQAM data-spreading pilots 24sc x 30sym, N=540, PAM-16, 7 SNR x (one-tap + 4 IC) x "
+           "(MMSE + perfect CSI)"),
+    "c5": ("c5", ("fbmc_aux", "fbmc_cod", "ofdm"), 8192,
+           "C5: 48sc x 30sym (OFDM 48x14) at SR 720 kHz, N=1080, 32 pilots, 3 taps, 16 SNR (10:2:40 dB), "
+           "3 schemes x (one-tap + 4 IC) x (MMSE + perfect CSI)"),
+}
 
-def cpu_baseline_leg(seconds):
-    """Oracle (literal NumPy restatement of the reference's dense formulation)
-    timed on one host core on a bounded sample of the same workload."""
+
+def source_hash():
+    """sha256 over the engine's sources: stamps PMC profiles to the build they measured."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "channel-estimation_amd", "csrc", "*"))) + [
+        os.path.join(ROOT, "include", "dsce.h"), os.path.join(ROOT, "channel-estimation_amd", "Makefile")]
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode())
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle (literal NumPy restatement of the reference's dense
+# formulation) on the GPU box's host cores, bounded sample, median of 3
+# ---------------------------------------------------------------------------
+def cpu_baseline_leg(seconds, workload):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import harness
     from dsce.configs import build_setup
     from oracle import refsim
-    S = build_setup("default", schemes=("ofdm",))
-    sc = S.schemes["ofdm"]
-    mm = harness.oracle_mmse(S, sc)                       # setup, untimed
+    name, schemes, _, _ = WORKLOADS[workload]
+    S = build_setup(name, schemes=schemes)
+    scs = [S.schemes[s] for s in schemes]
+    mm = [harness.oracle_mmse(S, sc) for sc in scs]             # setup, untimed
     chan = harness.oracle_chan(S)
-    osc = [harness.oracle_scheme(sc)]
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        refsim.simulate(SEED, 10_000_000 + n, 1, chan, osc, S.pn_time, S.n_iter, [mm])
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and n >= 2:
-            break
-    print(json.dumps({"value": n / el, "reps": n, "seconds": el}))
+    osc = [harness.oracle_scheme(sc) for sc in scs]
+    refsim.simulate(SEED, 20_000_000, 1, chan, osc, S.pn_time, S.n_iter, mm)   # warm-up
+    rates = []
+    n_total = 0
+    for k in range(3):
+        n = 0
+        t0 = time.perf_counter()
+        while True:
+            refsim.simulate(SEED, 10_000_000 + n_total, 1, chan, osc, S.pn_time, S.n_iter, mm)
+            n += 1
+            n_total += 1
+            el = time.perf_counter() - t0
+            if el >= seconds / 3 and n >= 1:
+                break
+        rates.append(n / el)
+    print(json.dumps({"rates": rates, "reps": n_total}))
 
 
-def run_cpu_baseline(seconds):
-    env = dict(os.environ)
-    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "BLIS_NUM_THREADS"):
-        env[k] = "1"
-    env["HIP_VISIBLE_DEVICES"] = ""
-    out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds",
-                          str(seconds)], env=env, capture_output=True, text=True, timeout=600)
-    if out.returncode != 0:
-        return None
-    r = json.loads(out.stdout.strip().splitlines()[-1])
-    return {"value": r["value"], "unit": "realisations/s", "cores": 1, "kind": "port",
-            "sample": "oracle/refsim.simulate (dense Q'HG, full(W) contraction, brute-force detection, "
-                      "NumPy fp64, 1 thread), %d realisations of the C2 workload in %.1f s" % (r["reps"], r["seconds"])}
+def host_info():
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Thread(s) per core", "Core(s) per socket"):
+                info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    return info
 
 
-def latest_pmc_traffic():
-    """HBM bytes per k_wcontract launch from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_wcontract.json written by tools/pmc_summary.py), or None."""
-    d = os.path.join(ROOT, "profiles")
-    if not os.path.isdir(d):
-        return None
-    c = sorted(f for f in os.listdir(d) if f.endswith("_pmc_wcontract.json"))
-    if not c:
-        return None
-    with open(os.path.join(d, c[-1])) as f:
-        return json.load(f).get("hbm_bytes_per_launch")
+def run_cpu_baseline(seconds, workload):
+    host = host_info()
+    nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or host.get("affinity") or host["nproc"]
+    legs = {}
+    for threads in (1, nt):
+        env = dict(os.environ)
+        for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "BLIS_NUM_THREADS"):
+            env[k] = str(threads)
+        env["HIP_VISIBLE_DEVICES"] = ""
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds",
+                              str(seconds / 2), "--config", workload], env=env, capture_output=True, text=True,
+                             timeout=900)
+        if out.returncode != 0:
+            return None
+        legs[threads] = json.loads(out.stdout.strip().splitlines()[-1])
+    med = {t: statistics.median(r["rates"]) for t, r in legs.items()}
+    return {"value": med[nt], "unit": "realisations/s", "cores": nt, "kind": "port",
+            "value_1t": med[1], "value_nt": med[nt], "samples_1t": legs[1]["rates"], "samples_nt": legs[nt]["rates"],
+            "label": "CPU restatement of reference algorithm, not MATLAB",
+            "sample": "oracle/refsim.simulate (dense Q'HG zgemm, full(W) reshape-and-sum contraction, brute-force "
+                      "nearest-neighbour detection, NumPy/OpenBLAS fp64) on %s; median of 3 samples of ~%.0f s per "
+                      "thread count (%d and %d threads), %d + %d realisations"
+                      % (workload.upper(), seconds / 6, 1, nt, legs[1]["reps"], legs[nt]["reps"]),
+            "host": host}
+
+
+def stored_traffic(kernel_tag, workload):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
+    summary (profiles/*_pmc_wcontract.json, tools/prof_summary.py), used only
+    when it was measured on a build of these exact sources and this workload."""
+    src = source_hash()
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_wcontract.json")), key=os.path.getmtime)
+    for f in reversed(cands):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("source_hash") == src and d.get("workload", "c2") == workload:
+            return d.get("hbm_bytes_per_launch"), "profiles/" + os.path.basename(f)
+    return None, "no PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
+
+
+# ---------------------------------------------------------------------------
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: one rank per GPU via torch.distributed.run,
+    started as a child process before anything touches the GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    line = None
+    for ln in p.stdout.splitlines():
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln
+    if p.returncode != 0 or line is None:
+        sys.stderr.write(p.stdout[-4000:] + p.stderr[-4000:])
+        return p.returncode or 1
+    print(line)
+    return 0
 
 
 def main():
@@ -93,17 +191,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reps-per-step", type=int, default=65536)
-    ap.add_argument("--batch", type=int, default=65536, help="realisations per device batch")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--reps-per-step", type=int, default=0, help="realisations per step per GPU (0: workload default)")
+    ap.add_argument("--batch", type=int, default=0, help="realisations per device batch (0: = reps per step)")
+    ap.add_argument("--option", action="append", default=[], help="engine option name=value (dsce_set_option)")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-leg", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_leg:
-        cpu_baseline_leg(args.cpu_seconds)
-        return
+        cpu_baseline_leg(args.cpu_seconds, args.config)
+        return 0
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%d\n" % (args.gpus, world))
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -121,63 +227,91 @@ def main():
     from dsce.configs import build_setup
     from dsce.engine import build_engine
 
-    S = build_setup("default", schemes=("ofdm",))
+    setup_name, schemes, default_reps, desc = WORKLOADS[args.config]
+    B = args.reps_per_step or default_reps
+    batch = args.batch or B
+    options = {}
+    for kv in args.option:
+        k, v = kv.split("=")
+        options[k.strip()] = int(v)
+    S = build_setup(setup_name, schemes=schemes)
     t_setup = time.perf_counter()
-    eng = build_engine(S, device=device, batch=args.batch)
+    eng = build_engine(S, device=device, batch=batch, options=options)
     setup_s = time.perf_counter() - t_setup
-    B = args.reps_per_step
     counts = np.zeros(eng.counter_shape(), dtype=np.int64)
     base = rank * (args.steps + args.warmup) * B
     for w in range(args.warmup):
         eng.run(SEED, base + w * B, B)
     eng.enable_timing(True)
     if dist:
-        dist.barrier()
         import torch
+        dist.barrier()
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         eng.run(SEED, base + (args.warmup + k) * B, B, counts)
     if dist:
         import torch
-        ct = torch.from_numpy(counts).cuda()
-        dist.all_reduce(ct)                 # the one exchange: BER counters (RCCL)
         torch.cuda.synchronize()
-        counts = ct.cpu().numpy()
+        dist.barrier()
     el = time.perf_counter() - t0
     if dist:
         import torch
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else "cpu"
+        ct = torch.from_numpy(counts).to(dev)
+        dist.all_reduce(ct)                 # the one exchange: BER counters (RCCL)
+        counts = ct.cpu().numpy()
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_reps = B * args.steps * world
     value = total_reps / el
 
-    # roofline of the dominant kernel (MMSE contraction), HIP events on the engine stream
+    # roofline of the dominant kernel (the MMSE contraction, timed as k_wcontract
+    # with HIP events on the engine's stream)
     launches, wc_ms = eng.kernel_time("k_wcontract")
-    cmac_per_rep, w_bytes = eng.work_model(0)
-    flops = cmac_per_rep * 8.0 * B * args.steps          # this rank's contraction flops in the timed region
+    flops = 0.0
+    executed = 0.0
+    paths = []
+    for sid in range(len(schemes)):
+        cmac_per_rep, _ = eng.work_model(sid)
+        f = cmac_per_rep * 8.0 * B * args.steps
+        p = eng.path_info(sid)
+        paths.append(sorted(p))
+        flops += f
+        # matrix-core flops actually executed per counted flop: 3 real MFMAs per
+        # complex product in the 3M form, 4 in the 4M form
+        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) else 1.0)
     achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
-    traffic = latest_pmc_traffic()
-    bits = eng.bits_per_rep(0)
-    ber = counts[0, :, 0, :, :] / float(bits[0] * total_reps)
+    exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
+    peak_meas = eng.fp64_mfma_peak()
+    traffic, traffic_src = stored_traffic("k_wcontract", args.config)
     kernels = {}
     for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
         kernels[k] = {"launches": n, "ms": round(ms, 3)}
+    ber = {}
+    for sid, name in enumerate(schemes):
+        bits = eng.bits_per_rep(sid)
+        b = counts[sid, :, 0, :, :] / float(bits[0] * total_reps)
+        ber[name] = {"snr_db_last": float(S.snr_db[-1]), "mmse_ic4": float(b[0, -1, -1]),
+                     "perfect_ic4": float(b[1, -1, -1]), "mmse_onetap": float(b[0, -1, 0]),
+                     "perfect_onetap": float(b[1, -1, 0])}
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
-        return
+        return 0
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = run_cpu_baseline(args.cpu_seconds)
+            cpu = run_cpu_baseline(args.cpu_seconds, args.config)
         except Exception:
             cpu = None
+    L = S.L
     line = {
-        "metric": METRIC,
+        "metric": METRIC if args.config == "c2" else
+        "Monte-Carlo channel realisations/sec at %dsc (%s)" % (L, args.config.upper()),
         "value": value,
         "unit": "realisations/s",
         "n_gpus": world,
@@ -189,26 +323,33 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (Philox4x32-10 streams, include/dsce.h)",
-        "config": {"workload": "C2: OFDM 24sc x 14sym, N=540, Jakes 500 km/h VehA, 256-QAM, 16 pilots, "
-                               "7 SNR (10:5:40 dB) x (one-tap + 4 IC) x (MMSE + perfect CSI)",
-                   "reps_per_step_per_gpu": B, "engine_batch": args.batch, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "kernel": "k_wpair3<24,4,fused> (pair-tile MMSE contraction, 3M, with the "
-                               "next stage's diag(D_hat) + detection in its epilogue; timed as k_wcontract)",
+        "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
+                   "parallelism": "dp%d" % world, "options": options},
+        "roofline": {"bound": "mfma",
+                     "kernel": "k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
+                               "diag(D_hat) + detection in its epilogue)",
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
-                     "traffic": traffic, "launches": launches,
-                     "avg_launch_ms": wc_ms / launches if launches else None,
-                     "flops_per_launch": flops / launches if launches else None},
+                     "peak_measured": peak_meas,
+                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas else None,
+                     "mfma_busy": (exec_tf / peak_meas) if exec_tf and peak_meas else None,
+                     "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
+                     "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
+                     "flops_per_launch": flops / launches if launches else None,
+                     "work_model": "support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
+                                   "fused diag(D_hat)), 8 real flops per CMAC; mfma_busy = executed matrix-core "
+                                   "flops (6 of 8 in the 3M form) / measured peak",
+                     "paths": paths},
         "cpu_baseline": cpu,
         "setup_s": setup_s,
         "kernels_ms": kernels,
-        "ber_40dB": {"mmse_ic4": float(ber[0, -1, -1]), "perfect_ic4": float(ber[1, -1, -1]),
-                     "mmse_onetap": float(ber[0, -1, 0]), "perfect_onetap": float(ber[1, -1, 0])},
+        "ber_last_snr": ber,
     }
     print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -73,9 +73,17 @@ static HostBand band_geometry(int nrow, RangeFn range, int kscale, int rb = DSCE
     return b;
 }
 
-struct DevBand {
-    Band k{};
-};
+// CMACs of one contraction over a packed W band (rows x (column, pilot) entries)
+// and how many of them are (r, r) pairs, which the band stores as zeros.
+static void band_work(const HostBand& b, int NP, long long& total, long long& diag) {
+    total = diag = 0;
+    for (size_t blk = 0; blk < b.row0.size(); ++blk) {
+        const int clo = b.klo[blk] / NP, chi = b.khi[blk] / NP;
+        total += (long long)b.nrows[blk] * (b.khi[blk] - b.klo[blk]);
+        for (int r = b.row0[blk]; r < b.row0[blk] + b.nrows[blk]; ++r)
+            if (r >= clo && r < chi) diag += NP;
+    }
+}
 
 struct Scheme {
     dsce_scheme_desc d{};
@@ -95,8 +103,9 @@ struct Scheme {
     double2* Wpil = nullptr;        // fused MMSE stage operands (null: not eligible)
     double2* WdA = nullptr;
     int* pil_c0 = nullptr;
-    int w3x4 = 0;
     long long wp_elems = 0, wp_exec = 0;
+    long long w_diag = 0;           // (r, r) pairs inside the band (stored as zeros: diag(D_hat) comes from Wd)
+    unsigned path = 0;              // PATH_* bits of the last dsce_run / trace (dsce_path_info)
     PairBand Pb{};
     std::vector<double2> R_hP, R_est, R_noI;
     bool mmse_ready = false;
@@ -128,7 +137,7 @@ struct dsce_ctx {
     double* d_pn = nullptr;
     std::vector<std::unique_ptr<Scheme>> schemes;
     int batch = 8192;
-    bool streams2 = false;                // DSCE_STREAMS=2: perfect-CSI IC chain on stream2
+    Opts op{};                            // kernel selection (dsce_set_option)
     McBuffers buf{};
     size_t buf_key[6] = {0, 0, 0, 0, 0, 0};
     std::vector<void*> buf_allocs;
@@ -412,9 +421,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
         },
         NP, DSCE_WRB, true);
     s.w_elems = s.wband.elems;
-    s.w_struct = 0;
-    for (size_t blk = 0; blk < s.wband.row0.size(); ++blk)
-        s.w_struct += (long long)s.wband.nrows[blk] * (s.wband.khi[blk] - s.wband.klo[blk]);
+    band_work(s.wband, NP, s.w_struct, s.w_diag);
     // precoder CSR and its conjugate transpose
     std::vector<int> pptr(LK + 1, 0), pcol;
     std::vector<double2> pval;
@@ -529,8 +536,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
 // estimator spans |dk| <= 7 symbols instead of the structural 15.
 // ---------------------------------------------------------------------------
 void trim_w_band(dsce_ctx* c, Scheme& s, std::vector<void*>& tmp) {
-    const char* env = getenv("DSCE_WTRIM");      // "0": keep the structural band (A/B, tests)
-    if (env && env[0] == '0') return;
+    if (!c->op.wtrim) return;                    // Opts::wtrim = 0 keeps the structural band
     hipStream_t st = c->stream;
     const int NP = s.d.n_pilots, nsl = 2 * c->nsnr, nblk = (int)s.wband.row0.size();
     int* dlohi;
@@ -573,8 +579,7 @@ void trim_w_band(dsce_ctx* c, Scheme& s, std::vector<void*>& tmp) {
     s.W = W2;
     s.wband = nb;
     s.w_elems = off;
-    s.w_struct = 0;
-    for (int b = 0; b < nblk; ++b) s.w_struct += (long long)nb.nrows[b] * (nb.khi[b] - nb.klo[b]);
+    band_work(nb, NP, s.w_struct, s.w_diag);
     s.Wb = upload_band(c, nb, false);
 }
 
@@ -615,15 +620,9 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
     s.wp_exec = exec;
     const int nsl = 2 * c->nsnr;
     s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
+    // W's 3M planes, two k-steps per 16-byte lane load
     s.Wp3 = dalloc<double>(c, (size_t)nsl * 3 * s.wp_elems);
-    // W's 3M planes two k-steps per 16-byte lane load (half the load
-    // instructions of the contraction's tile loop); DSCE_W3_X4=0 at build time:
-    // one double per lane and plane
-    {
-        const char* e = getenv("DSCE_W3_X4");
-        s.w3x4 = (s.Pb.nks % 2 == 0 && !(e && e[0] == '0')) ? 1 : 0;
-    }
-    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3, s.w3x4);
+    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3);
     // fused MMSE stage: block-diagonal W (every block's columns are its own 24
     // rows, OFDM), row-local precoder, select-mode detection, NP = 16
     bool fuse = rbp == 24 && NP == 16 && s.k.p_diag && !s.d.despread;
@@ -801,11 +800,10 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
 // ---------------------------------------------------------------------------
 // Monte-Carlo batches
 // ---------------------------------------------------------------------------
-// SNR points processed together by the receiver kernels (DSCE_SNR_CHUNK, default
+// SNR points processed together by the receiver kernels (Opts::snr_chunk, default
 // all): smaller chunks shrink the per-unit working set of a stage.
 int snr_chunk(dsce_ctx* c) {
-    const char* e = getenv("DSCE_SNR_CHUNK");
-    int k = e ? atoi(e) : 0;
+    int k = c->op.snr_chunk;
     if (k <= 0 || k > c->nsnr) k = c->nsnr;
     return k;
 }
@@ -851,12 +849,15 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.qp = dalloc<uint16_t>(c, ND * U, L);
 }
 
+// One traced unit (dsce_trace_unit_ex): realisation lane `lane` of the batch at
+// SNR index `snr` of scheme `scheme`.  Quantities that sit in a per-unit buffer
+// anyway (y, h, hP, and y_est / y_perf of the unfused paths) are copied from
+// it; the rest is written by the kernels that form them through TraceK.
 struct Trace {
     int scheme, snr, lane;
-    double* y;
-    double* hp;
-    double* hest;
-    double* h;
+    const dsce_trace* out;
+    TraceK* dev = nullptr;          // device copy of `k`
+    TraceK k{};
 };
 
 void copy_col(dsce_ctx* c, double* dst, const double2* src, int rows, int stride, int lane) {
@@ -866,24 +867,19 @@ void copy_col(dsce_ctx* c, double* dst, const double2* src, int rows, int stride
 
 int var_of_stage(int stage, int niter) { return (stage == 0 || stage <= niter / 2) ? 0 : 1; }
 
-void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, const Trace* tr) {
+void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
     McBuffers& b = c->buf;
+    const Opts& op = c->op;
     b.R = R;
+    b.tr = nullptr;
     {
         Timed t(c, "k_jakes");
-        launch_jakes(c->stream, c->ch, seed, rep0, R, b.ir);
+        launch_jakes(c->stream, op, c->ch, seed, rep0, R, b.ir);
     }
-    (void)valid;
     const int chunk = snr_chunk(c);
-    {
-        // DSCE_STREAMS=2 overlaps the perfect-CSI chain with the MMSE chain on a
-        // second stream: measured +0.3..1.2 % and it stretches both kernels'
-        // durations, so the default is one stream
-        const char* e = getenv("DSCE_STREAMS");
-        c->streams2 = e && atoi(e) == 2;
-    }
     for (size_t si = 0; si < c->schemes.size(); ++si) {
         Scheme& s = *c->schemes[si];
+        s.path = 0;
         MmseK mm{};
         mm.W = s.W;
         mm.Wd = s.Wd;
@@ -897,37 +893,41 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
         mm.Wpil = s.Wpil;
         mm.WdA = s.WdA;
         mm.pil_c0 = s.pil_c0;
-        mm.w3x4 = s.w3x4;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
         }
-        const bool pfuse = perfect_fusable(s.k);
+        const bool pfuse = perfect_fusable(op, s.k);
         for (int s0 = 0; s0 < c->nsnr; s0 += chunk) {
             b.snr0 = s0;
             b.U = R * std::min(chunk, c->nsnr - s0);
             const bool tracing = tr && tr->scheme == (int)si && tr->snr >= s0 && tr->snr < s0 + chunk;
             const int tunit = tracing ? (tr->snr - s0) * R + tr->lane : 0;
+            if (tracing) {
+                tr->k.unit = tunit;
+                DSCE_HIP_CHECK(hipMemcpyAsync(tr->dev, &tr->k, sizeof(TraceK), hipMemcpyHostToDevice, c->stream));
+            }
+            b.tr = tracing ? tr->dev : nullptr;
+            const dsce_trace* to = tracing ? tr->out : nullptr;
+            const int LK = s.LK, NP = s.d.n_pilots;
             {
                 Timed t(c, "rx_front");
-                launch_rx_front(c->stream, s.k, c->ch, c->d_pn, seed, rep0, b);
+                s.path |= launch_rx_front(c->stream, op, s.k, c->ch, c->d_pn, seed, rep0, b);
             }
-            if (tracing) {
-                copy_col(c, tr->y, b.y, s.LK, b.U, tunit);
-                copy_col(c, tr->h, b.h, s.LK, R, tr->lane);
-            }
+            if (to && to->y) copy_col(c, to->y, b.y, LK, b.U, tunit);
+            if (to && to->h_perfect) copy_col(c, to->h_perfect, b.h, LK, R, tr->lane);
             // With the perfect-CSI branch fused into perfect_ic, the IC iterations
-            // are two independent chains after stage 0: MMSE (k_wcontract ->
-            // stage, MFMA-bound) on the main stream and perfect CSI (perfect_ic,
-            // HBM-bound) on stream2, overlapping; joined before the next chunk.
-            const bool two = pfuse && c->streams2;
+            // are two independent chains after stage 0: MMSE (contraction ->
+            // stage, MFMA-bound) on the main stream and perfect CSI on stream2
+            // (Opts::streams = 2), joined before the next chunk.
+            const bool two = pfuse && op.streams == 2 && !tracing;
             // pic_ok schemes (OFDM): the whole perfect-CSI chain is one kernel
-            // (k_pic_chain, u in registers across the iterations)
-            const bool chain = pfuse && perfect_chain_ok(s.k, c->ch, b);
+            // (k_pic_mfma / k_pic_chain, u in registers across the iterations)
+            const bool chain = pfuse && perfect_chain_ok(op, s.k, c->ch, b);
             // block-diagonal W + row-local P (OFDM): the MMSE stage of every IC
             // iteration rides in the contraction's epilogue (k_pilot_pre +
             // k_wpair3<..., true>); hP alternates between hp and hp2
-            const bool mfuse = pfuse && !tracing && mmse_fused_ok(s.k, mm, b);
+            const bool mfuse = pfuse && mmse_fused_ok(op, s.k, mm, b);
             double2* hp_prev = b.hp;
             double2* hp_cur = b.hp2;
             for (int it = 0; it <= c->niter; ++it) {
@@ -940,13 +940,13 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
                     if (chain) {
                         Timed t(c, "perfect_ic", ps);
                         PerfectDetectArgs pd{c->d_counters, (int)si, 1, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
-                        launch_perfect_chain(ps, s.k, c->ch, b, &pd, c->niter);
+                        s.path |= launch_perfect_chain(ps, op, s.k, c->ch, b, &pd, c->niter);
                     } else {
                         for (int jt = 1; jt <= c->niter; ++jt) {
                             Timed t(c, "perfect_ic", ps);
                             PerfectDetectArgs pd{c->d_counters, (int)si, jt, c->niter + 1, c->nsnr, jt == c->niter,
                                                  s.k.slI, s.k.slQ};
-                            launch_perfect_ic(ps, s.k, c->ch, b, &pd);
+                            s.path |= launch_perfect_ic(ps, op, s.k, c->ch, b, &pd);
                         }
                     }
                     if (two) DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
@@ -956,44 +956,47 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int valid, cons
                         Timed t(c, "k_pilot_pre");
                         launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur);
                     }
+                    if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, hp_cur, NP, b.U, tunit);
                     {
                         // the contraction with the stage in its epilogue (bench's roofline kernel)
                         Timed t(c, "k_wcontract");
-                        launch_mmse_fused(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), var_of_stage(it, c->niter),
-                                          it, c->niter, it == c->niter, b, hp_prev, hp_cur, c->d_counters, (int)si);
+                        s.path |= launch_mmse_fused(c->stream, op, s.k, mm, var_of_stage(it - 1, c->niter),
+                                                    var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
+                                                    hp_prev, hp_cur, c->d_counters, (int)si);
                     }
                     std::swap(hp_prev, hp_cur);
                     if (!two && !chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
                                              s.k.slI, s.k.slQ};
-                        launch_perfect_ic(c->stream, s.k, c->ch, b, pfuse ? &pd : nullptr);
+                        s.path |= launch_perfect_ic(c->stream, op, s.k, c->ch, b, pfuse ? &pd : nullptr);
                     }
                     continue;
                 }
                 if (it > 0) {
                     {
                         Timed t(c, "k_wcontract");
-                        launch_wcontract(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b);
+                        s.path |= launch_wcontract(c->stream, op, s.k, mm, var_of_stage(it - 1, c->niter), b);
                     }
+                    if (to && to->yest_stages) copy_col(c, to->yest_stages + (size_t)2 * it * LK, b.yest, LK, b.U, tunit);
                     if (!two && !chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
                                              s.k.slI, s.k.slQ};
-                        launch_perfect_ic(c->stream, s.k, c->ch, b, pfuse ? &pd : nullptr);
+                        s.path |= launch_perfect_ic(c->stream, op, s.k, c->ch, b, pfuse ? &pd : nullptr);
+                        if (to && to->yperf_stages && !pfuse)
+                            copy_col(c, to->yperf_stages + (size_t)2 * it * LK, b.yperf, LK, b.U, tunit);
                     }
                 }
                 {
                     Timed t(c, "k_stage");
-                    launch_stage(c->stream, s.k, mm, it, var_of_stage(it, c->niter), c->niter, it == c->niter, b,
-                                 c->d_counters, (int)si, tracing, !(pfuse && it > 0));
+                    s.path |= launch_stage(c->stream, op, s.k, mm, it, var_of_stage(it, c->niter), c->niter,
+                                           it == c->niter, b, c->d_counters, (int)si, !(pfuse && it > 0));
                 }
-                if (tracing) {
-                    copy_col(c, tr->hp + (size_t)2 * it * s.d.n_pilots, b.hp, s.d.n_pilots, b.U, tunit);
-                    copy_col(c, tr->hest + (size_t)2 * it * s.LK, b.hest, s.LK, b.U, tunit);
-                }
+                if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, b.hp, NP, b.U, tunit);
             }
             if (two && c->niter > 0) DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+            b.tr = nullptr;
         }
     }
     DSCE_HIP_CHECK(hipGetLastError());
@@ -1262,7 +1265,7 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
         const int R = (int)std::min<uint64_t>((uint64_t)ctx->batch, left);
         ensure_buffers(ctx, R <= ctx->batch ? ctx->batch : R);
         set_mse_buffers(ctx);
-        run_batch(ctx, seed, first_rep + done, R, R, nullptr);
+        run_batch(ctx, seed, first_rep + done, R, nullptr);
         done += (uint64_t)R;
     }
     std::vector<unsigned long long> h(ctx->counters_n);
@@ -1294,7 +1297,7 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     // position of the kernels' realisation-to-wave mapping
     const int N = ctx->ch.N, R = 64, lane = (int)(rep % 8);
     double2* ir = dalloc<double2>(ctx, (size_t)ctx->ch.ntap * N * R);
-    launch_jakes(ctx->stream, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
+    launch_jakes(ctx->stream, ctx->op, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
     std::vector<double2> h((size_t)ctx->ch.ntap * N * R);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ir, h.size() * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -1415,19 +1418,92 @@ int dsce_get_W(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, double* w_out)
     API_END
 }
 
-int dsce_trace_unit(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, int32_t k, double* y, double* hp,
-                    double* hest, double* h) {
+int dsce_trace_unit_ex(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, int32_t k, const dsce_trace* out) {
     API_BEGIN
     check_ctx(ctx);
-    get_scheme(ctx, id);
-    if (k < 0 || k >= ctx->nsnr || !y || !hp || !hest || !h) throw ApiError(DSCE_EINVAL, "bad trace arguments");
+    Scheme& s = get_scheme(ctx, id);
+    if (k < 0 || k >= ctx->nsnr || !out) throw ApiError(DSCE_EINVAL, "bad trace arguments");
     prepare_run(ctx);
     ensure_buffers(ctx, ctx->batch);
-    Trace tr{id, k, 0, y, hp, hest, h};
-    run_batch(ctx, seed, rep, 64, 64, &tr);
-    DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    if (ctx->timing) collect_timing(ctx);
+    set_mse_buffers(ctx);
+    const int LK = s.LK, ND = s.d.n_data, ns = ctx->niter + 1;
+    std::vector<void*> tmp;
+    auto talloc = [&](size_t bytes) {
+        void* p;
+        DSCE_HIP_CHECK(hipMalloc(&p, bytes));
+        tmp.push_back(p);
+        return p;
+    };
+    try {
+        Trace tr{id, k, 0, out};
+        tr.k.LK = LK;
+        tr.k.ND = ND;
+        tr.k.yest = (double2*)talloc((size_t)ns * LK * sizeof(double2));
+        tr.k.yperf = (double2*)talloc((size_t)ns * LK * sizeof(double2));
+        tr.k.hest = (double2*)talloc((size_t)ns * LK * sizeof(double2));
+        tr.k.dec_e = (int*)talloc((size_t)ns * ND * sizeof(int));
+        tr.k.dec_p = (int*)talloc((size_t)ns * ND * sizeof(int));
+        tr.dev = (TraceK*)talloc(sizeof(TraceK));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yest, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yperf, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.hest, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.dec_e, 0xff, (size_t)ns * ND * sizeof(int), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.dec_p, 0xff, (size_t)ns * ND * sizeof(int), ctx->stream));
+        // the unit sits at lane 0 of a 64-realisation batch starting at rep
+        run_batch(ctx, seed, rep, 64, &tr);
+        std::vector<double2> ye((size_t)ns * LK), yp((size_t)ns * LK);
+        DSCE_HIP_CHECK(hipMemcpyAsync(ye.data(), tr.k.yest, ye.size() * sizeof(double2), hipMemcpyDeviceToHost,
+                                      ctx->stream));
+        DSCE_HIP_CHECK(hipMemcpyAsync(yp.data(), tr.k.yperf, yp.size() * sizeof(double2), hipMemcpyDeviceToHost,
+                                      ctx->stream));
+        if (out->hest_stages)
+            DSCE_HIP_CHECK(hipMemcpyAsync(out->hest_stages, tr.k.hest, (size_t)ns * LK * sizeof(double2),
+                                          hipMemcpyDeviceToHost, ctx->stream));
+        if (out->dec_est)
+            DSCE_HIP_CHECK(hipMemcpyAsync(out->dec_est, tr.k.dec_e, (size_t)ns * ND * sizeof(int),
+                                          hipMemcpyDeviceToHost, ctx->stream));
+        if (out->dec_perf)
+            DSCE_HIP_CHECK(hipMemcpyAsync(out->dec_perf, tr.k.dec_p, (size_t)ns * ND * sizeof(int),
+                                          hipMemcpyDeviceToHost, ctx->stream));
+        DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        // stage 0 of y_est / y_perf is y itself; later stages come from the kernels
+        // (fused paths) unless the host already copied them from y_est / y_perf
+        auto merge = [&](double* dst, const std::vector<double2>& dev, bool copied_unfused) {
+            if (!dst) return;
+            for (int st = 1; st < ns; ++st)
+                for (int r = 0; r < LK; ++r) {
+                    const double2 v = dev[(size_t)st * LK + r];
+                    double* d = dst + 2 * ((size_t)st * LK + r);
+                    if (!copied_unfused || v.x != 0.0 || v.y != 0.0) {
+                        d[0] = v.x;
+                        d[1] = v.y;
+                    }
+                }
+        };
+        merge(out->yest_stages, ye, !(s.path & PATH_WPAIR3_FUSED));
+        merge(out->yperf_stages, yp, true);
+        if (out->y) {
+            for (double* d : {out->yest_stages, out->yperf_stages})
+                if (d) memcpy(d, out->y, (size_t)LK * 2 * sizeof(double));
+        }
+        if (ctx->timing) collect_timing(ctx);
+    } catch (...) {
+        for (void* p : tmp) (void)hipFree(p);
+        throw;
+    }
+    for (void* p : tmp) DSCE_HIP_CHECK(hipFree(p));
     API_END
+}
+
+int dsce_trace_unit(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, int32_t k, double* y, double* hp,
+                    double* hest, double* h) {
+    if (!y || !hp || !hest || !h) return api_fail(ctx, DSCE_EINVAL, "bad trace arguments");
+    dsce_trace t{};
+    t.y = y;
+    t.hp_stages = hp;
+    t.hest_stages = hest;
+    t.h_perfect = h;
+    return dsce_trace_unit_ex(ctx, id, seed, rep, k, &t);
 }
 
 int dsce_mmse_onetap(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, const double* hp_ls, int32_t n,
@@ -1533,12 +1609,106 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
     API_BEGIN
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
-    // contraction CMACs; with the fused MMSE stage (OFDM) the same kernel also
-    // forms diag(D_hat) = Wd hP of the next stage (LK x NP CMACs per unit)
-    const char* fe = getenv("DSCE_FUSE_STAGE");
-    const double fused = s.Wpil && !(fe && fe[0] == '0') ? (double)s.LK * s.d.n_pilots : 0.0;
-    if (cmac) *cmac = ((double)s.w_struct + fused) * ctx->nsnr * ctx->niter;
+    // contraction CMACs over the band's off-diagonal pairs (the (r, r) pairs are
+    // stored as zeros: D_hat - diag(D_hat) of script:482-484); with the fused MMSE
+    // stage (OFDM) the same kernel also forms diag(D_hat) = Wd hP of the next
+    // stage (LK x NP CMACs per unit)
+    const double fused = (s.path & PATH_WPAIR3_FUSED) ? (double)s.LK * s.d.n_pilots : 0.0;
+    if (cmac) *cmac = ((double)(s.w_struct - s.w_diag) + fused) * ctx->nsnr * ctx->niter;
     if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
+    API_END
+}
+
+int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!tflops) throw ApiError(DSCE_EINVAL, "null output");
+    int cus = 0;
+    DSCE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    const int blocks = cus * 8, iters = 4096;          // 8 blocks x 4 waves per CU: 8 waves per SIMD
+    double* out = dalloc<double>(ctx, (size_t)blocks * 256);
+    hipEvent_t e0 = get_event(ctx), e1 = get_event(ctx);
+    launch_mfma_f64_peak(ctx->stream, blocks, iters, out);     // warm-up (clocks up)
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+        DSCE_HIP_CHECK(hipEventRecord(e0, ctx->stream));
+        launch_mfma_f64_peak(ctx->stream, blocks, iters, out);
+        DSCE_HIP_CHECK(hipEventRecord(e1, ctx->stream));
+        DSCE_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        DSCE_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+    }
+    DSCE_HIP_CHECK(hipGetLastError());
+    ctx->event_pool.push_back(e0);
+    ctx->event_pool.push_back(e1);
+    free_alloc(ctx, out);
+    *tflops = (double)blocks * 4 * iters * PEAK_MFMA_PER_ITER * 2048.0 / (best * 1e-3) / 1e12;
+    API_END
+}
+
+// Kernel-selection options (Opts); the defaults are the measured-best path.
+#define DSCE_OPTIONS(X)                                                                                  \
+    X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu)
+
+int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!name) throw ApiError(DSCE_EINVAL, "null option name");
+    const std::string n(name);
+    int* slot = nullptr;
+#define X(f) if (n == #f) slot = &ctx->op.f;
+    DSCE_OPTIONS(X)
+#undef X
+    if (!slot) throw ApiError(DSCE_EINVAL, "unknown option '" + n + "'");
+    if (n == "stage_rb" && value != 4 && value != 8 && value != 16) throw ApiError(DSCE_EINVAL, "stage_rb: 4 | 8 | 16");
+    if (n == "jakes_rpw" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "jakes_rpw: 1 | 2");
+    if (n == "pic_chain" && (value < 0 || value > 2)) throw ApiError(DSCE_EINVAL, "pic_chain: 0 | 1 | 2");
+    if (n == "streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "streams: 1 | 2");
+    if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
+    *slot = (int)value;
+    API_END
+}
+
+int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value) {
+    API_BEGIN
+    if (!ctx || !name || !value) throw ApiError(DSCE_EINVAL, "null argument");
+    const std::string n(name);
+    const int* slot = nullptr;
+#define X(f) if (n == #f) slot = &ctx->op.f;
+    DSCE_OPTIONS(X)
+#undef X
+    if (!slot) throw ApiError(DSCE_EINVAL, "unknown option '" + n + "'");
+    *value = *slot;
+    API_END
+}
+#undef DSCE_OPTIONS
+
+int dsce_path_info(dsce_ctx* ctx, int32_t id, uint32_t* flags) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!flags) throw ApiError(DSCE_EINVAL, "null output");
+    *flags = s.path;
+    API_END
+}
+
+int dsce_scheme_dims(dsce_ctx* ctx, int32_t id, dsce_dims* dims) {
+    API_BEGIN
+    if (!ctx) throw ApiError(DSCE_EINVAL, "null context");
+    Scheme& s = get_scheme(ctx, id);
+    if (!dims) throw ApiError(DSCE_EINVAL, "null output");
+    dims->n_samples = s.N;
+    dims->n_taps = (int32_t)ctx->pdp_norm.size();
+    dims->lk = s.LK;
+    dims->n_pilots = s.d.n_pilots;
+    dims->n_data = s.d.n_data;
+    dims->n_tx_symbols = s.d.n_tx_symbols;
+    dims->n_schemes = (int32_t)ctx->schemes.size();
+    dims->n_snr = ctx->nsnr;
+    dims->n_iter = ctx->niter;
+    dims->n_counters = (int64_t)ctx->schemes.size() * 4 * ctx->nsnr * (ctx->niter + 1);
     API_END
 }
 

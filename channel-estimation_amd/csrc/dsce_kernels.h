@@ -5,6 +5,53 @@
 
 namespace dsce {
 
+// Kernel-selection options of a context (dsce_set_option; defaults = the
+// measured-best path).  Read by the launchers; nothing reads the environment.
+struct Opts {
+    int xcd = 1;              // XCD-aware work order (each XCD walks a contiguous range)
+    int fuse_stage = 1;       // MMSE stage of the IC iterations fused into the contraction
+    int wpair_3m = -1;        // 3M complex products in k_wpair3: -1 auto, 0 off (4 MFMAs), 1 on
+    int wda_3m = 1;           // fused epilogue's diag(D_hat) in 3M form
+    int pic_chain = 2;        // perfect-CSI IC: 0 per-iteration passes, 1 VALU chain, 2 MFMA chain
+    int pfuse = 1;            // perfect-CSI detection fused into the second banded pass
+    int stage_split = 0;      // 1: 3-kernel stage (k_ls_hest, k_detect, k_precode) for every scheme
+    int stage_rb = 8;         // rows per wave of k_stage_fused: 4 | 8 | 16
+    int noise_fuse = 1;       // AWGN drawn inside the Q^H pass (disjoint Q^H blocks)
+    int snr_chunk = 0;        // SNR points per receiver chunk (0: all)
+    int streams = 1;          // 2: perfect-CSI chain on a second stream
+    int jakes_rpw = 2;        // realisations per Jakes wave (1 | 2)
+    int wtrim = 1;            // trim W to its non-zero column extent (read by dsce_build_mmse)
+    int wcontract_valu = 0;   // 1: VALU contraction instead of the MFMA pair tiles
+};
+
+// Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
+// (dsce_path_info; bit values mirrored in include/dsce.h DSCE_PATH_*).
+enum : unsigned {
+    PATH_WPAIR3_FUSED = 1u << 0,   // k_pilot_pre + k_wpair3<.., FUSE> (stage in the contraction epilogue)
+    PATH_WPAIR3 = 1u << 1,         // k_wpair3 (3M, unfused)
+    PATH_WPAIR4M = 1u << 2,        // k_wpair (4 real MFMAs per complex product)
+    PATH_WCONTRACT_VALU = 1u << 3, // k_wcontract_valu
+    PATH_PIC_MFMA = 1u << 4,       // k_pic_mfma (perfect-CSI chain on the matrix cores)
+    PATH_PIC_CHAIN = 1u << 5,      // k_pic_chain (VALU chain)
+    PATH_PIC_PASSES = 1u << 6,     // G u pass + Q^H H pass per iteration
+    PATH_STAGE_FUSED = 1u << 7,    // k_ls + k_stage_fused
+    PATH_STAGE_SPLIT = 1u << 8,    // k_ls_hest + k_detect + k_precode
+    PATH_NOISE_FUSED = 1u << 9,    // noise drawn inside the Q^H pass
+};
+
+// Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
+// of these quantities for unit `unit` of the traced scheme writes it here.
+// Device arrays, stage-major: [stage][LK] / [stage][ND].
+struct TraceK {
+    int unit;
+    int LK, ND;
+    double2* yest;     // y_est of stage s (the MMSE IC input y - (D_hat - diag) v), s >= 1
+    double2* yperf;    // y_perf of stage s (perfect-CSI IC), s >= 1
+    double2* hest;     // diag(D_hat) of stage s
+    int* dec_e;        // detected symbol index per data symbol, MMSE branch
+    int* dec_p;        // perfect-CSI branch
+};
+
 struct McBuffers {
     int R;            // repetitions per batch (multiple of 64)
     int nsnr;
@@ -35,6 +82,7 @@ struct McBuffers {
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
+    const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)
 };
 
 struct MmseK {
@@ -51,42 +99,44 @@ struct MmseK {
     const double2* Wpil;  // [var][snr][NP pilots][24 columns][NP]
     const double2* WdA;   // [var][snr][blk][2][NP/4][64] diag(W) rows, MFMA A layout
     const int* pil_c0;    // NP: first column of each pilot row's block
-    int w3x4;             // Wp3 in the 16-byte layout (two k-steps per lane and plane)
 };
 
-// Monte-Carlo pipeline
-void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir);
+// Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
+void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
+                  double2* ir);
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
                uint64_t rep0, McBuffers& b);
-void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
-                     uint64_t rep0, McBuffers& b);
-void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace, bool perfect);
+unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
+                         uint64_t seed, uint64_t rep0, McBuffers& b);
+unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
+                      int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
+                      bool perfect);
 // true when launch_stage uses the fused select-mode pass and the precoder is
 // row-local, so the perfect-CSI branch of IC iterations can ride on perfect_ic
-bool perfect_fusable(const SchemeK& sk);
-void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
+bool perfect_fusable(const Opts& op, const SchemeK& sk);
+unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b);
 // Fused MMSE stage of IC iteration `stage` (block-diagonal W, row-local P):
 // k_pilot_pre (pilot rows + LS into hp_new) then the contraction with the
 // stage's detection in its epilogue (no y_est, no separate stage kernel).
-bool mmse_fused_ok(const SchemeK& sk, const MmseK& mm, const McBuffers& b);
+bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b);
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
                       const double2* hp_prev, double2* hp_new);
-void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, int var_cur, int stage,
-                       int n_iter, bool last, McBuffers& b, const double2* hp_prev, double2* hp_new,
-                       unsigned long long* counters, int scheme_index);
+unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
+                           int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
+                           double2* hp_new, unsigned long long* counters, int scheme_index);
 // Perfect-CSI detection fused into the perfect IC pass (select mode, row-local P)
 struct PerfectDetectArgs {
     unsigned long long* counters;
     int scheme, stage, nstage, nsnr, last;
     double sI, sQ;   // 1 / slicer step (I, Q)
 };
-void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd);
+unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                           const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
-// registers (pic_ok schemes with 1-3 taps); perfect_chain_ok tells when it applies.
-bool perfect_chain_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
-void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                          const PerfectDetectArgs* pd, int niter);
+// registers (pic_ok schemes); perfect_chain_ok tells when it applies.
+bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
+unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                              const PerfectDetectArgs* pd, int niter);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)
@@ -117,12 +167,16 @@ struct TxDesc {
     int kind, L, K, N, fft, ifb, ts, cp, zg, proto;
     double norm, phase0, rx_scale;
 };
+// FP64 matrix-core peak microbenchmark: blocks x 4 waves, each `iters` x 8
+// independent v_mfma_f64_16x16x4_f64 (2048 flops each)
+static constexpr int PEAK_MFMA_PER_ITER = 8;
+void launch_mfma_f64_peak(hipStream_t s, int blocks, int iters, double* out);
 void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q);
 void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const double2* w, long long w_elems,
                        const double2* wd, int nslices, const int* pil_blk, const int* pilot_pos, int ncol,
                        double2* wpil, double2* wda);
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices, double* w3, int w3x4);
+                 double2* wp, long long wp_elems, int nslices, double* w3);
 void setup_w_extent(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, int nslices, int* lohi);
 void setup_w(hipStream_t s, const SetupArgs& a, const Band& Wb, long long w_elems, const double2* rd,
              const double2* rinv /* NP x NP */, double2* w /* packed */, double2* wd /* LK x NP */);

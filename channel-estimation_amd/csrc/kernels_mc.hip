@@ -378,16 +378,8 @@ __global__ void __launch_bounds__(64) k_discrete(ChannelK ch, uint64_t seed, uin
     }
 }
 
-// DSCE_JAKES_RPW=1 keeps one realisation per wave (A/B switch)
-static bool jakes_rpw2() {
-    static const bool on = [] {
-        const char* e = getenv("DSCE_JAKES_RPW");
-        return !(e && atoi(e) == 1);
-    }();
-    return on;
-}
-
-void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
+                  double2* ir) {
     if (ch.fD == 0.0) {
         hipLaunchKernelGGL(k_static, dim3(R / WAVE, (ch.N + 63) / 64, ch.ntap), dim3(WAVE), 0, s, ch, seed, rep0, R, ir);
         return;
@@ -402,7 +394,7 @@ void launch_jakes(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep
     // then take 64 P bytes per realisation, 51 KB per block at P = 200
     const int jch2 = (ch.N + WAVE / 2 - 1) / (WAVE / 2);
     if (jch2 >= 9 && jch2 <= 20 && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024 &&
-        jakes_rpw2()) {
+        op.jakes_rpw == 2) {
         switch (jch2) {
             case 9: launch_jakes_t<9, 2>(s, ch, seed, rep0, R, ir); return;
             case 10: launch_jakes_t<10, 2>(s, ch, seed, rep0, R, ir); return;
@@ -455,10 +447,17 @@ struct BandOrder {
     int xcd;       // 1: SNR-fastest XCD-aware order
 };
 
+// Hardware dispatch sends block b to XCD b % 8.  Remap b so that each XCD walks
+// one contiguous range of [0, n) — for any n (XCDs x < n % 8 take one block more).
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 __device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug, int& blk) {
     int L = blockIdx.x;
     if (o.xcd) {
-        L = (L & 7) * (gridDim.x >> 3) + (L >> 3);
+        L = xcd_remap(L, gridDim.x);
         const int sn = L % o.nchunk, rest = L / o.nchunk;
         blk = rest % nblk;
         ug = sn * o.rgs + rest / nblk;
@@ -501,7 +500,7 @@ template <class In, class Out>
 void launch_band(hipStream_t s, const Band& A, int lanes, const BandOrder* ord, const In& in, const Out& out,
                  size_t lds = 0) {
     BandOrder o{lanes / WAVE, 1, 1, 0};
-    if (ord && ((size_t)o.nug * A.nblk) % 8 == 0) o = *ord;
+    if (ord) o = *ord;
     hipLaunchKernelGGL((k_band<In, Out>), dim3((lanes / WAVE) * A.nblk), dim3(WAVE), lds, s, A, o, in, out);
 }
 
@@ -631,6 +630,8 @@ struct StorePerfectDetect {
     int cstride_edge, cstride_snr;
     int U, R, snr0, last, M, nI, nQ, real_detect;
     double idd, sI, sQ;
+    const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
+    int stage;                         // IC iteration of this pass (trace only)
     double2* sym;
     SlicerLds* slt;
     int c0, c1;
@@ -712,6 +713,10 @@ struct StorePerfectDetect {
                 const int ne = __popc((unsigned)(dp ^ tx[k]));
                 c0 += ne;
                 c1 += cn[k] ? ne : 0;
+                if (tr && lane == tr->unit) {
+                    tr->yperf[(size_t)stage * tr->LK + row0 + r] = rr;
+                    tr->dec_p[(size_t)stage * tr->ND + dd[k]] = dp;
+                }
                 if (!last) {
                     double2 av = make_double2(0.0, 0.0);
                     c_fma(av, pv[k], sym[dp]);
@@ -735,6 +740,10 @@ struct StorePerfectDetect {
         const int ne = __popc((unsigned)(dp ^ (int)sidx[(size_t)d * R + rl]));
         c0 += ne;
         c1 += row_cons[row] ? ne : 0;
+        if (tr && lane == tr->unit) {
+            tr->yperf[(size_t)stage * tr->LK + row] = r;
+            tr->dec_p[(size_t)stage * tr->ND + d] = dp;
+        }
         if (!last) {
             double2 av = make_double2(0.0, 0.0);
             c_fma(av, row_pval[row], sym[dp]);
@@ -860,109 +869,24 @@ struct LoadNoisy {
     __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
 };
 
-void launch_rx_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const double* pn, uint64_t seed,
-                     uint64_t rep0, McBuffers& b) {
-    const char* e = getenv("DSCE_NOISE_FUSE");
-    if (sk.qh_disjoint && !(e && e[0] == '0')) {
+unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
+                         uint64_t seed, uint64_t rep0, McBuffers& b) {
+    if (sk.qh_disjoint && op.noise_fuse) {
         launch_band(s, sk.QH, b.U, nullptr, LoadNoisy{b.r0, pn, seed, rep0, b.R, b.snr0, sk.noise_slot},
                     StoreSoA{b.y, b.U});
-        return;
+        return PATH_NOISE_FUSED;
     }
     hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, sk.noise_slot, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)
     launch_band(s, sk.QH, b.U, nullptr, LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
 // perfect-CSI interference cancellation product (D - diag h) u = Q'(H(G u)) - h.*u
 // (script:541-543), two banded passes.
 // ---------------------------------------------------------------------------
-// Perfect-CSI IC iteration in one pass for schemes whose Q^H blocks only see
-// their own G columns (SchemeK::pic_ok, OFDM): per (64 units, Q^H block) the
-// block's u values stay in registers, t = G u is formed on the fly for each
-// sample and tap delay from the dense per-block G rows, (H t)[n] from the taps
-// and y_perf = Q^H (H t) accumulated for the block's rows; the epilogue is
-// StorePerfectDetect (y - acc + h u, slice, count, re-precode u in place).
-// t never touches memory.  grid: Q^H blocks x units/64 in BandOrder.
-template <int NT>
-__global__ void __launch_bounds__(64) k_pic(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, int ntap,
-                                            TapDelays dl, StorePerfectDetect out) {
-    extern __shared__ double2 pic_lds[];
-    constexpr int NTS = NT > 0 ? NT : DSCE_MAX_TAPS;
-    int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
-    const int lane = ug * WAVE + threadIdx.x;
-    const int U = out.U, R = out.R, rl = lane % R;
-    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk], khi = sk.QH.khi[blk];
-    const int s0 = sk.pic_s0[blk];
-    // LDS: constellation + slicer (epilogue), then the block's G rows [s0, khi) x 24
-    // and Q^H columns [klo, khi) x 24, read as broadcasts
-    double2* sg = pic_lds + 256 + (sizeof(SlicerLds) + 15) / 16;
-    const int ng = (khi - s0) * DSCE_RB, nq = (khi - klo) * DSCE_RB;
-    double2* sq = sg + ng;
-    {
-        const double2* __restrict__ gsrc = sk.pic_g + sk.pic_goff[blk];
-        const double2* __restrict__ qsrc = sk.QH.vals + sk.QH.off[blk];
-        for (int i = threadIdx.x; i < ng; i += WAVE) sg[i] = gsrc[i];
-        for (int i = threadIdx.x; i < nq; i += WAVE) sq[i] = qsrc[i];
-    }
-    StorePerfectDetect o = out;
-    double2 ur[DSCE_RB];
-#pragma unroll
-    for (int c = 0; c < DSCE_RB; ++c)
-        ur[c] = row0 + c < sk.LK ? o.u[(size_t)(row0 + c) * U + lane] : make_double2(0.0, 0.0);
-    o.prepare(pic_lds);                                  // stages its tables and syncs the block
-    double2 acc[DSCE_RB];
-#pragma unroll
-    for (int r = 0; r < DSCE_RB; ++r) acc[r] = make_double2(0.0, 0.0);
-    const int nt = NT > 0 ? NT : ntap;
-    // taps of sample n+1 are requested while sample n is processed
-    constexpr int NPF = NT > 0 ? NT : 1;
-    double2 hcur[NPF], hnxt[NPF];
-    if (NT > 0) {
-#pragma unroll
-        for (int q = 0; q < NPF; ++q) hcur[q] = ir[((size_t)q * N + klo) * R + rl];
-    }
-    for (int n = klo; n < khi; ++n) {
-        if (NT > 0) {
-            const int nn = n + 1 < khi ? n + 1 : n;
-#pragma unroll
-            for (int q = 0; q < NPF; ++q) hnxt[q] = ir[((size_t)q * N + nn) * R + rl];
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        double2 x = make_double2(0.0, 0.0);
-#pragma unroll
-        for (int q = 0; q < NTS; ++q) {
-            if (q >= nt) break;
-            const int m = n - dl.d[q];
-            if (m < 0) continue;
-            const double2 hq = NT > 0 ? hcur[q < NPF ? q : 0] : ir[((size_t)q * N + n) * R + rl];
-            const double2* gr = sg + (m - s0) * DSCE_RB;
-            // t = G[m, :] u with 4 partial sums (independent FMA chains)
-            double2 t0 = make_double2(0.0, 0.0), t1 = t0, t2 = t0, t3 = t0;
-#pragma unroll
-            for (int c = 0; c < DSCE_RB; c += 4) {
-                c_fma(t0, gr[c], ur[c]);
-                c_fma(t1, gr[c + 1], ur[c + 1]);
-                c_fma(t2, gr[c + 2], ur[c + 2]);
-                c_fma(t3, gr[c + 3], ur[c + 3]);
-            }
-            const double2 t = c_add(c_add(t0, t1), c_add(t2, t3));
-            c_fma(x, hq, t);
-        }
-        const double2* qk = sq + (n - klo) * DSCE_RB;
-#pragma unroll
-        for (int r = 0; r < DSCE_RB; ++r) c_fma(acc[r], qk[r], x);
-        if (NT > 0) {
-#pragma unroll
-            for (int q = 0; q < NPF; ++q) hcur[q] = hnxt[q];
-        }
-    }
-    o.rows_u(row0, nrows, lane, acc, ur);
-    o.finish(lane);
-}
-
 // The whole perfect-CSI IC chain (iterations 1..n_iter, script:541-561) in one
 // kernel for pic_ok schemes (OFDM): D = Q'HG is block-diagonal there, so the
 // chain of a (unit, Q^H block) never needs another block, and u (the block's
@@ -1117,6 +1041,10 @@ __global__ void __launch_bounds__(256) k_pic_chain(SchemeK sk, BandOrder ord, co
                 const int ne = __popc((unsigned)(dp ^ tx[k]));
                 c0 += ne;
                 c1 += cn[k] ? ne : 0;
+                if (o.tr && lane == o.tr->unit) {
+                    o.tr->yperf[(size_t)it * o.tr->LK + row0 + rh + r] = rr;
+                    o.tr->dec_p[(size_t)it * o.tr->ND + dd[k]] = dp;
+                }
                 if (!last) {
                     double2 av = make_double2(0.0, 0.0);
                     c_fma(av, pv[k], sym[dp]);
@@ -1363,6 +1291,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
                 e0 += ne;
                 e1 += (dc[r] & 1) ? ne : 0;
                 dps[r] = dp;
+                if (o.tr && data && unit == o.tr->unit) {
+                    o.tr->yperf[(size_t)it * o.tr->LK + row0 + 16 * t + kq + 4 * r] = yp;
+                    o.tr->dec_p[(size_t)it * o.tr->ND + (dc[r] >> 1)] = dp;
+                }
             }
             // one uniform branch per tile, after all its rows (a branch per row
             // splits the rows into separate blocks the scheduler cannot interleave)
@@ -1428,27 +1360,21 @@ static int pic_chain_variant(const ChannelK& ch) {
     return 0;
 }
 
-// DSCE_PIC_CHAIN: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 (default) =
+// Opts::pic_chain: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 (default) =
 // k_pic_mfma where the scheme allows it, else k_pic_chain
-static int pic_chain_mode() {
-    const char* e = getenv("DSCE_PIC_CHAIN");
-    return e ? atoi(e) : 2;
+static bool pic_mfma_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch) {
+    return sk.pm_ok && op.pic_chain == 2 && ch.ntap <= 2 && (sk.pm_ksq == 6 || sk.pm_ksq == 7);
 }
 
-static bool pic_mfma_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
-    return sk.pm_ok && pic_chain_mode() == 2 && ch.ntap <= 2 && (sk.pm_ksq == 6 || sk.pm_ksq == 7) &&
-           ((size_t)(b.U / WAVE) * sk.QH.nblk) % 8 == 0;
+bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    if (pic_mfma_ok(op, sk, ch)) return true;
+    return sk.pic_ok && pic_chain_variant(ch) && op.pic_chain != 0 && b.R % PCH_UNITS == 0;
 }
 
-bool perfect_chain_ok(const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
-    if (pic_mfma_ok(sk, ch, b)) return true;
-    return sk.pic_ok && pic_chain_variant(ch) && pic_chain_mode() != 0 && b.R % PCH_UNITS == 0 &&
-           ((size_t)(b.U / PCH_UNITS) * sk.QH.nblk) % 8 == 0;
-}
-
-void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                          const PerfectDetectArgs* pd, int niter) {
+unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                              const PerfectDetectArgs* pd, int niter) {
     StorePerfectDetect o{};
+    o.tr = b.tr;
     o.y = b.y;
     o.h = b.h;
     o.u = b.u;
@@ -1476,9 +1402,8 @@ void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, 
     o.sQ = pd->sQ;
     TapDelays dl{};
     for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
-    const char* xe = getenv("DSCE_XCD");
-    if (pic_mfma_ok(sk, ch, b)) {
-        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, (!xe || xe[0] != '0') ? 1 : 0};
+    if (pic_mfma_ok(op, sk, ch)) {
+        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
         const size_t lds = ((size_t)(2 * 6 + 2 * sk.pm_ksq) * 64 + 256) * sizeof(double2) + sizeof(SlicerLds);
         const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
         const int d1 = ch.ntap > 1 ? ch.tap_delay[1] : 0;
@@ -1492,9 +1417,9 @@ void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, 
             else LAUNCH_PM(7, 1);
         }
 #undef LAUNCH_PM
-        return;
+        return PATH_PIC_MFMA;
     }
-    const BandOrder ord{b.U / PCH_UNITS, b.U / b.R, b.R / PCH_UNITS, (!xe || xe[0] != '0') ? 1 : 0};
+    const BandOrder ord{b.U / PCH_UNITS, b.U / b.R, b.R / PCH_UNITS, op.xcd};
     const size_t plds = 256 * sizeof(double2) + sizeof(SlicerLds) + 16 + (size_t)sk.pic_rows * DSCE_RB * sizeof(double2);
     const dim3 grid((b.U / PCH_UNITS) * sk.QH.nblk), blk(256);
     switch (pic_chain_variant(ch)) {
@@ -1503,20 +1428,17 @@ void launch_perfect_chain(hipStream_t s, const SchemeK& sk, const ChannelK& ch, 
         case 3: hipLaunchKernelGGL((k_pic_chain<3, 2>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
         default: break;
     }
+    return PATH_PIC_CHAIN;
 }
 
-void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const PerfectDetectArgs* pd) {
-    // DSCE_PIC=1: one-pass k_pic (t never written; 248 VGPRs -> 2 waves/SIMD,
-    // measured 5 % slower than the two passes at C2, so opt-in)
-    const char* pe = getenv("DSCE_PIC");
-    const bool pic = pd && sk.pic_ok && (pe && pe[0] == '1') && ((size_t)(b.U / WAVE) * sk.QH.nblk) % 8 == 0;
-    if (!pic) launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
+unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                           const PerfectDetectArgs* pd) {
+    launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
     // SNR-fastest XCD-aware order: the SNR units of a realisation share its taps
-    const char* xe = getenv("DSCE_XCD");
-    const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, (!xe || xe[0] != '0') ? 1 : 0};
+    const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
     if (!pd) {
         launch_pass2_nt(s, sk, ch, b, ord, StorePerfectIC{b.yperf, b.y, b.h, b.u, b.U, b.R});
-        return;
+        return PATH_PIC_PASSES;
     }
     StorePerfectDetect o{};
     o.y = b.y;
@@ -1545,23 +1467,10 @@ void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McB
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
-    const size_t lds = 256 * sizeof(double2) + sizeof(SlicerLds);
-    if (pic) {
-        // one pass, t never written (the G u pass above is skipped)
-        TapDelays dl{};
-        for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
-        // + the G rows and Q^H columns of the widest block
-        const size_t plds = lds + 16 + (size_t)sk.pic_rows * DSCE_RB * sizeof(double2);
-        const dim3 grid((b.U / WAVE) * sk.QH.nblk);
-        switch (ch.ntap) {
-            case 1: hipLaunchKernelGGL(k_pic<1>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
-            case 2: hipLaunchKernelGGL(k_pic<2>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
-            case 3: hipLaunchKernelGGL(k_pic<3>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
-            default: hipLaunchKernelGGL(k_pic<0>, grid, dim3(WAVE), plds, s, sk, ord, b.ir, ch.N, ch.ntap, dl, o); break;
-        }
-        return;
-    }
-    launch_pass2_nt(s, sk, ch, b, ord, o, lds);
+    o.tr = b.tr;
+    o.stage = pd->stage;
+    launch_pass2_nt(s, sk, ch, b, ord, o, 256 * sizeof(double2) + sizeof(SlicerLds));
+    return PATH_PIC_PASSES;
 }
 
 // ---------------------------------------------------------------------------
@@ -1572,99 +1481,9 @@ void launch_perfect_ic(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McB
 // right operand Z = hP (x) v generated on the fly; W is shared by all units of
 // one SNR point.
 //
-// k_wcontract_mfma: v_mfma_f64_16x16x4_f64.  A = W (16 rows x 4 k, one f64 per
-// lane: row = lane&15, k = lane>>4), B = Z (4 k x 16 units: k = lane>>4,
-// unit = lane&15), D: row = (lane>>4) + 4*reg, unit = lane&15
-// (cdna_hip_programming.md §3 f64 layout; probed by tools/mfma_f64_layout.hip).
-// Complex product with 4 real MFMAs: Re += Wr Zr + (-Wi) Zi, Im += Wr Zi + Wi Zr.
-// Wave tile = 32 rows (2 row tiles, one W band block) x 64 units (4 unit
-// tiles) -> 32 MFMAs per 4-deep k step.  Block = 4 waves = 256 units.
-// grid (U/256, nblk).
-// ---------------------------------------------------------------------------
-// one complex 16x16x4 tile: (re, im) += W (16 rows x 4 k) * Z (4 k x 16 units)
-#define CTILE(RE, IM, W, Z)                 \
-    RE = MFMA64((W).x, (Z).x, RE);          \
-    RE = MFMA64(-(W).y, (Z).y, RE);         \
-    IM = MFMA64((W).x, (Z).y, IM);          \
-    IM = MFMA64((W).y, (Z).x, IM)
-
-// Wave tile: 32 rows x 32 units (2 x 2 complex tiles, 64 accumulator AGPRs ->
-// 2-3 waves per SIMD).  Block = 4 waves = 128 units.  grid (U/128, nblk).
-__global__ void __launch_bounds__(256) k_wcontract_mfma(Band Wb, const double2* __restrict__ Wall, long long w_elems,
-                                                        int var, int nsnr, int snr0, int NP, int R, int U,
-                                                        const double2* __restrict__ hp,
-                                                        const double2* __restrict__ v,
-                                                        const double2* __restrict__ y,
-                                                        double2* __restrict__ yest) {
-    extern __shared__ double2 shp[];                     // [4 waves][NP][32]
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int ubase = blockIdx.x * 128 + wv * 32;
-    const int snr = snr0 + ubase / R;
-    const int blk = blockIdx.y;
-    double2* sh = shp + (size_t)wv * NP * 32;
-    if (l < 32)
-        for (int p = 0; p < NP; ++p) sh[p * 32 + l] = hp[(size_t)p * U + ubase + l];
-    __syncthreads();
-    const int rb = Wb.rb;
-    const int row0 = Wb.row0[blk], nrows = Wb.nrows[blk];
-    const int c_lo = Wb.klo[blk] / NP, c_hi = Wb.khi[blk] / NP;
-    const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)w_elems + Wb.off[blk];
-    const int kk = l >> 4, j = l & 15;
-    d4 r00 = {0, 0, 0, 0}, i00 = r00, r01 = r00, i01 = r00, r10 = r00, i10 = r00, r11 = r00, i11 = r00;
-    const int nq = NP >> 2;
-    const int nstep = (c_hi - c_lo) * nq;                 // k steps of 4 (column c, pilots 4q..4q+3); even
-    const double2* __restrict__ vb = v + ubase + j;
-    const double2* __restrict__ wb = w + (size_t)kk * rb + j;
-    // step st: column c = c_lo + st / nq, pilots 4 (st % nq) + kk
-#define LOADSTEP(ST, W0, W1, V0, V1)                                              \
-    {                                                                            \
-        const int c_ = (ST) / nq;                                                \
-        const double2* wk_ = wb + ((size_t)c_ * NP + 4 * ((ST) - c_ * nq)) * rb; \
-        W0 = wk_[0];                                                             \
-        W1 = wk_[16];                                                            \
-        const double2* vv_ = vb + (size_t)(c_lo + c_) * U;                       \
-        V0 = vv_[0];                                                             \
-        V1 = vv_[16];                                                            \
-    }
-#define MMASTEP(ST, W0, W1, V0, V1)                                   \
-    {                                                                 \
-        const int p_ = 4 * ((ST) % nq) + kk;                          \
-        const double2 z0 = c_mul(sh[p_ * 32 + j], V0);                \
-        const double2 z1 = c_mul(sh[p_ * 32 + 16 + j], V1);           \
-        CTILE(r00, i00, W0, z0);                                      \
-        CTILE(r01, i01, W0, z1);                                      \
-        CTILE(r10, i10, W1, z0);                                      \
-        CTILE(r11, i11, W1, z1);                                      \
-    }
-    double2 a0, a1, av0, av1, b0, b1, bv0, bv1;
-    if (nstep > 0) LOADSTEP(0, a0, a1, av0, av1);
-    for (int st = 0; st < nstep; st += 2) {
-        LOADSTEP(st + 1, b0, b1, bv0, bv1);
-        MMASTEP(st, a0, a1, av0, av1);
-        const int sn = min(st + 2, nstep - 1);
-        LOADSTEP(sn, a0, a1, av0, av1);
-        MMASTEP(st + 1, b0, b1, bv0, bv1);
-    }
-#undef LOADSTEP
-#undef MMASTEP
-    // D layout: row = 16*it + kk + 4*reg, unit = 16*jt + j
-#define STORE(ACCR, ACCI, IT, JT)                                                       \
-    _Pragma("unroll") for (int reg = 0; reg < 4; ++reg) {                               \
-        const int row = 16 * (IT) + kk + 4 * reg;                                       \
-        if (row < nrows) {                                                              \
-            const size_t i_ = (size_t)(row0 + row) * U + ubase + 16 * (JT) + j;         \
-            yest[i_] = c_sub(y[i_], make_double2(ACCR[reg], ACCI[reg]));                \
-        }                                                                               \
-    }
-    STORE(r00, i00, 0, 0)
-    STORE(r01, i01, 0, 1)
-    STORE(r10, i10, 1, 0)
-    STORE(r11, i11, 1, 1)
-#undef STORE
-}
-
-// VALU reference variant (one unit per lane, W rows wave-uniform via scalar
-// loads); kept for in-process A/B (DSCE_WCONTRACT=valu) and NP % 4 != 0.
+// VALU variant (one unit per lane, W rows wave-uniform via scalar loads): the
+// fallback for pilot counts without a pair-tile instance (NP / 4 not in {2, 4, 8})
+// and Opts::wcontract_valu.
 __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* __restrict__ Wall, long long w_elems,
                                                        int var, int nsnr, int snr0, int NP, int R, int U,
                                                        const double2* __restrict__ hp, const double2* __restrict__ v,
@@ -1711,7 +1530,7 @@ __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* _
 // periods (RBP 24: 3 tiles = 2 columns, RBP 32: 2 tiles = 1 column) so pair ->
 // (column, row) is compile-time.  Wave = 16 units, block = 4 waves = 64 units of
 // one SNR point; grid (U/64, nblk).
-template <int RBP, int NKS, bool PF>
+template <int RBP, int NKS>
 __global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __restrict__ Wall, long long wp_elems,
                                                int var, int nsnr, int snr0, int R, int U,
                                                const double2* __restrict__ hp, const double2* __restrict__ v,
@@ -1766,41 +1585,27 @@ __global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __rest
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     double2 A0[NKS], A1[NKS], vv[CPP];
-    if (PF) {
-        // tile-level ping-pong: tile t+1's W loads are in flight during tile t's MFMAs
-        if (ntile > 0) ldt(0, A0);
-        for (int t0 = 0; t0 < ntile; t0 += PER) {
-            ldv(t0, vv);
-            const int tn = t0 + PER < ntile ? t0 + PER : t0;          // clamp: harmless reload at the end
-            if (PER == 3) {
-                // period of 3 tiles: A0 A1 A0, and the next period's first tile lands in A1 ->
-                // swap roles by reloading it into A0 after the last tile (one register copy)
-                ldt(t0 + 1, A1);
-                tile(A0, vv, I0{});
-                ldt(t0 + 2, A0);
-                tile(A1, vv, I1{});
-                ldt(tn, A1);
-                tile(A0, vv, I2{});
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) A0[ks] = A1[ks];
-            } else {
-                ldt(t0 + 1, A1);
-                tile(A0, vv, I0{});
-                ldt(tn, A0);
-                tile(A1, vv, I1{});
-            }
-        }
-    } else {
-        for (int t0 = 0; t0 < ntile; t0 += PER) {
-            ldv(t0, vv);
-            ldt(t0, A0);
-            tile(A0, vv, I0{});
+    // tile-level ping-pong: tile t+1's W loads are in flight during tile t's MFMAs
+    if (ntile > 0) ldt(0, A0);
+    for (int t0 = 0; t0 < ntile; t0 += PER) {
+        ldv(t0, vv);
+        const int tn = t0 + PER < ntile ? t0 + PER : t0;          // clamp: harmless reload at the end
+        if (PER == 3) {
+            // period of 3 tiles: A0 A1 A0, and the next period's first tile lands in A1 ->
+            // swap roles by reloading it into A0 after the last tile (one register copy)
             ldt(t0 + 1, A1);
+            tile(A0, vv, I0{});
+            ldt(t0 + 2, A0);
             tile(A1, vv, I1{});
-            if (PER == 3) {
-                ldt(t0 + 2, A0);
-                tile(A0, vv, I2{});
-            }
+            ldt(tn, A1);
+            tile(A0, vv, I2{});
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) A0[ks] = A1[ks];
+        } else {
+            ldt(t0 + 1, A1);
+            tile(A0, vv, I0{});
+            ldt(tn, A0);
+            tile(A1, vv, I1{});
         }
     }
     const int row0 = P.row0[blk], nrows = P.nrows[blk];
@@ -1835,10 +1640,11 @@ struct FuseArgs {
     unsigned long long* counters;
     double* mse_err;
     double* mse_pow;
+    const TraceK* tr;              // null unless tracing (dsce_trace_unit_ex)
     int var, stage, nstage, last, scheme;
 };
 
-template <int RBP, int NKS, bool FUSE, bool WDA_3M, bool X4>
+template <int RBP, int NKS, bool FUSE, bool WDA_3M>
 __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __restrict__ W3, long long wp_elems,
                                             int var, int nsnr, int snr0, int R, int U,
                                             const double2* __restrict__ hp, const double2* v,
@@ -1895,7 +1701,7 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
     }
     const int clo = P.clo[blk], ntile = P.ntile[blk];
     const double* __restrict__ w =
-        W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + (X4 ? 2 * lane : lane);
+        W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + 2 * lane;
     double2 acc[NACC];
 #pragma unroll
     for (int k = 0; k < NACC; ++k) acc[k] = make_double2(0.0, 0.0);
@@ -1907,27 +1713,17 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
         d4 p1, p2, p3;
     };
     auto ldt = [&](int t, T3& a) {
-        if (X4) {
-            // [tile][k-step pair][plane][lane][2]: one 16-byte load per plane and pair
+        // [tile][k-step pair][plane][lane][2]: one 16-byte load per plane and pair
 #pragma unroll
-            for (int kp = 0; kp < NKS / 2; ++kp) {
-                const double2* q = reinterpret_cast<const double2*>(w + ((size_t)t * (NKS / 2) + kp) * 384);
-                const double2 r = q[0], i = q[64], sm = q[128];
-                a.r[2 * kp] = r.x;
-                a.r[2 * kp + 1] = r.y;
-                a.i[2 * kp] = i.x;
-                a.i[2 * kp + 1] = i.y;
-                a.s[2 * kp] = sm.x;
-                a.s[2 * kp + 1] = sm.y;
-            }
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const double* q = w + ((size_t)t * NKS + ks) * 192;
-                a.r[ks] = q[0];
-                a.i[ks] = q[64];
-                a.s[ks] = q[128];
-            }
+        for (int kp = 0; kp < NKS / 2; ++kp) {
+            const double2* q = reinterpret_cast<const double2*>(w + ((size_t)t * (NKS / 2) + kp) * 384);
+            const double2 r = q[0], i = q[64], sm = q[128];
+            a.r[2 * kp] = r.x;
+            a.r[2 * kp + 1] = r.y;
+            a.i[2 * kp] = i.x;
+            a.i[2 * kp + 1] = i.y;
+            a.s[2 * kp] = sm.x;
+            a.s[2 * kp + 1] = sm.y;
         }
     };
     auto mma = [&](const T3& a, D3& d) {
@@ -2098,6 +1894,11 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
         const int ne = dc >= 0 ? __popc((unsigned)(de ^ (int)((ftx[k >> 2] >> (8 * (k & 3))) & 0xffu))) : 0;
         cnt[0] += ne;
         cnt[1] += (dc & 1) ? ne : 0;
+        if (fa.tr && valid && unit == fa.tr->unit) {
+            fa.tr->yest[(size_t)fa.stage * fa.tr->LK + row] = ye;
+            fa.tr->hest[(size_t)fa.stage * fa.tr->LK + row] = he;
+            if (dc >= 0) fa.tr->dec_e[(size_t)fa.stage * fa.tr->ND + (dc >> 1)] = de;
+        }
         if (!fa.last && dc >= 0) {
             double2 av = make_double2(0.0, 0.0);
             c_fma(av, frpv[valid ? r : 0], fsym[de]);
@@ -2109,21 +1910,13 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
     if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage);
 }
 
-#define WPAIR3_ARGS                                                                                          \
-    PairBand P, const double* __restrict__ W3, long long wp_elems, int var, int nsnr, int snr0, int R, int U, \
-        const double2* __restrict__ hp, const double2* v, const double2* __restrict__ y,                      \
-        double2* __restrict__ yest, SchemeK sk, FuseArgs fa
-template <int RBP, int NKS, bool FUSE, bool WDA_3M = false, bool X4 = false>
-__global__ void __launch_bounds__(256) k_wpair3(WPAIR3_ARGS) {
-    wpair3_body<RBP, NKS, FUSE, WDA_3M, X4>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
+template <int RBP, int NKS, bool FUSE, bool WDA_3M = false>
+__global__ void __launch_bounds__(256)
+    k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems, int var, int nsnr, int snr0, int R, int U,
+             const double2* __restrict__ hp, const double2* v, const double2* __restrict__ y,
+             double2* __restrict__ yest, SchemeK sk, FuseArgs fa) {
+    wpair3_body<RBP, NKS, FUSE, WDA_3M>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
 }
-
-// the fused kernel with the 16-byte W loads held to 168 VGPRs (3 waves/SIMD)
-template <int RBP, int NKS, bool WDA_3M>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_wpair3_f3(WPAIR3_ARGS) {
-    wpair3_body<RBP, NKS, true, WDA_3M, true>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
-}
-#undef WPAIR3_ARGS
 
 // Pre-pass of the fused MMSE stage of IC iteration `stage` (script:482-489):
 // y_est at the NP pilot rows with the previous stage's D_hat (W of var_prev,
@@ -2172,12 +1965,14 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
     }
 }
 
-bool mmse_fused_ok(const SchemeK& sk, const MmseK& mm, const McBuffers& b) {
-    const char* e = getenv("DSCE_FUSE_STAGE");
-    const char* m3e = getenv("DSCE_WPAIR_3M");
-    const char* we = getenv("DSCE_WCONTRACT");
-    return mm.Wpil && mm.WdA && mm.Wp3 && mm.Pb.rbp == 24 && mm.Pb.nks == 4 && sk.NP == 16 && !(e && e[0] == '0') &&
-           !(m3e && m3e[0] == '0') && !(we && we[0] != 'p') && (b.U % 64) == 0 && (b.R % 64) == 0;
+static bool wpair_3m(const Opts& op, const MmseK& mm) {
+    // 3M by default where its extra registers still leave 3 waves/SIMD (NP <= 16)
+    return mm.Wp3 && (op.wpair_3m < 0 ? mm.Pb.nks <= 4 : op.wpair_3m != 0);
+}
+
+bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b) {
+    return mm.Wpil && mm.WdA && mm.Pb.rbp == 24 && mm.Pb.nks == 4 && sk.NP == 16 && op.fuse_stage &&
+           !op.wcontract_valu && wpair_3m(op, mm) && (b.U % 64) == 0 && (b.R % 64) == 0;
 }
 
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
@@ -2186,9 +1981,9 @@ void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
                        b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.xp, hp_new);
 }
 
-void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, int var_cur, int stage,
-                       int n_iter, bool last, McBuffers& b, const double2* hp_prev, double2* hp_new,
-                       unsigned long long* counters, int scheme_index) {
+unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
+                           int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
+                           double2* hp_new, unsigned long long* counters, int scheme_index) {
     FuseArgs fa{};
     fa.WdA = mm.WdA;
     fa.hp_new = hp_new;
@@ -2198,101 +1993,61 @@ void launch_mmse_fused(hipStream_t s, const SchemeK& sk, const MmseK& mm, int va
     fa.counters = counters;
     fa.mse_err = b.mse_err;
     fa.mse_pow = b.mse_pow;
+    fa.tr = b.tr;
     fa.var = var_cur;
     fa.stage = stage;
     fa.nstage = n_iter + 1;
     fa.last = last ? 1 : 0;
     fa.scheme = scheme_index;
-    // DSCE_WDA_3M=0: diag(D_hat) of the epilogue with four real MFMAs per k-step
-    const char* e3 = getenv("DSCE_WDA_3M");
-    const bool wda3 = !(e3 && e3[0] == '0');
-#define LAUNCH_FW(WDA, X4V)                                                                                        \
-    hipLaunchKernelGGL((k_wpair3<24, 4, true, WDA, X4V>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb,         \
-                       mm.Wp3, mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa)
-    const char* e3w = getenv("DSCE_WPAIR_3W");
-    if (mm.w3x4 && e3w && e3w[0] == '1') {
-        if (wda3)
-            hipLaunchKernelGGL((k_wpair3_f3<24, 4, true>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
-                               mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
-        else
-            hipLaunchKernelGGL((k_wpair3_f3<24, 4, false>), dim3(b.U / 64, mm.Pb.nblk), dim3(256), 0, s, mm.Pb, mm.Wp3,
-                               mm.wp_elems, var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
-    } else if (mm.w3x4) {
-        if (wda3) LAUNCH_FW(true, true);
-        else LAUNCH_FW(false, true);
-    } else {
-        if (wda3) LAUNCH_FW(true, false);
-        else LAUNCH_FW(false, false);
-    }
-#undef LAUNCH_FW
+    const dim3 grid(b.U / 64, mm.Pb.nblk);
+    // Opts::wda_3m = 0: diag(D_hat) of the epilogue with four real MFMAs per k-step
+    if (op.wda_3m)
+        hipLaunchKernelGGL((k_wpair3<24, 4, true, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var_prev,
+                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    else
+        hipLaunchKernelGGL((k_wpair3<24, 4, true, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var_prev,
+                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    return PATH_WPAIR3_FUSED;
 }
 
-void launch_wcontract(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
-    // DSCE_WCONTRACT = pair (default) | mfma (32-row tiles) | valu — read per launch for A/B.
-    const char* mode = getenv("DSCE_WCONTRACT");
-    const bool pair_ok = mm.Wp && (b.U % 64) == 0 && (b.R % 64) == 0 && !(mode && mode[0] != 'p');
+unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
+    const bool pair_ok = mm.Wp && (b.U % 64) == 0 && (b.R % 64) == 0 && !op.wcontract_valu;
     if (pair_ok) {
         const dim3 grid(b.U / 64, mm.Pb.nblk);
-        const char* pfe = getenv("DSCE_WPAIR_PF");
-        const bool pf = !(pfe && pfe[0] == '0');
-        // DSCE_WPAIR_3M=0 selects the 4-MFMA complex product
-        // 3M form by default where its extra registers still leave 3 waves/SIMD
-        // (NP <= 16); DSCE_WPAIR_3M=0 / 1 forces it off / on
-        const char* m3e = getenv("DSCE_WPAIR_3M");
-        const bool m3 = m3e ? m3e[0] != '0' : mm.Pb.nks <= 4;
-        if (mm.Wp3 && m3) {
-#define LAUNCH_W3(RBPV, NKSV)                                                                                    \
-    {                                                                                                            \
-        if (mm.w3x4)                                                                                             \
-            hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false, false, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3,   \
-                               mm.wp_elems, var, mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{}); \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems,   \
-                               var, mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{});           \
-    }
+        if (wpair_3m(op, mm)) {
+#define LAUNCH_W3(RBPV, NKSV)                                                                                  \
+    hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,    \
+                       mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{})
             if (mm.Pb.rbp == 24) {
-                if (mm.Pb.nks == 2) LAUNCH_W3(24, 2)
-                else if (mm.Pb.nks == 4) LAUNCH_W3(24, 4)
-                else LAUNCH_W3(24, 8)
+                if (mm.Pb.nks == 2) LAUNCH_W3(24, 2);
+                else if (mm.Pb.nks == 4) LAUNCH_W3(24, 4);
+                else LAUNCH_W3(24, 8);
             } else {
-                if (mm.Pb.nks == 2) LAUNCH_W3(32, 2)
-                else if (mm.Pb.nks == 4) LAUNCH_W3(32, 4)
-                else LAUNCH_W3(32, 8)
+                if (mm.Pb.nks == 2) LAUNCH_W3(32, 2);
+                else if (mm.Pb.nks == 4) LAUNCH_W3(32, 4);
+                else LAUNCH_W3(32, 8);
             }
 #undef LAUNCH_W3
-            return;
+            return PATH_WPAIR3;
         }
 #define LAUNCH_WP(RBPV, NKSV)                                                                                    \
-    {                                                                                                            \
-        if (pf)                                                                                                  \
-            hipLaunchKernelGGL((k_wpair<RBPV, NKSV, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var,  \
-                               mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                               \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_wpair<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var, \
-                               mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest);                               \
-    }
+    hipLaunchKernelGGL((k_wpair<RBPV, NKSV>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var, mm.nsnr, b.snr0, \
+                       b.R, b.U, b.hp, b.v, b.y, b.yest)
         if (mm.Pb.rbp == 24) {
-            if (mm.Pb.nks == 2) LAUNCH_WP(24, 2)
-            else if (mm.Pb.nks == 4) LAUNCH_WP(24, 4)
-            else LAUNCH_WP(24, 8)
+            if (mm.Pb.nks == 2) LAUNCH_WP(24, 2);
+            else if (mm.Pb.nks == 4) LAUNCH_WP(24, 4);
+            else LAUNCH_WP(24, 8);
         } else {
-            if (mm.Pb.nks == 2) LAUNCH_WP(32, 2)
-            else if (mm.Pb.nks == 4) LAUNCH_WP(32, 4)
-            else LAUNCH_WP(32, 8)
+            if (mm.Pb.nks == 2) LAUNCH_WP(32, 2);
+            else if (mm.Pb.nks == 4) LAUNCH_WP(32, 4);
+            else LAUNCH_WP(32, 8);
         }
 #undef LAUNCH_WP
-        return;
+        return PATH_WPAIR4M;
     }
-    bool valu = (sk.NP % 8) != 0 || mm.Wb.rb != 32 || (b.U % 128) != 0 || (b.R % 32) != 0;
-    if (mode && mode[0] == 'v') valu = true;
-    if (valu) {
-        hipLaunchKernelGGL(k_wcontract_valu, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2),
-                           s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
-    } else {
-        hipLaunchKernelGGL(k_wcontract_mfma, dim3(b.U / 128, mm.Wb.nblk), dim3(256),
-                           (size_t)4 * sk.NP * 32 * sizeof(double2), s, mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0,
-                           sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
-    }
+    hipLaunchKernelGGL(k_wcontract_valu, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2), s,
+                       mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
+    return PATH_WCONTRACT_VALU;
 }
 
 // ---------------------------------------------------------------------------
@@ -2327,7 +2082,8 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
 }
 
 struct StageArgs {
-    int stage, var, nsnr, nstage, scheme, last, trace, perfect, R, U, snr0, xcd_order;
+    int stage, var, nsnr, nstage, scheme, last, perfect, R, U, snr0, xcd_order;
+    const TraceK* tr;          // null unless tracing (dsce_trace_unit_ex)
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
     double* mse_err;           // null: no MSE accumulation (see flush_mse)
@@ -2364,6 +2120,7 @@ __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const 
         const size_t i = (size_t)c * U + unit;
         const double2 hv = h[(size_t)c * R + rl];
         hest[i] = acc;
+        if (st.tr && unit == st.tr->unit) st.tr->hest[(size_t)st.stage * st.tr->LK + c] = acc;
         e_est[i] = c_div(st.ysrc_e[i], acc);
         e_perf[i] = c_div(st.ysrc_p[i], hv);
         if (st.mse_err) {
@@ -2414,6 +2171,7 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
             const int d = lds_slicer ? slice_fast(slt, sk.nI, sk.nQ, z, sI, sQ) : slice(sk, z);
             const int tx = sidx[(size_t)i * R + rl];
             const int ne = __popc((unsigned)(d ^ tx));
+            if (st.tr && unit == st.tr->unit) (csi ? st.tr->dec_p : st.tr->dec_e)[(size_t)st.stage * st.tr->ND + i] = d;
             cnt[csi * 2 + 0] += ne;
             if (sk.considered[i]) cnt[csi * 2 + 1] += ne;
             if (!st.last) qo[(size_t)i * U + unit] = (uint16_t)d;
@@ -2495,7 +2253,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
     // together; with xcd_order each XCD (block b runs on XCD b % 8) walks its own
     // contiguous range of that order, keeping the reuse inside one L2.
     int L = blockIdx.x;
-    if (st.xcd_order) L = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    if (st.xcd_order) L = xcd_remap(L, gridDim.x);
     const int rbk = L % nrb;
     int ug = L / nrb;
     if (st.xcd_order) {
@@ -2593,7 +2351,8 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
         if (r < nr) {
             const int row = r0 + r;
             const size_t ix = (size_t)row * U + unit;
-            if (st.trace) hest[ix] = acc[r];
+            const bool traced = st.tr && unit == st.tr->unit;
+            if (traced) st.tr->hest[(size_t)st.stage * st.tr->LK + row] = acc[r];
             const int i = rdat[r];
             if (i >= 0) {
                 const double2 ze = c_div1(ye[r], acc[r]);
@@ -2611,6 +2370,10 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                     const int np_ = __popc((unsigned)(dp ^ tx[r]));
                     cnt[2] += np_;
                     cnt[3] += cons ? np_ : 0;
+                }
+                if (traced) {
+                    st.tr->dec_e[(size_t)st.stage * st.tr->ND + i] = de;
+                    if (PERF) st.tr->dec_p[(size_t)st.stage * st.tr->ND + i] = dp;
                 }
                 if (!st.last) {
                     if (sk.p_diag) {
@@ -2641,31 +2404,27 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
 }
 
 template <int NPT>
-static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
+static void launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
                                   unsigned long long* counters, int rb) {
     const int ug = b.U / 64;
-    const char* xe = getenv("DSCE_XCD");
-    const bool xcd = !xe || xe[0] != '0';
 #define LAUNCH_SF(RBV)                                                                                          \
     {                                                                                                           \
         const int nrb = (sk.LK + 4 * (RBV) - 1) / (4 * (RBV));                                                  \
-        StageArgs sa = st;                                                                                      \
-        sa.xcd_order = xcd && ((ug * nrb) % 8) == 0;                                                            \
         if (st.mse_err) {                                                                                       \
             if (st.perfect)                                                                                     \
-                hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, true>), dim3(ug * nrb), dim3(256), 0, s, sk, sa, \
+                hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, true>), dim3(ug * nrb), dim3(256), 0, s, sk, st, \
                                    nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters); \
             else                                                                                                \
                 hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, true>), dim3(ug * nrb), dim3(256), 0, s, sk,  \
-                                   sa, nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u,       \
+                                   st, nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u,       \
                                    counters);                                                                   \
         } else if (st.perfect)                                                                                  \
-            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa,   \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, false>), dim3(ug * nrb), dim3(256), 0, s, sk, st,   \
                                nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
         else                                                                                                    \
-            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, false>), dim3(ug * nrb), dim3(256), 0, s, sk, sa,  \
+            hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, false>), dim3(ug * nrb), dim3(256), 0, s, sk, st,  \
                                nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
-        return true;                                                                                            \
+        return;                                                                                                 \
     }
     if (rb == 4) LAUNCH_SF(4)
     if (rb == 16) LAUNCH_SF(16)
@@ -2673,20 +2432,16 @@ static bool launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageA
 #undef LAUNCH_SF
 }
 
-static bool stage_fused_ok(const SchemeK& sk) {
-    const char* mode = getenv("DSCE_STAGE");
-    const bool split = mode && mode[0] == 's';
-    return !sk.despread && !split && (sk.NP == 8 || sk.NP == 16 || sk.NP == 32) && sk.M <= 256 && sk.nI <= 16 &&
-           sk.nQ <= 16;
+static bool stage_fused_ok(const Opts& op, const SchemeK& sk) {
+    return !sk.despread && !op.stage_split && (sk.NP == 8 || sk.NP == 16 || sk.NP == 32) && sk.M <= 256 &&
+           sk.nI <= 16 && sk.nQ <= 16;
 }
 
-bool perfect_fusable(const SchemeK& sk) {
-    const char* e = getenv("DSCE_PFUSE");
-    return stage_fused_ok(sk) && sk.p_diag && !(e && e[0] == '0');
-}
+bool perfect_fusable(const Opts& op, const SchemeK& sk) { return stage_fused_ok(op, sk) && sk.p_diag && op.pfuse; }
 
-void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, int var, int n_iter, bool last,
-                  McBuffers& b, unsigned long long* counters, int scheme_index, bool trace, bool perfect) {
+unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
+                      int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
+                      bool perfect) {
     StageArgs st;
     st.perfect = perfect ? 1 : 0;
     st.stage = stage;
@@ -2695,29 +2450,27 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
     st.nstage = n_iter + 1;
     st.scheme = scheme_index;
     st.last = last ? 1 : 0;
-    st.trace = trace ? 1 : 0;
+    st.tr = b.tr;
     st.R = b.R;
     st.U = b.U;
     st.snr0 = b.snr0;
-    st.xcd_order = 0;
+    st.xcd_order = op.xcd;
     st.ysrc_e = stage == 0 ? b.y : b.yest;
     st.ysrc_p = stage == 0 ? b.y : b.yperf;
     st.mse_err = b.mse_err;
     st.mse_pow = b.mse_pow;
     const int rblk = (sk.LK + DSCE_RB - 1) / DSCE_RB;
-    // select-mode schemes: k_ls + one fused pass (DSCE_STAGE=split keeps the
-    // 3-kernel path for A/B; DSCE_STAGE_RB = rows per fused block, 4 | 8 | 16)
-    if (stage_fused_ok(sk)) {
-        const char* e = getenv("DSCE_STAGE_RB");
-        const int rb = e ? atoi(e) : 8;
+    // select-mode schemes: k_ls + one fused pass (Opts::stage_split keeps the
+    // 3-kernel path; Opts::stage_rb = rows per wave of the fused pass, 4 | 8 | 16)
+    if (stage_fused_ok(op, sk)) {
         hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);
-        if (sk.NP == 8) launch_stage_fused_np<8>(s, sk, st, mm, b, counters, rb);
-        else if (sk.NP == 16) launch_stage_fused_np<16>(s, sk, st, mm, b, counters, rb);
-        else launch_stage_fused_np<32>(s, sk, st, mm, b, counters, rb);
+        if (sk.NP == 8) launch_stage_fused_np<8>(s, sk, st, mm, b, counters, op.stage_rb);
+        else if (sk.NP == 16) launch_stage_fused_np<16>(s, sk, st, mm, b, counters, op.stage_rb);
+        else launch_stage_fused_np<32>(s, sk, st, mm, b, counters, op.stage_rb);
         if (!last && !sk.p_diag)
             hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v,
                                b.u);
-        return;
+        return PATH_STAGE_FUSED;
     }
     hipLaunchKernelGGL(k_ls_hest, dim3(b.U / WAVE, rblk), dim3(WAVE), (size_t)sk.NP * WAVE * sizeof(double2), s, sk,
                        st, mm.Wd, b.xp, b.h, b.hp, b.hest, b.e, b.e2);
@@ -2725,6 +2478,7 @@ void launch_stage(hipStream_t s, const SchemeK& sk, const MmseK& mm, int stage, 
                        b.sidx, b.e, b.e2, b.qe, b.qp, counters);
     if (!last)
         hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v, b.u);
+    return PATH_STAGE_SPLIT;
 }
 
 // MMSE one-tap channel h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p for n LS

@@ -359,12 +359,10 @@ __global__ void k_wpair_pack(Band Wb, int NP, const double2* __restrict__ w, lon
 }
 
 // 3M planes of the pair tiles: per (tile, k-step) the 64 lanes' Re, Im and
-// Re+Im as three contiguous 64-double rows (k_wpair's Gauss/Karatsuba form).
-// x4 (MmseK::w3x4): the planes of two consecutive k-steps interleaved per lane,
-// [tile][k-step pair][plane][lane][2], so k_wpair3 fetches them with 16-byte
-// loads — half the load instructions of one double per lane and plane.
-__global__ void k_wpair_pack3(long long wp_elems, int nks, int x4, const double2* __restrict__ wp,
-                              double* __restrict__ w3) {
+// Re+Im (k_wpair3's Gauss/Karatsuba form), the planes of two consecutive
+// k-steps interleaved per lane, [tile][k-step pair][plane][lane][2], so
+// k_wpair3 fetches them with 16-byte loads.  nks is even (2, 4 or 8).
+__global__ void k_wpair_pack3(long long wp_elems, int nks, const double2* __restrict__ wp, double* __restrict__ w3) {
     const long long n = wp_elems;
     const double2* __restrict__ src = wp + (size_t)blockIdx.y * wp_elems;
     double* __restrict__ dst = w3 + (size_t)blockIdx.y * 3 * wp_elems;
@@ -372,13 +370,8 @@ __global__ void k_wpair_pack3(long long wp_elems, int nks, int x4, const double2
         const double2 v = src[e];
         const long long g = e / 64, l = e % 64;
         const double pv[3] = {v.x, v.y, v.x + v.y};
-        if (x4) {
-            const long long t = g / nks, ks = g % nks;
-            for (int pl = 0; pl < 3; ++pl)
-                dst[((t * (nks / 2) + ks / 2) * 3 + pl) * 128 + 2 * l + (ks & 1)] = pv[pl];
-        } else {
-            for (int pl = 0; pl < 3; ++pl) dst[(g * 3 + pl) * 64 + l] = pv[pl];
-        }
+        const long long t = g / nks, ks = g % nks;
+        for (int pl = 0; pl < 3; ++pl) dst[((t * (nks / 2) + ks / 2) * 3 + pl) * 128 + 2 * l + (ks & 1)] = pv[pl];
     }
 }
 
@@ -426,10 +419,9 @@ void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const doub
 }
 
 void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long long w_elems, const PairBand& P,
-                 double2* wp, long long wp_elems, int nslices, double* w3, int w3x4) {
+                 double2* wp, long long wp_elems, int nslices, double* w3) {
     hipLaunchKernelGGL(k_wpair_pack, dim3(Wb.nblk, nslices), dim3(256), 0, s, Wb, NP, w, w_elems, P, wp, wp_elems);
-    if (w3)
-        hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, P.nks, w3x4, wp, w3);
+    if (w3) hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, P.nks, wp, w3);
 }
 
 // G[n, l + L k] in closed form (OFDM.m:153-165, :184-203; FBMC.m:255-285,
@@ -482,6 +474,38 @@ __global__ void k_tx_matrix(TxDesc d, const double* __restrict__ proto, double2*
 
 void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q) {
     hipLaunchKernelGGL(k_tx_matrix, dim3(4096), dim3(256), 0, s, d, proto, G, Q);
+}
+
+}  // namespace dsce
+
+namespace dsce {
+
+// ---------------------------------------------------------------------------
+// Measured FP64 matrix-core peak (the roofline denominator next to the 78.6 TF
+// spec, which the microarchitecture guide does not list as measured): every
+// wave issues back-to-back v_mfma_f64_16x16x4_f64 on NACC independent
+// accumulators (no dependent-latency stalls), 2048 flops each.
+// ---------------------------------------------------------------------------
+typedef double pk4 __attribute__((ext_vector_type(4)));
+static constexpr int PEAK_NACC = PEAK_MFMA_PER_ITER;
+
+__global__ void __launch_bounds__(256) k_mfma_f64_peak(int iters, double seed, double* __restrict__ out) {
+    pk4 acc[PEAK_NACC];
+#pragma unroll
+    for (int k = 0; k < PEAK_NACC; ++k) acc[k] = (pk4){0.0, 0.0, 0.0, 0.0};
+    const double a = seed + 1e-3 * (threadIdx.x & 63), b = 1.0 - 1e-3 * (threadIdx.x & 7);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < PEAK_NACC; ++k) acc[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[k], 0, 0, 0);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < PEAK_NACC; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+void launch_mfma_f64_peak(hipStream_t s, int blocks, int iters, double* out) {
+    hipLaunchKernelGGL(k_mfma_f64_peak, dim3(blocks), dim3(256), 0, s, iters, 0.5, out);
 }
 
 }  // namespace dsce

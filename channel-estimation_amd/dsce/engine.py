@@ -21,8 +21,17 @@ EXPORTED = [
     "dsce_set_channel", "dsce_set_snr", "dsce_add_scheme", "dsce_build_mmse", "dsce_set_batch", "dsce_run",
     "dsce_bits_per_rep", "dsce_channel_realise", "dsce_get_correlation", "dsce_get_W", "dsce_trace_unit",
     "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
-    "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse",
+    "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse", "dsce_trace_unit_ex",
+    "dsce_scheme_dims", "dsce_path_info", "dsce_set_option", "dsce_get_option", "dsce_fp64_mfma_peak",
 ]
+
+ABI_VERSION = 3
+
+# dsce_path_info bits (include/dsce.h DSCE_PATH_*)
+PATH_BITS = {
+    "wpair3_fused": 1 << 0, "wpair3": 1 << 1, "wpair4m": 1 << 2, "wcontract_valu": 1 << 3, "pic_mfma": 1 << 4,
+    "pic_chain": 1 << 5, "pic_passes": 1 << 6, "stage_fused": 1 << 7, "stage_split": 1 << 8, "noise_fused": 1 << 9,
+}
 
 
 class ChannelDesc(C.Structure):
@@ -40,6 +49,19 @@ class SchemeDesc(C.Structure):
                 ("P", C.POINTER(C.c_double)), ("pilot_pos", C.POINTER(C.c_int32)),
                 ("data_pos", C.POINTER(C.c_int32)), ("considered", C.POINTER(C.c_uint8)),
                 ("symbols", C.POINTER(C.c_double))]
+
+
+class Dims(C.Structure):
+    _fields_ = [("n_samples", C.c_int32), ("n_taps", C.c_int32), ("lk", C.c_int32), ("n_pilots", C.c_int32),
+                ("n_data", C.c_int32), ("n_tx_symbols", C.c_int32), ("n_schemes", C.c_int32), ("n_snr", C.c_int32),
+                ("n_iter", C.c_int32), ("n_counters", C.c_int64)]
+
+
+class Trace(C.Structure):
+    _fields_ = [("y", C.POINTER(C.c_double)), ("h_perfect", C.POINTER(C.c_double)),
+                ("hp_stages", C.POINTER(C.c_double)), ("hest_stages", C.POINTER(C.c_double)),
+                ("yest_stages", C.POINTER(C.c_double)), ("yperf_stages", C.POINTER(C.c_double)),
+                ("dec_est", C.POINTER(C.c_int32)), ("dec_perf", C.POINTER(C.c_int32))]
 
 
 class TxDesc(C.Structure):
@@ -93,6 +115,12 @@ def load_library(path=None):
     lib.dsce_set_interpolation.argtypes = [vp, C.c_int32, dp]
     lib.dsce_enable_mse.argtypes = [vp, C.c_int32]
     lib.dsce_get_mse.argtypes = [vp, dp, dp]
+    lib.dsce_trace_unit_ex.argtypes = [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32, C.POINTER(Trace)]
+    lib.dsce_scheme_dims.argtypes = [vp, C.c_int32, C.POINTER(Dims)]
+    lib.dsce_path_info.argtypes = [vp, C.c_int32, C.POINTER(C.c_uint32)]
+    lib.dsce_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
+    lib.dsce_get_option.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int64)]
+    lib.dsce_fp64_mfma_peak.argtypes = [vp, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -272,16 +300,45 @@ class Engine:
         return out.view(np.complex128)
 
     def trace_unit(self, sid, seed, rep, snr_index):
-        sc = self.schemes[sid]
-        ns = self.niter + 1
-        y = np.zeros(2 * sc.LK)
-        hp = np.zeros(2 * ns * sc.n_pilots)
-        he = np.zeros(2 * ns * sc.LK)
-        h = np.zeros(2 * sc.LK)
-        self._chk(self.lib.dsce_trace_unit(self.h, int(sid), int(seed), int(rep), int(snr_index), _dptr(y),
-                                           _dptr(hp), _dptr(he), _dptr(h)), "dsce_trace_unit")
+        """Every stage of one (rep, SNR) unit through the same kernels as run()
+        (dsce_trace_unit_ex): y, h (= diag D), and per stage hp (LS pilots), hest
+        (diag D_hat), yest / yperf (IC inputs; row 0 = y) and the detected symbol
+        indices dec_e / dec_p (-1 where the path forms no decision)."""
+        d = self.scheme_dims(sid)
+        ns, LK, NP, ND = d.n_iter + 1, d.lk, d.n_pilots, d.n_data
+        bufs = dict(y=np.zeros(2 * LK), h=np.zeros(2 * LK), hp=np.zeros(2 * ns * NP), hest=np.zeros(2 * ns * LK),
+                    yest=np.zeros(2 * ns * LK), yperf=np.zeros(2 * ns * LK))
+        dec_e = np.zeros(ns * ND, dtype=np.int32)
+        dec_p = np.zeros(ns * ND, dtype=np.int32)
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))
+        t = Trace(_dptr(bufs["y"]), _dptr(bufs["h"]), _dptr(bufs["hp"]), _dptr(bufs["hest"]), _dptr(bufs["yest"]),
+                  _dptr(bufs["yperf"]), ip(dec_e), ip(dec_p))
+        self._chk(self.lib.dsce_trace_unit_ex(self.h, int(sid), int(seed), int(rep), int(snr_index), C.byref(t)),
+                  "dsce_trace_unit_ex")
         v = lambda a: a.view(np.complex128)
-        return dict(y=v(y), hp=v(hp).reshape(ns, sc.n_pilots), hest=v(he).reshape(ns, sc.LK), h=v(h))
+        return dict(y=v(bufs["y"]), h=v(bufs["h"]), hp=v(bufs["hp"]).reshape(ns, NP),
+                    hest=v(bufs["hest"]).reshape(ns, LK), yest=v(bufs["yest"]).reshape(ns, LK),
+                    yperf=v(bufs["yperf"]).reshape(ns, LK), dec_e=dec_e.reshape(ns, ND), dec_p=dec_p.reshape(ns, ND))
+
+    # -- engine state ------------------------------------------------------------
+    def scheme_dims(self, sid):
+        d = Dims()
+        self._chk(self.lib.dsce_scheme_dims(self.h, int(sid), C.byref(d)), "dsce_scheme_dims")
+        return d
+
+    def path_info(self, sid):
+        """Names of the kernel paths the scheme's last run / trace went through."""
+        f = C.c_uint32()
+        self._chk(self.lib.dsce_path_info(self.h, int(sid), C.byref(f)), "dsce_path_info")
+        return {k for k, bit in PATH_BITS.items() if f.value & bit}
+
+    def set_option(self, name, value):
+        self._chk(self.lib.dsce_set_option(self.h, name.encode(), int(value)), "dsce_set_option(%s)" % name)
+
+    def get_option(self, name):
+        v = C.c_int64()
+        self._chk(self.lib.dsce_get_option(self.h, name.encode(), C.byref(v)), "dsce_get_option(%s)" % name)
+        return v.value
 
     def mmse_onetap(self, sid, snr_index, hp_ls, variant=0):
         """h_hat = diag(sum_p W_p hP_p) for LS vectors hp_ls (NP,) or (NP, n)."""
@@ -321,6 +378,12 @@ class Engine:
         self._chk(self.lib.dsce_kernel_time(self.h, name.encode(), C.byref(n), C.byref(ms)), "dsce_kernel_time")
         return n.value, ms.value
 
+    def fp64_mfma_peak(self):
+        """Measured FP64 matrix-core peak of this GPU, TFLOP/s (dsce_fp64_mfma_peak)."""
+        t = C.c_double()
+        self._chk(self.lib.dsce_fp64_mfma_peak(self.h, C.byref(t)), "dsce_fp64_mfma_peak")
+        return t.value
+
     def work_model(self, sid):
         cm = C.c_double()
         wb = C.c_double()
@@ -328,9 +391,12 @@ class Engine:
         return cm.value, wb.value
 
 
-def build_engine(setup, schemes=None, device=0, zero_threshold=None, batch=None):
-    """Engine configured like the script: channel, SNR list, schemes, MMSE setup."""
+def build_engine(setup, schemes=None, device=0, zero_threshold=None, batch=None, options=None):
+    """Engine configured like the script: channel, SNR list, schemes, MMSE setup.
+    ``options``: dsce_set_option name -> value, applied before the MMSE build."""
     eng = Engine(device)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
     eng.set_channel(setup.channel)
     eng.set_snr(setup.pn_time, setup.n_iter)
     names = list(setup.schemes) if schemes is None else list(schemes)

@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 2
+#define DSCE_ABI_VERSION 3
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
@@ -149,6 +149,49 @@ typedef struct {
     double rx_scale;            /* GetRXMatrix scale (OFDM L F/SR, FBMC L/(SR T)) */
     const double* prototype;    /* FBMC PrototypeFilter.TimeDomain (proto_len) */
 } dsce_tx_desc;
+
+/* Dimensions of a configured scheme, so a binding sizes every output from the
+ * engine's own state (dsce_scheme_dims).  n_counters = length of dsce_run's
+ * err_counts (all schemes). */
+typedef struct {
+    int32_t n_samples;          /* N                                          */
+    int32_t n_taps;             /* length of the sampled PDP (ImpulseResponse columns) */
+    int32_t lk;                 /* L * K                                      */
+    int32_t n_pilots;           /* NP                                         */
+    int32_t n_data;             /* ND                                         */
+    int32_t n_tx_symbols;       /* NP + ND                                    */
+    int32_t n_schemes;
+    int32_t n_snr;
+    int32_t n_iter;
+    int64_t n_counters;
+} dsce_dims;
+
+/* Per-stage trace of one unit (dsce_trace_unit_ex).  Every pointer is optional
+ * (null: not returned).  Complex buffers interleaved; "stage" s = 0 one-tap,
+ * s = i IC iteration i; (1 + n_iter) rows, each LK (or NP / ND) long. */
+typedef struct {
+    double* y;                  /* LK: y = Q'r                                    script:406-409 */
+    double* h_perfect;          /* LK: diag(D), D = Q'HG                           script:388-393 */
+    double* hp_stages;          /* (1+n_iter) x NP: LS pilot estimates             script:412-414, :487-489 */
+    double* hest_stages;        /* (1+n_iter) x LK: diag(D_hat)                    script:417-428, :493-515 */
+    double* yest_stages;        /* (1+n_iter) x LK: y_est = y - (D_hat - diag) v   script:482-484 (row 0 = y) */
+    double* yperf_stages;       /* (1+n_iter) x LK: y_perf = y - (D - diag h) u    script:541-543 (row 0 = y;
+                                   data rows only on the fused perfect-CSI paths) */
+    int32_t* dec_est;           /* (1+n_iter) x ND: detected symbol index, MMSE    script:431, :527 */
+    int32_t* dec_perf;          /* (1+n_iter) x ND: detected symbol index, perfect script:453, :548 */
+} dsce_trace;
+
+/* Kernel paths (dsce_path_info) */
+#define DSCE_PATH_WPAIR3_FUSED    (1u << 0)   /* k_pilot_pre + k_wpair3 with the MMSE stage in its epilogue */
+#define DSCE_PATH_WPAIR3          (1u << 1)   /* k_wpair3: MFMA pair-tile contraction, 3M products        */
+#define DSCE_PATH_WPAIR4M         (1u << 2)   /* k_wpair: pair tiles, 4 real MFMAs per complex product     */
+#define DSCE_PATH_WCONTRACT_VALU  (1u << 3)   /* k_wcontract_valu                                         */
+#define DSCE_PATH_PIC_MFMA        (1u << 4)   /* k_pic_mfma: perfect-CSI IC chain on the matrix cores      */
+#define DSCE_PATH_PIC_CHAIN       (1u << 5)   /* k_pic_chain: perfect-CSI IC chain on the VALU             */
+#define DSCE_PATH_PIC_PASSES      (1u << 6)   /* perfect-CSI IC as two banded passes per iteration         */
+#define DSCE_PATH_STAGE_FUSED     (1u << 7)   /* k_ls + k_stage_fused                                      */
+#define DSCE_PATH_STAGE_SPLIT     (1u << 8)   /* k_ls_hest + k_detect + k_precode                          */
+#define DSCE_PATH_NOISE_FUSED     (1u << 9)   /* AWGN drawn inside the Q^H pass                            */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -227,16 +270,39 @@ int dsce_trace_unit(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t re
 int dsce_enable_mse(dsce_ctx* ctx, int32_t enable);
 int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum);
 
+/* Same kernels as dsce_run (a 64-realisation batch starting at `rep`, the traced
+ * unit at its lane 0), with every stage's intermediate quantities of one
+ * (rep, snr) unit returned through `out` (see dsce_trace). */
+int dsce_trace_unit_ex(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t rep, int32_t snr_index,
+                       const dsce_trace* out);
+
+/* ---- engine state ------------------------------------------------------- */
+int dsce_scheme_dims(dsce_ctx* ctx, int32_t scheme_id, dsce_dims* dims);
+/* Which kernels a scheme's last dsce_run / trace used: DSCE_PATH_* bits. */
+int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
+/* Kernel-selection options (defaults = the measured-best path; for A/B runs and
+ * tests): xcd, fuse_stage, wpair_3m (-1 auto), wda_3m, pic_chain (0 passes,
+ * 1 VALU chain, 2 MFMA chain), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
+ * snr_chunk (0 all), streams (1|2), jakes_rpw (1|2), wtrim (read by
+ * dsce_build_mmse), wcontract_valu.  Unknown names return DSCE_EINVAL. */
+int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);
+int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
+
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, dsce_run records HIP events around every launch of each kernel
  * on the context's stream; dsce_kernel_time returns (launches, total ms). */
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
 /* Algorithmic work of one realisation of a scheme (support-aware): complex
- * multiply-accumulates of the MMSE contraction kernel (including, when the MMSE
- * stage is fused into it, the diag(D_hat) = Wd hP products) and the number of W
- * bytes streamed per contraction launch. */
+ * multiply-accumulates of the MMSE contraction kernel over W's off-diagonal
+ * (row, column) pairs (including, when the last dsce_run fused the MMSE stage
+ * into it, the diag(D_hat) = Wd hP products) and the number of W bytes streamed
+ * per contraction launch. */
 int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per_rep, double* w_bytes_per_snr);
+/* Measured FP64 matrix-core peak of the context's GPU: back-to-back
+ * v_mfma_f64_16x16x4_f64 on independent accumulators, 8 waves per SIMD,
+ * best of 3 timed launches (TFLOP/s). */
+int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops);
 
 #ifdef __cplusplus
 }

@@ -330,6 +330,10 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                     trace.setdefault("hest0", []).append(hest)
                     trace.setdefault("hp_stages", []).append([hP])
                     trace.setdefault("hest_stages", []).append([hest])
+                    # per (rep, SNR) unit, every stage: the quantities dsce_trace_unit_ex returns
+                    unit = dict(rep=rep, snr=isnr, y=y, h=h, hp=[hP], hest=[hest], yest=[y], yperf=[y],
+                                dec_e=[idx], dec_p=[idxp], margin_e=[mg], margin_p=[mgp])
+                    trace.setdefault("units", []).append(unit)
                 Dt = Dest
                 ht = hest
                 for it in range(1, n_iter + 1):
@@ -357,6 +361,9 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                         trace.setdefault("ypc", []).append(ypc)
                         trace["hp_stages"][-1].append(hPt)
                         trace["hest_stages"][-1].append(ht)
+                        for key, val in (("hp", hPt), ("hest", ht), ("yest", yic), ("yperf", ypc), ("dec_e", idx),
+                                         ("dec_p", idxp), ("margin_e", mg), ("margin_p", mgp)):
+                            unit[key].append(val)
     return dict(err=err, borderline=border, nbits=nbits, mse_err=mse_err, mse_pow=mse_pow)
 
 

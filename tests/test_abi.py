@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     from dsce import engine
     lib = engine.load_library()
-    assert lib.dsce_abi_version() == 2
+    assert lib.dsce_abi_version() == engine.ABI_VERSION
 
 
 def test_struct_layout_matches_c(tmp_path):
@@ -40,16 +40,19 @@ def test_struct_layout_matches_c(tmp_path):
 
     from dsce import engine
     src = tmp_path / "l.c"
-    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dsce.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dsce.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu '
+                   '%zu %zu %zu %zu\\n",'
                    'sizeof(dsce_channel_desc), sizeof(dsce_scheme_desc), offsetof(dsce_scheme_desc, kappa),'
                    'offsetof(dsce_scheme_desc, G), offsetof(dsce_scheme_desc, symbols), sizeof(dsce_tx_desc),'
-                   'offsetof(dsce_tx_desc, norm));return 0;}\n')
+                   'offsetof(dsce_tx_desc, norm), sizeof(dsce_dims), offsetof(dsce_dims, n_counters),'
+                   'sizeof(dsce_trace), offsetof(dsce_trace, dec_perf));return 0;}\n')
     exe = tmp_path / "l"
     subprocess.run(["gcc", "-I", os.path.dirname(HDR), str(src), "-o", str(exe)], check=True)
     c = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     py = [ctypes.sizeof(engine.ChannelDesc), ctypes.sizeof(engine.SchemeDesc), engine.SchemeDesc.kappa.offset,
           engine.SchemeDesc.G.offset, engine.SchemeDesc.symbols.offset, ctypes.sizeof(engine.TxDesc),
-          engine.TxDesc.norm.offset]
+          engine.TxDesc.norm.offset, ctypes.sizeof(engine.Dims), engine.Dims.n_counters.offset,
+          ctypes.sizeof(engine.Trace), engine.Trace.dec_perf.offset]
     assert c == py
 
 

@@ -40,3 +40,19 @@ def test_simulate_two_ranks_equals_one(tmp_path):
     assert np.array_equal(np.array(a["counts"]), np.array(b["counts"]))
     for s in ("ofdm", "fbmc_aux"):
         np.testing.assert_allclose(np.array(a["nmse"][s]), np.array(b["nmse"][s]), rtol=1e-12)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """bench.py --gpus 2 without a launcher starts torch.distributed.run itself
+    (one rank per GPU; here both ranks share the one GPU over gloo) and forwards
+    rank 0's JSON line, which reports both ranks' realisations."""
+    env = dict(os.environ, DSCE_DIST_BACKEND="gloo")
+    out = subprocess.run([sys.executable, os.path.join(harness.ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                          "--warmup", "1", "--reps-per-step", "1024", "--no-cpu-baseline"], env=env, check=True,
+                         timeout=300, capture_output=True, text=True)
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["value"] > 0
+    bad = subprocess.run([sys.executable, os.path.join(harness.ROOT, "bench.py"), "--gpus", "2"],
+                         env=dict(env, WORLD_SIZE="1"), timeout=120, capture_output=True, text=True)
+    assert bad.returncode != 0

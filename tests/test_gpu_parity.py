@@ -129,10 +129,10 @@ def test_fbmc_estimator_and_trace(fbmc):
                     trace=tr)
     for k in range(2):
         g = eng.trace_unit(0, SEED, 9, k)
-        np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
-        for st in range(S.n_iter + 1):
-            np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
-            np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
+        u = tr["units"][k]
+        ns = _check_trace(g, u, "%s snr %d" % (name, k))
+        for st in range(1, ns):        # unfused perfect-CSI passes: y_perf of every row
+            np.testing.assert_allclose(g["yperf"][st], u["yperf"][st], rtol=0, atol=1e-9)
 
 
 def test_fbmc_error_counts(fbmc):
@@ -203,14 +203,12 @@ def test_psace_mmse_plugin(ofdm):
     np.testing.assert_allclose(got.reshape(-1, order="F"), ref, rtol=0, atol=1e-11 * np.abs(ref).max())
 
 
-def test_w_band_trim_is_bit_exact(monkeypatch):
+def test_w_band_trim_is_bit_exact():
     """Trimming W to its non-zero column extent (after the 1e-8 threshold) skips
     exact zeros only: counts are bit-identical and the contracted work shrinks."""
     from dsce.engine import build_engine
     S = build_setup("default", schemes=("fbmc_aux",), snr_db=[20.0, 40.0])
-    monkeypatch.setenv("DSCE_WTRIM", "0")
-    full = build_engine(S, batch=128)
-    monkeypatch.setenv("DSCE_WTRIM", "1")
+    full = build_engine(S, batch=128, options={"wtrim": 0})
     trim = build_engine(S, batch=128)
     np.testing.assert_array_equal(full.run(SEED, 0, 128), trim.run(SEED, 0, 128))
     for k in range(2):
@@ -221,58 +219,118 @@ def test_w_band_trim_is_bit_exact(monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["ofdm", "fbmc_aux"])
-def test_stage_variants_agree(monkeypatch, name):
-    """The fused select-mode stage (k_ls + k_stage_fused, any row-block size,
-    perfect-CSI branch fused into perfect_ic or not, any work order) and the
-    3-kernel split path (k_ls_hest, k_detect, k_precode) differ only in rounding
-    of the one-tap quotient: identical counts on 1024 realisations."""
+def test_stage_variants_agree(name):
+    """Every kernel option (dsce_set_option) gives identical counts on 1024
+    realisations: the fused select-mode stage vs the 3-kernel split path (any
+    row-block size), perfect-CSI detection fused into the second pass or not,
+    XCD-aware work order on/off, SNR-chunked receiver, two streams, 4-MFMA
+    instead of 3M complex products, the VALU contraction, the MMSE stage as its
+    own kernels instead of fused into the contraction, the perfect-CSI chain as
+    per-iteration passes / VALU chain instead of k_pic_mfma, the fused
+    epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave."""
     from dsce.engine import build_engine
     S = build_setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = build_engine(S, batch=512)
-    monkeypatch.setenv("DSCE_STAGE", "split")
+    eng.set_option("stage_split", 1)
     ref = eng.run(SEED, 0, 1024)
-    monkeypatch.setenv("DSCE_STAGE", "fused")
-    for rb in ("4", "8", "16"):
-        monkeypatch.setenv("DSCE_STAGE_RB", rb)
-        np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=rb)
-    # perfect-CSI detection fused into perfect_ic (OFDM) on/off, XCD-aware
-    # work order on/off, SNR-chunked receiver, two streams instead of one, the
-    # one-pass perfect-CSI IC (k_pic) instead of the two passes, 4-MFMA instead of
-    # 3M complex products, 32-row contraction tiles instead of pairs, the MMSE
-    # stage as its own kernels instead of fused into the contraction, the
-    # perfect-CSI chain as per-iteration passes / VALU chain instead of k_pic_mfma,
-    # the fused epilogue's diag(D_hat) with 4 real MFMAs instead of 3M, one
-    # realisation per Jakes wave (17- vs 9-sample recurrence chunks), the fused
-    # contraction held to 3 waves/SIMD
-    variants = ({"DSCE_PFUSE": "0"}, {"DSCE_XCD": "0"}, {"DSCE_SNR_CHUNK": "2"}, {"DSCE_STREAMS": "2"},
-                {"DSCE_PIC": "1", "DSCE_PIC_CHAIN": "0"}, {"DSCE_WPAIR_3M": "0"}, {"DSCE_WCONTRACT": "mfma"},
-                {"DSCE_FUSE_STAGE": "0"}, {"DSCE_PIC_CHAIN": "0"}, {"DSCE_PIC_CHAIN": "1"},
-                {"DSCE_STREAMS": "2", "DSCE_FUSE_STAGE": "0"}, {"DSCE_NOISE_FUSE": "0"}, {"DSCE_WDA_3M": "0"},
-                {"DSCE_JAKES_RPW": "1"}, {"DSCE_WPAIR_3W": "1"}, {"DSCE_WPAIR_3W": "1", "DSCE_WDA_3M": "0"})
+    assert "stage_split" in eng.path_info(0)
+    eng.set_option("stage_split", 0)
+    for rb in (4, 8, 16):
+        eng.set_option("stage_rb", rb)
+        np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(rb))
+    eng.set_option("stage_rb", 8)
+    variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2}, {"streams": 2}, {"wpair_3m": 0},
+                {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1},
+                {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1})
     for env in variants:
-        for var, val in env.items():
-            monkeypatch.setenv(var, val)
+        old = {k: eng.get_option(k) for k in env}
+        for k, v in env.items():
+            eng.set_option(k, v)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(env))
-        for var in env:
-            monkeypatch.delenv(var)
+        for k, v in old.items():
+            eng.set_option(k, v)
     eng.close()
 
 
-def test_w3_layouts_agree(monkeypatch):
-    """W's 3M planes packed two k-steps per 16-byte lane load (default) or one
-    double per lane (DSCE_W3_X4=0, chosen when the estimator is built): the
-    contraction reads the same values, counts are identical, fused and unfused."""
-    from dsce.engine import build_engine
-    S = build_setup("default", schemes=("ofdm",), snr_db=[10.0, 25.0, 40.0])
-    x4 = build_engine(S, batch=512)
-    monkeypatch.setenv("DSCE_W3_X4", "0")
-    x2 = build_engine(S, batch=512)
-    monkeypatch.delenv("DSCE_W3_X4")
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("DSCE_FUSE_STAGE", fuse)
-        np.testing.assert_array_equal(x4.run(SEED, 0, 1024), x2.run(SEED, 0, 1024), err_msg=fuse)
-    x4.close()
-    x2.close()
+def test_options_are_validated():
+    from dsce.engine import DsceError, Engine
+    eng = Engine()
+    with pytest.raises(DsceError):
+        eng.set_option("no_such_option", 1)
+    with pytest.raises(DsceError):
+        eng.set_option("stage_rb", 5)
+    assert eng.get_option("fuse_stage") == 1
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
+# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_mfma for
+# the perfect-CSI IC chain, k_stage_fused for the one-tap stage).
+# ---------------------------------------------------------------------------
+BENCH_PATH = {"wpair3_fused", "pic_mfma", "stage_fused", "noise_fused"}
+
+
+def _check_trace(g, u, name, rtol_ulp=1e-9):
+    """Per element, per stage: |gpu - oracle| <= 1e-9 for y, hP, diag(D_hat),
+    y_est (all rows) and y_perf (data rows: the fused perfect-CSI chain forms
+    only those); decisions identical except where the oracle's nearest-point
+    margin is below 1e-9 (borderline, none expected)."""
+    ns = len(u["hp"])
+    np.testing.assert_allclose(g["y"], u["y"], rtol=0, atol=1e-10, err_msg=name)
+    np.testing.assert_allclose(g["h"], u["h"], rtol=0, atol=1e-10, err_msg=name)
+    for st in range(ns):
+        np.testing.assert_allclose(g["hp"][st], u["hp"][st], rtol=0, atol=rtol_ulp, err_msg="%s hp %d" % (name, st))
+        np.testing.assert_allclose(g["hest"][st], u["hest"][st], rtol=0, atol=rtol_ulp,
+                                   err_msg="%s hest %d" % (name, st))
+        np.testing.assert_allclose(g["yest"][st], u["yest"][st], rtol=0, atol=rtol_ulp,
+                                   err_msg="%s yest %d" % (name, st))
+        for key, mk in (("dec_e", "margin_e"), ("dec_p", "margin_p")):
+            ok = (g[key][st] == u[key][st]) | (u[mk][st] < 1e-9)
+            assert ok.all(), (name, key, st, np.flatnonzero(~ok)[:8])
+    return ns
+
+
+def _data_rows(sc):
+    return np.asarray(sc.data_pos) if not sc.despread else None
+
+
+def test_bench_kernels_trace_matches_oracle(ofdm):
+    """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
+    dsce_path_info) and every intermediate of every stage of a unit matches the
+    oracle: the fused contraction's y_est and diag(D_hat), k_pilot_pre's LS
+    pilots, k_pic_mfma's y_perf and both branches' decisions."""
+    S, eng, mm = ofdm
+    sc = S.schemes["ofdm"]
+    rows = _data_rows(sc)
+    for rep in (5, 70):
+        tr = {}
+        refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
+                        [mm], trace=tr)
+        for k in range(len(S.pn_time)):
+            g = eng.trace_unit(0, SEED, rep, k)
+            assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+            u = tr["units"][k]
+            ns = _check_trace(g, u, "rep %d snr %d" % (rep, k))
+            for st in range(1, ns):
+                np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
+
+
+def test_bench_path_counts_match_oracle(ofdm):
+    """Error counts through the bench path at a shape where every fast kernel
+    is eligible (asserted), 128 realisations x 7 SNR points, and at an odd
+    shape (64 realisations: 7 x 14 blocks of the perfect-CSI chain, not a
+    multiple of the 8 XCDs)."""
+    S, eng, mm = ofdm
+    sc = S.schemes["ofdm"]
+    for first, n in ((128, 128), (320, 64)):
+        eng.set_batch(n)
+        cg = eng.run(SEED, first, n)
+        assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+        res = refsim.simulate(SEED, first, n, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time,
+                              S.n_iter, [mm])
+        assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (first, cg - res["err"])
+    eng.set_batch(256)
 
 
 @pytest.mark.parametrize("name", ["default", "c5", "paper"])
