@@ -1,0 +1,104 @@
+"""CPU: the oracle's own restatement of the setup producers (oracle/setup.py)
+against (i) the reference's structural statements and (ii) the product's host
+mirror (channel-estimation_amd/dsce), which it replaces as the oracle's input:
+a bug in either would now show up here instead of being shared by both sides
+of every GPU parity test."""
+import numpy as np
+import pytest
+
+import harness  # noqa: F401  (sys.path)
+from oracle import setup as osu
+
+
+@pytest.fixture(scope="module")
+def both():
+    from dsce.configs import build_setup
+    return osu.script_setup("default"), build_setup("default")
+
+
+def test_matlab_semantics_helpers():
+    np.testing.assert_array_equal(osu.mround([0.5, 1.5, 2.5, -0.5, -2.5, 2.4999]), [1, 2, 3, -1, -3, 2])
+    c = osu.colon(-1.0, 0.1, 0.95)
+    assert c.size == 20 and c[0] == -1.0 and abs(c[-1] - 0.9) < 1e-15
+    a = np.zeros((3, 2))
+    m = np.array([[True, False], [False, True], [True, True]])
+    np.testing.assert_array_equal(osu.logical_assign(a, m, [1, 2, 3, 4]), [[1, 0], [0, 3], [2, 4]])
+
+
+def test_ofdm_structure(both):
+    """Q'G = I (OFDM.m:205-218 zeroes only the CP columns; script:195) and
+    Demodulation(Modulation(x)) = Q' G x (OFDM.m:184-218 comments)."""
+    O, _ = both
+    of = O["ofdm"]
+    G, Q = of.tx_matrix(), of.rx_matrix().conj().T
+    np.testing.assert_allclose(Q.conj().T @ G, np.eye(G.shape[1]), atol=1e-12)
+    x = np.random.default_rng(1).standard_normal(G.shape[1]) + 0j
+    np.testing.assert_allclose(osu.col(of.demodulation(of.modulation(x))), Q.conj().T @ (G @ x), atol=1e-12)
+
+
+def test_fbmc_structure(both):
+    """Re(Q'G) = I for OQAM (FBMC.m:1-14: purely imaginary interference),
+    G x = Modulation(x) (FBMC.m:319-320) and GetFBMCMatrix = Demod(Mod(.))
+    (FBMC.m:356-357) = Q'G."""
+    O, _ = both
+    fb = O["fbmc"]
+    G, Q = fb.tx_matrix(), fb.rx_matrix().conj().T
+    D = Q.conj().T @ G
+    np.testing.assert_allclose(D.real, np.eye(D.shape[0]), atol=1e-7)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal(G.shape[1])
+    np.testing.assert_allclose(fb.modulation(x), G @ x, atol=1e-12)
+    np.testing.assert_allclose(fb.fbmc_matrix(), D, atol=1e-9)
+
+
+def test_precoders_cancel_pilot_interference(both):
+    """IIC.m:88-96 / :199-207: the precoded transmission D P has (almost) no
+    imaginary interference at the pilots; the power normalisation gives
+    ||P||_F^2 = LK (:86, :200)."""
+    O, _ = both
+    for key in ("fbmc_aux", "fbmc_cod"):
+        m = O["schemes"][key]["iic"]
+        assert np.all(m["SIR_dB"] > 30), (key, m["SIR_dB"].min())
+        assert abs(np.sum(np.abs(m["P"]) ** 2) - m["P"].shape[0]) < 1e-9
+    assert O["schemes"]["fbmc_aux"]["iic"]["NA"] == 64
+    assert O["schemes"]["fbmc_cod"]["n_data"] == 720 - 32
+
+
+@pytest.mark.parametrize("key", ["fbmc_aux", "fbmc_cod", "ofdm"])
+def test_product_host_mirror_equals_oracle_setup(both, key):
+    O, S = both
+    o, p = O["schemes"][key], S.schemes[key]
+    for f in ("G", "Q", "P"):
+        a, b = o[f], getattr(p, f)
+        assert a.shape == b.shape, (key, f)
+        np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max(), err_msg="%s %s" % (key, f))
+    for f, g in (("pilot_pos", "pilot_pos"), ("data_pos", "data_pos"), ("considered", "considered_symbols")):
+        np.testing.assert_array_equal(np.asarray(getattr(p, g)), np.asarray(o[f]), err_msg="%s %s" % (key, f))
+    for f in ("kappa", "data_div"):
+        assert abs(getattr(p, f) - o[f]) <= 1e-12 * abs(o[f]), (key, f)
+    assert (p.despread, p.real_detect, p.bits_slot, p.pilot_slot, p.n_data) == \
+        (o["despread"], o["real_detect"], o["bits_slot"], o["pilot_slot"], o["n_data"])
+    np.testing.assert_array_equal(p.const.SymbolMapping, o["symbols"])
+    np.testing.assert_array_equal(p.const.BitMapping.astype(np.uint8), o["bitmap"])
+
+
+def test_channel_and_sizes(both):
+    O, S = both
+    ch = S.channel
+    assert O["N"] == S.N == 540
+    np.testing.assert_array_equal(O["chan"]["idx_taps"], ch.IndexDelayTaps)
+    np.testing.assert_allclose(O["chan"]["pdp_norm"], ch.PowerDelayProfileNormalized, rtol=0, atol=1e-15)
+    np.testing.assert_allclose(O["pn_time"], S.pn_time, rtol=1e-15)
+    assert abs(O["chan"]["fD"] - ch.MaximumDopplerShift) < 1e-9
+
+
+def test_c5_sizes_and_mirror():
+    """C5 (48 x 30 at 720 kHz): N = 1080, LK 1440 / 672, NP = 32, 3 taps
+    (SURVEY §A1); OFDM operators equal the product mirror."""
+    from dsce.configs import build_setup
+    O = osu.script_setup("c5", schemes=("ofdm",))
+    S = build_setup("c5", schemes=("ofdm",))
+    assert O["N"] == 1080 and O["schemes"]["ofdm"]["G"].shape == (1080, 672)
+    assert len(O["schemes"]["ofdm"]["pilot_pos"]) == 32 and len(O["chan"]["idx_taps"]) == 3
+    for f in ("G", "Q", "P"):
+        np.testing.assert_allclose(getattr(S.schemes["ofdm"], f), O["schemes"]["ofdm"][f], rtol=0, atol=1e-13)
