@@ -80,14 +80,12 @@ def source_hash():
 def cpu_baseline_leg(seconds, workload):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import harness
-    from dsce.configs import build_setup
     from oracle import refsim
     name, schemes, _, _ = WORKLOADS[workload]
-    S = build_setup(name, schemes=schemes)
-    scs = [S.schemes[s] for s in schemes]
-    mm = [harness.oracle_mmse(S, sc) for sc in scs]             # setup, untimed
-    chan = harness.oracle_chan(S)
-    osc = [harness.oracle_scheme(sc) for sc in scs]
+    S = harness.setup(name, schemes=schemes)
+    mm = [harness.oracle_mmse(S, s) for s in schemes]              # setup, untimed
+    chan = S.chan
+    osc = [S.schemes[s] for s in schemes]
     refsim.simulate(SEED, 20_000_000, 1, chan, osc, S.pn_time, S.n_iter, mm)   # warm-up
     rates = []
     n_total = 0
@@ -138,7 +136,8 @@ def run_cpu_baseline(seconds, workload):
             return None
         legs[threads] = json.loads(out.stdout.strip().splitlines()[-1])
     med = {t: statistics.median(r["rates"]) for t, r in legs.items()}
-    return {"value": med[nt], "unit": "realisations/s", "cores": nt, "kind": "port",
+    best = max(med, key=med.get)          # the baseline is the faster of the two thread counts
+    return {"value": med[best], "unit": "realisations/s", "cores": best, "kind": "port",
             "value_1t": med[1], "value_nt": med[nt], "samples_1t": legs[1]["rates"], "samples_nt": legs[nt]["rates"],
             "label": "CPU restatement of reference algorithm, not MATLAB",
             "sample": "oracle/refsim.simulate (dense Q'HG zgemm, full(W) reshape-and-sum contraction, brute-force "

@@ -63,7 +63,7 @@ def quantise_pdp(pdp, sampling_rate):
             raise ValueError("Power delay profile model not supported!")
         pw = np.asarray(pw, dtype=float)
         dl = np.asarray(dl, dtype=float)
-        idx = np.round(dl / dt).astype(np.int64)               # 0-based (FastFading.m:111 is 1-based)
+        idx = (np.sign(dl / dt) * np.floor(np.abs(dl / dt) + 0.5)).astype(np.int64)   # MATLAB round               # 0-based (FastFading.m:111 is 1-based)
         tmp = np.zeros((idx.size, int(idx.max()) + 1))
         for i in range(idx.size):
             tmp[i, idx[i]] = 10.0 ** (pw[i] / 10)

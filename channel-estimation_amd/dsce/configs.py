@@ -21,7 +21,7 @@ import numpy as np
 
 from .channel import FastFading
 from .estimation import ImaginaryInterferenceCancellationAtPilotPosition as IIC
-from .modulation import FBMC, OFDM, SignalConstellation
+from .modulation import FBMC, OFDM, SignalConstellation, mround
 
 
 def _col(x):
@@ -108,7 +108,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
     snr = np.asarray(cfg["snr"] if snr_db is None else snr_db, dtype=float)
 
     fbmc = FBMC(L, 30 * nsub, F, SR, 0, False, "Hermite-OQAM", 8, 0, True)
-    zg_time = ((fbmc.Nr.SamplesTotal - (round((1 / 15e3 / 14) * SR) + round(SR / 15e3)) * 14 * nsub) / 2) / SR
+    zg_time = ((fbmc.Nr.SamplesTotal - (mround((1 / 15e3 / 14) * SR) + mround(SR / 15e3)) * 14 * nsub) / 2) / SR
     ofdm = OFDM(L, 14 * nsub, F, SR, 0, False, 1 / 15e3 / 14, zg_time)
     if ofdm.Nr.SamplesTotal != fbmc.Nr.SamplesTotal:
         raise ValueError("Total number of samples must be the same for OFDM and FBMC.")

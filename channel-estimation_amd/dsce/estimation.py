@@ -11,7 +11,7 @@
   ``+ChannelEstimation/PilotSymbolAidedChannelEstimation.m:33-133``.  The
   reference stubs its 'MMSE' method with ``error('Needs to be implemented')``
   (PSACE.m:110-111, :128-129); here 'MMSE' is the plug-in slot served by the
-  HIP engine (see ``dsce.engine`` / ``dsce.experiment``).
+  HIP engine (see ``dsce.engine`` and ``dsce.simulate``).
 """
 from __future__ import annotations
 
@@ -20,6 +20,14 @@ import numpy as np
 
 def _col(x):
     return np.asarray(x).reshape(-1, order="F")
+
+
+def mround(x):
+    """MATLAB round: half away from zero (Python's round and np.round round half
+    to even, which moves e.g. round(2.5) of PSACE.m:48 from 3 to 2)."""
+    x = np.asarray(x, dtype=float)
+    r = np.sign(x) * np.floor(np.abs(x) + 0.5)
+    return r if r.ndim else float(r)
 
 
 def _hadamard(n):
@@ -113,7 +121,7 @@ class ImaginaryInterferenceCancellationAtPilotPosition:
             for ip in range(1, NP + 1):
                 row = int(np.flatnonzero(ci == ip)[0])
                 cols = np.flatnonzero(ci == -ip)
-                interf = np.round(np.imag(D[row, cols]) * 1e10) / 1e10
+                interf = mround(np.imag(D[row, cols]) * 1e10) / 1e10
                 n = interf.size
                 order = np.argsort(-np.abs(interf), kind="stable")       # sort 'descend', stable
                 abs_sorted = np.abs(interf)[order]
@@ -205,8 +213,8 @@ class PilotSymbolAidedChannelEstimation:
             nK, st = int(Params[1][0]), Params[1][1]
             self.PilotSpacingFrequency, self.PilotSpacingTime = sf, st
             PM = np.zeros((nL, nK))
-            r0 = int(round(((nL - 1) % sf) / 2))
-            c0 = int(round(round(((nK - 1) % st) / 2)))
+            r0 = int(mround(((nL - 1) % sf) / 2))                          # PSACE.m:48
+            c0 = int(mround(mround(((nK - 1) % st) / 2)))
             PM[r0:nL:int(sf), c0:nK:int(st)] = 1
         elif PilotPattern == "Diamond":
             nL, sf = int(Params[0][0]), Params[0][1]
@@ -226,10 +234,10 @@ class PilotSymbolAidedChannelEstimation:
                 f = np.arange(f0, nL + 1, 2 * sf).astype(int) - 1
                 t = np.arange(t0, nK + 1, 2 * st).astype(int) - 1
                 PM[np.ix_(f, t)] = 1
-            mset(fshift, tshift)
-            mset(fshift + int(round(sf / 2)), int(round(tshift + st)))
-            mset(fshift + int(round(sf)), tshift)
-            mset(fshift + int(round(3 * sf / 2)), int(round(tshift + st)))
+            mset(fshift, tshift)                                            # PSACE.m:57-60
+            mset(fshift + int(mround(sf / 2)), int(mround(tshift + st)))
+            mset(fshift + int(mround(sf)), tshift)
+            mset(fshift + int(mround(3 * sf / 2)), int(mround(tshift + st)))
         elif PilotPattern == "Custom":
             self.PilotSpacingFrequency = np.nan
             self.PilotSpacingTime = np.nan

@@ -26,6 +26,11 @@ def _col(x):
     return np.asarray(x).reshape(-1, order="F")
 
 
+def mround(x):
+    """MATLAB round (half away from zero); Python's round is half-to-even."""
+    return float(np.sign(x) * np.floor(abs(x) + 0.5))
+
+
 # --------------------------------------------------------------------------
 # FBMC
 # --------------------------------------------------------------------------
@@ -55,7 +60,7 @@ def _hermite_h(n, x):
 
 def prototype_filter_hermite(T0, dt, OF):
     """FBMC.m:629-647.  Time grid ``-(OF*T0):dt:(OF*T0-dt)``."""
-    n = int(round(2 * OF * T0 / dt))
+    n = int(mround(2 * OF * T0 / dt))
     t = -(OF * T0) + np.arange(n) * dt
     z = np.sqrt(2 * np.pi) * (t / (T0 / np.sqrt(2)))
     g = np.exp(-np.pi * (t / (T0 / np.sqrt(2))) ** 2) / np.sqrt(T0)
@@ -109,15 +114,15 @@ class FBMC:
         """FBMC.m:61-160 (Hermite-OQAM branch)."""
         PHY, Nr, Impl, PF = self.PHY, self.Nr, self.Implementation, self.PrototypeFilter
         if (PHY.SamplingRate / (2 * PHY.SubcarrierSpacing)) % 1 != 0:
-            PHY.SubcarrierSpacing = PHY.SamplingRate / (2 * round(PHY.SamplingRate / (2 * PHY.SubcarrierSpacing)))
+            PHY.SubcarrierSpacing = PHY.SamplingRate / (2 * mround(PHY.SamplingRate / (2 * PHY.SubcarrierSpacing)))
         if (PHY.IntermediateFrequency / PHY.SubcarrierSpacing) % 1 != 0:
-            PHY.IntermediateFrequency = round(PHY.IntermediateFrequency / PHY.SubcarrierSpacing) * PHY.SubcarrierSpacing
+            PHY.IntermediateFrequency = mround(PHY.IntermediateFrequency / PHY.SubcarrierSpacing) * PHY.SubcarrierSpacing
         if PHY.SamplingRate < Nr.Subcarriers * PHY.SubcarrierSpacing:
             raise ValueError("Sampling Rate must be higher: at least Number of Subcarriers times Subcarrier Spacing")
         PHY.dt = 1.0 / PHY.SamplingRate
         if self.Method != "Hermite-OQAM":
             raise ValueError('Method (prototype filter) "%s" is not supported' % self.Method)
-        Impl.TimeSpacing = int(round(PHY.SamplingRate / (2 * PHY.SubcarrierSpacing)))
+        Impl.TimeSpacing = int(mround(PHY.SamplingRate / (2 * PHY.SubcarrierSpacing)))
         PHY.TimeSpacing = Impl.TimeSpacing * PHY.dt
         Impl.FrequencySpacing = PF.OverlappingFactor
         PF.TimeDomain = prototype_filter_hermite(PHY.TimeSpacing * 2, PHY.dt, PF.OverlappingFactor / 2)
@@ -125,8 +130,8 @@ class FBMC:
         Nr.SamplesTotal = Nr.SamplesPrototypeFilter + (Nr.MCSymbols - 1) * Impl.TimeSpacing
         l, k = np.meshgrid(np.arange(Nr.Subcarriers), np.arange(Nr.MCSymbols), indexing="ij")
         Impl.PhaseShift = np.exp(1j * np.pi / 2 * (l + k)) * np.exp(1j * Impl.InitialPhaseShift)
-        Impl.FFTSize = int(round(Nr.SamplesPrototypeFilter / Impl.FrequencySpacing))
-        Impl.IntermediateFrequency = int(round(PHY.IntermediateFrequency / PHY.SubcarrierSpacing))
+        Impl.FFTSize = int(mround(Nr.SamplesPrototypeFilter / Impl.FrequencySpacing))
+        Impl.IntermediateFrequency = int(mround(PHY.IntermediateFrequency / PHY.SubcarrierSpacing))
         rows = (np.arange(Nr.Subcarriers) + Impl.IntermediateFrequency) % Impl.FFTSize
         pm = np.zeros((Impl.FFTSize, Nr.MCSymbols), dtype=bool)
         pm[rows, :] = True
@@ -235,19 +240,19 @@ class OFDM:
     def SetDependentParameters(self):
         """OFDM.m:53-88."""
         PHY, Nr, Impl = self.PHY, self.Nr, self.Implementation
-        if (round(PHY.SamplingRate / PHY.SubcarrierSpacing * 1e5) / 1e5) % 1 != 0:
-            PHY.SubcarrierSpacing = PHY.SamplingRate / round(PHY.SamplingRate / PHY.SubcarrierSpacing)
-        if (round(PHY.IntermediateFrequency / PHY.SubcarrierSpacing * 1e5) / 1e5) % 1 != 0:
-            PHY.IntermediateFrequency = round(PHY.IntermediateFrequency / PHY.SubcarrierSpacing) * PHY.SubcarrierSpacing
+        if (mround(PHY.SamplingRate / PHY.SubcarrierSpacing * 1e5) / 1e5) % 1 != 0:
+            PHY.SubcarrierSpacing = PHY.SamplingRate / mround(PHY.SamplingRate / PHY.SubcarrierSpacing)
+        if (mround(PHY.IntermediateFrequency / PHY.SubcarrierSpacing * 1e5) / 1e5) % 1 != 0:
+            PHY.IntermediateFrequency = mround(PHY.IntermediateFrequency / PHY.SubcarrierSpacing) * PHY.SubcarrierSpacing
         if PHY.SamplingRate < Nr.Subcarriers * PHY.SubcarrierSpacing:
             raise ValueError("Sampling theorem is not fullfilled")
-        if abs((round(PHY.CyclicPrefixLength * PHY.SamplingRate * 1e5) / 1e5) % 1) != 0:
-            PHY.CyclicPrefixLength = round(PHY.CyclicPrefixLength * PHY.SamplingRate) / PHY.SamplingRate
-        Impl.CyclicPrefix = int(round(PHY.CyclicPrefixLength * PHY.SamplingRate))
-        Impl.ZeroGuardSamples = int(round(PHY.ZeroGuardTimeLength * PHY.SamplingRate))
-        Impl.TimeSpacing = int(round(PHY.SamplingRate / PHY.SubcarrierSpacing)) + Impl.CyclicPrefix
-        Impl.FFTSize = int(round(PHY.SamplingRate / PHY.SubcarrierSpacing))
-        Impl.IntermediateFrequency = int(round(PHY.IntermediateFrequency / PHY.SubcarrierSpacing))
+        if abs((mround(PHY.CyclicPrefixLength * PHY.SamplingRate * 1e5) / 1e5) % 1) != 0:
+            PHY.CyclicPrefixLength = mround(PHY.CyclicPrefixLength * PHY.SamplingRate) / PHY.SamplingRate
+        Impl.CyclicPrefix = int(mround(PHY.CyclicPrefixLength * PHY.SamplingRate))
+        Impl.ZeroGuardSamples = int(mround(PHY.ZeroGuardTimeLength * PHY.SamplingRate))
+        Impl.TimeSpacing = int(mround(PHY.SamplingRate / PHY.SubcarrierSpacing)) + Impl.CyclicPrefix
+        Impl.FFTSize = int(mround(PHY.SamplingRate / PHY.SubcarrierSpacing))
+        Impl.IntermediateFrequency = int(mround(PHY.IntermediateFrequency / PHY.SubcarrierSpacing))
         Impl.NormalizationFactor = np.sqrt(PHY.SamplingRate**2 / PHY.SubcarrierSpacing**2 / Nr.Subcarriers)
         PHY.dt = 1.0 / PHY.SamplingRate
         PHY.TimeSpacing = Impl.TimeSpacing * PHY.dt
@@ -324,7 +329,7 @@ class SignalConstellation:
         self.ModulationOrder = M
         self.Method = Method
         if Method == "QAM":
-            sq = int(round(np.sqrt(M)))
+            sq = int(mround(np.sqrt(M)))
             atom = np.zeros((sq, int(np.log2(sq))), dtype=bool)
             atom[:sq // 2, 0] = True
             for i in range(1, atom.shape[1]):

@@ -312,8 +312,8 @@ def constellation(M, method):
             bm[np.ix_(Q_rep == x, np.arange(0, bm.shape[1], 2))] = atom
     elif method == "PAM":
         bm = _gray_atom(M, int(round(np.log2(M))))
-        sym = (2 * np.arange(1, M + 1) - M - 1).astype(complex)
-        sym = sym / np.sqrt(np.mean(np.abs(sym) ** 2))
+        sym = (2 * np.arange(1, M + 1) - M - 1).astype(float)        # real, as in MATLAB
+        sym = (sym / np.sqrt(np.mean(np.abs(sym) ** 2))).astype(complex)
     else:
         raise ValueError(method)
     order = np.argsort(_bi2de_lsb_first(bm), kind="stable")

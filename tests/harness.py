@@ -1,10 +1,21 @@
-"""Test-side adapters: turn the product's host setup (dsce.configs) into the
-plain-array inputs of the CPU oracle.  Lives under tests/ because only tests,
-smoke() and bench's cpu_baseline may touch oracle/."""
+"""Test-side adapters between the CPU oracle and the engine.
+
+The oracle's inputs come from the oracle's OWN restatement of the reference's
+setup (oracle/setup.py), never from the product's host mirror; GPU parity
+tests hand those same arrays to the engine through the C-ABI (they are data at
+the boundary: G, Q, P, pilot / data positions, masks, constellation, PDP), so a
+parity test compares engine and oracle on identical, independently produced
+inputs.  The product's host mirror (dsce.configs) is checked against
+oracle/setup.py separately (tests/test_oracle_setup.py).
+
+Lives under tests/ because only tests, smoke() and bench's cpu_baseline may
+touch oracle/."""
 from __future__ import annotations
 
+import functools
 import os
 import sys
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -15,25 +26,94 @@ for p in (ROOT, PKG):
         sys.path.insert(0, p)
 
 
-def oracle_chan(setup):
-    ch = setup.channel
-    return dict(N=setup.N, dt=ch.dt, pdp=ch.PowerDelayProfile, pdp_norm=ch.PowerDelayProfileNormalized,
-                idx_taps=ch.IndexDelayTaps, fD=ch.MaximumDopplerShift, paths=ch.Paths, model=ch.DopplerModel)
+@functools.lru_cache(maxsize=8)
+def _script_setup(name, schemes, snr_db, n_iter):
+    from oracle import setup as osu
+    return osu.script_setup(name, schemes=schemes, snr_db=None if snr_db is None else list(snr_db), n_iter=n_iter)
 
 
-def oracle_scheme(sc):
+def setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db=None, n_iter=4):
+    """The oracle's restatement of the script's setup (script:16-205) as a
+    namespace: N, L, pn_time, snr_db, n_iter, zero_threshold, chan (dict),
+    schemes (name -> oracle scheme dict), fbmc / ofdm (modulator objects)."""
+    d = _script_setup(name, tuple(schemes), None if snr_db is None else tuple(float(x) for x in snr_db), n_iter)
+    return SimpleNamespace(**d)
+
+
+def oracle_chan(S):
+    return S.chan
+
+
+_MMSE = {}
+
+
+def oracle_mmse(S, name):
+    """R_hP, R_est, R_noI, R_Dij, W, W0 of scheme `name` (refsim.mmse_setup,
+    script:208-313) from the oracle's own G / Q / P and channel (cached)."""
+    key = (S.name, tuple(S.snr_db), S.n_iter, tuple(sorted(S.schemes)), name)
+    if key not in _MMSE:
+        from oracle import refsim
+        ch = S.chan
+        tc = refsim.time_correlation(S.N, ch["dt"], ch["fD"], ch["model"])
+        R_vecH = refsim.correlation_matrix(S.N, ch["pdp_norm"], tc)
+        sc = S.schemes[name]
+        _MMSE[key] = refsim.mmse_setup(R_vecH, S.N, sc["G"], sc["Q"], sc["P"], sc["pilot_pos"], sc["kappa"],
+                                       S.pn_time, S.zero_threshold)
+    return _MMSE[key]
+
+
+# ---------------------------------------------------------------------------
+# the engine, configured from the oracle's arrays (dsce.engine is the ctypes
+# binding of include/dsce.h; these namespaces carry exactly what it reads)
+# ---------------------------------------------------------------------------
+def _engine_scheme(S, name):
+    sc = S.schemes[name]
+    const = SimpleNamespace(SymbolMapping=sc["symbols"], ModulationOrder=sc["symbols"].size,
+                            BitsPerSymbol=sc["bits_per_symbol"])
+    return SimpleNamespace(name=name, G=sc["G"], Q=sc["Q"], P=sc["P"], pilot_pos=sc["pilot_pos"],
+                           data_pos=sc["data_pos"], considered_symbols=sc["considered"], const=const,
+                           n_pilots=len(sc["pilot_pos"]), n_data=sc["n_data"], bits_per_symbol=sc["bits_per_symbol"],
+                           despread=sc["despread"], real_detect=sc["real_detect"], bits_slot=sc["bits_slot"],
+                           pilot_slot=sc["pilot_slot"], kappa=sc["kappa"], data_div=sc["data_div"],
+                           LK=sc["G"].shape[1], n_bits=sc["n_data"] * sc["bits_per_symbol"],
+                           extras={"pilot_matrix": np.zeros((S.L, sc["G"].shape[1] // S.L))})
+
+
+def engine(S, schemes=None, batch=None, options=None, device=0):
+    """dsce.engine.Engine built from the oracle setup S (channel, SNR list,
+    schemes, MMSE build), like dsce.engine.build_engine does from dsce.configs."""
+    from dsce.engine import Engine
+    ch = S.chan
+    eng = Engine(device)
+    for k, v in (options or {}).items():
+        eng.set_option(k, v)
+    models = {"Jakes": 0, "Uniform": 1, "Discrete-Jakes": 2, "Discrete-Uniform": 3}
+    eng.set_channel(SimpleNamespace(PowerDelayProfileNormalized=np.asarray(ch["pdp_norm"], dtype=float),
+                                    SamplesTotal=S.N, SamplingRate=1.0 / ch["dt"], MaximumDopplerShift=ch["fD"],
+                                    Paths=ch["paths"], DopplerModel=ch["model"], MODELS=models))
+    eng.set_snr(S.pn_time, S.n_iter)
+    for n in (list(S.schemes) if schemes is None else list(schemes)):
+        eng.add_scheme(_engine_scheme(S, n))
+    eng.build_mmse(S.zero_threshold)
+    if batch:
+        eng.set_batch(batch)
+    return eng
+
+
+def simulate(S, seed, first, n, names, trace=None):
+    """oracle/refsim.simulate over schemes `names` of S."""
+    from oracle import refsim
+    return refsim.simulate(seed, first, n, S.chan, [S.schemes[k] for k in names], S.pn_time, S.n_iter,
+                           [oracle_mmse(S, k) for k in names], trace=trace)
+
+
+def product_scheme_dict(sc):
+    """Oracle-format dict of a PRODUCT scheme (dsce.configs.Scheme).  Used only
+    for BASELINE config 1 (the doubly-flat script), whose PSACE interpolation
+    weights (scatteredInterpolant restated on the host, PSACE.m:74-121) exist
+    only in the product: that config's parity shares this setup input."""
     return dict(G=sc.G, Q=sc.Q, P=sc.P, pilot_pos=sc.pilot_pos, data_pos=sc.data_pos, despread=sc.despread,
                 real_detect=sc.real_detect, data_div=sc.data_div, kappa=sc.kappa,
                 symbols=sc.const.SymbolMapping, bitmap=sc.const.BitMapping.astype(np.uint8),
                 bits_per_symbol=sc.bits_per_symbol, n_data=sc.n_data, considered=sc.considered_symbols,
                 bits_slot=sc.bits_slot, pilot_slot=sc.pilot_slot)
-
-
-def oracle_mmse(setup, sc, R_vecH=None, want_W=True):
-    from oracle import refsim
-    ch = setup.channel
-    if R_vecH is None:
-        tc = refsim.time_correlation(setup.N, ch.dt, ch.MaximumDopplerShift, ch.DopplerModel)
-        R_vecH = refsim.correlation_matrix(setup.N, ch.PowerDelayProfileNormalized, tc)
-    return refsim.mmse_setup(R_vecH, setup.N, sc.G, sc.Q, sc.P, sc.pilot_pos, sc.kappa, setup.pn_time,
-                             setup.zero_threshold, want_W=want_W)

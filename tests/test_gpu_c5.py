@@ -6,8 +6,7 @@ and (OFDM) bit-error counts.  Two of the 16 SNR points keep the literal oracle
 import numpy as np
 import pytest
 
-import harness  # noqa: F401  (sys.path)
-from dsce.configs import build_setup
+import harness
 from oracle import refsim
 
 pytestmark = pytest.mark.gpu
@@ -27,51 +26,49 @@ def _check_w(eng, mm, nsnr):
             assert np.all((np.abs(wg - wo) <= tol) | border), (k, var)
 
 
-def _check_trace(S, sc, eng, mm, rep, snrs):
+def _check_trace(S, name, eng, rep, snrs):
+    """Every stage of a unit: y, hP, diag(D_hat), y_est, y_perf, decisions."""
     tr = {}
-    refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
-                    trace=tr)
+    harness.simulate(S, SEED, rep, 1, [name], trace=tr)
     for k in snrs:
         g = eng.trace_unit(0, SEED, rep, k)
-        np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
+        u = tr["units"][k]
+        np.testing.assert_allclose(g["y"], u["y"], rtol=0, atol=1e-10)
         for st in range(S.n_iter + 1):
-            np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
-            np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
+            for key in ("hp", "hest", "yest"):
+                np.testing.assert_allclose(g[key][st], u[key][st], rtol=0, atol=1e-9, err_msg="%s %d" % (key, st))
+            for key, mk in (("dec_e", "margin_e"), ("dec_p", "margin_p")):
+                assert np.all((g[key][st] == u[key][st]) | (u[mk][st] < 1e-9)), (key, st)
 
 
 def test_c5_ofdm_matches_oracle():
-    from dsce.engine import build_engine
-    S = build_setup("c5", schemes=("ofdm",), snr_db=SNR)
+    S = harness.setup("c5", schemes=("ofdm",), snr_db=SNR)
     sc = S.schemes["ofdm"]
-    assert S.N == 1080 and sc.LK == 672 and len(sc.pilot_pos) == 32 and len(S.channel.IndexDelayTaps) == 3
-    eng = build_engine(S, batch=64)
+    assert S.N == 1080 and sc["G"].shape[1] == 672 and len(sc["pilot_pos"]) == 32 and len(S.chan["idx_taps"]) == 3
+    eng = harness.engine(S, batch=64)
+    ch = S.chan
     for rep in (0, 3):
         ir_g = eng.channel_impulse_response(SEED, rep)
-        ch = S.channel
-        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
-                               ch.MaximumDopplerShift, ch.Paths)
+        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch["dt"], ch["pdp_norm"], ch["idx_taps"], ch["fD"], ch["paths"])
         np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
-    mm = harness.oracle_mmse(S, sc)
+    mm = harness.oracle_mmse(S, "ofdm")
     rhp, rest, rnoi = eng.correlation(0)
     scale = np.abs(mm["R_hP"]).max()
     np.testing.assert_allclose(rhp, mm["R_hP"], rtol=0, atol=1e-12 * scale)
     np.testing.assert_allclose(rest, mm["R_est"], rtol=0, atol=1e-12 * scale)
     _check_w(eng, mm, len(SNR))
-    _check_trace(S, sc, eng, mm, 7, (0, 1))
+    _check_trace(S, "ofdm", eng, 7, (0, 1))
     cg = eng.run(SEED, 0, 64)
-    res = refsim.simulate(SEED, 0, 64, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
-                          [mm])
+    res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
     eng.close()
 
 
 def test_c5_fbmc_aux_matches_oracle():
-    from dsce.engine import build_engine
-    S = build_setup("c5", schemes=("fbmc_aux",), snr_db=SNR[1:])
-    sc = S.schemes["fbmc_aux"]
-    assert sc.LK == 1440
-    eng = build_engine(S, batch=64)
-    mm = harness.oracle_mmse(S, sc)
+    S = harness.setup("c5", schemes=("fbmc_aux",), snr_db=SNR[1:])
+    assert S.schemes["fbmc_aux"]["G"].shape[1] == 1440
+    eng = harness.engine(S, batch=64)
+    mm = harness.oracle_mmse(S, "fbmc_aux")
     _check_w(eng, mm, 1)
-    _check_trace(S, sc, eng, mm, 2, (0,))
+    _check_trace(S, "fbmc_aux", eng, 2, (0,))
     eng.close()

@@ -89,7 +89,7 @@ def _oracle_schemes(S):
     out = []
     for n in ("fbmc_aux", "fbmc_cod", "ofdm"):
         sc = S.schemes[n]
-        d = harness.oracle_scheme(sc)
+        d = harness.product_scheme_dict(sc)
         d.update(noise_slot=sc.extras["noise_slot"], interp=sc.extras["interp"])
         out.append(d)
     return out

@@ -1,12 +1,13 @@
 """GPU parity: the HIP engine (through the C-ABI) against the CPU oracle on the
-same Philox streams.  Floating-point quantities: |gpu - oracle| within the
-stated fp64 tolerances; bit-error counts: identical, up to the number of
-decisions the oracle flags as borderline (distance margin < 1e-9)."""
+same Philox streams and the same, independently produced setup (the oracle's
+own restatement oracle/setup.py, handed to the engine as data; tests/harness.py).
+Floating-point quantities: |gpu - oracle| within the stated fp64 tolerances;
+bit-error counts: identical, up to the number of decisions the oracle flags as
+borderline (distance margin < 1e-9)."""
 import numpy as np
 import pytest
 
-import harness  # noqa: F401  (sys.path)
-from dsce.configs import build_setup
+import harness
 from oracle import refsim
 
 pytestmark = pytest.mark.gpu
@@ -16,23 +17,21 @@ SEED = 0x5EED0002
 
 @pytest.fixture(scope="module")
 def ofdm():
-    from dsce.engine import build_engine
-    S = build_setup("default", schemes=("ofdm",))
-    eng = build_engine(S, batch=256)
-    mm = harness.oracle_mmse(S, S.schemes["ofdm"])
+    S = harness.setup("default", schemes=("ofdm",))
+    eng = harness.engine(S, batch=256)
+    mm = harness.oracle_mmse(S, "ofdm")
     yield S, eng, mm
     eng.close()
 
 
 def test_jakes_ir_matches_oracle(ofdm):
     S, eng, _ = ofdm
-    ch = S.channel
+    ch = S.chan
     # rep % 8 is the realisation's lane in its batch (dsce_channel_realise): 1 and
     # 77 sit in the second half-wave of k_jakes's two-realisations-per-wave mapping
     for rep in (0, 1, 6, 77, 1 << 33):
         ir_g = eng.channel_impulse_response(SEED, rep)
-        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
-                               ch.MaximumDopplerShift, ch.Paths)
+        ir_o = refsim.jakes_ir(SEED, rep, S.N, ch["dt"], ch["pdp_norm"], ch["idx_taps"], ch["fD"], ch["paths"])
         assert ir_g.shape == ir_o.shape
         np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
 
@@ -46,57 +45,92 @@ def test_correlation_matrices_match_oracle(ofdm):
     np.testing.assert_allclose(rnoi, mm["R_noI"], rtol=0, atol=1e-12 * scale)
 
 
-def test_mmse_estimator_matches_oracle(ofdm):
+def _check_W(eng, mm, nsnr):
     """W = R_Dij pinv(R): the tolerance is fp64 rounding amplified by the
     condition number of R (pinv/inverse of an ill-conditioned pilot
     correlation at high SNR) and growing with its dimension NP,
-    tol = 1e-14 * cond(R) * max(1, NP/16) * max|W|."""
-    S, eng, mm = ofdm
-    for k in range(len(S.pn_time)):
+    tol = 1e-14 * cond(R) * max(1, NP/16) * max|W|; entries within tol of the
+    1e-8 zero threshold (script:287-289) may legitimately flip to 0."""
+    for k in range(nsnr):
         for var, key, R in ((0, "W", mm["R_est"][k]), (1, "W0", mm["R_noI"][k])):
             wg = eng.W(0, k, var)
             wo = mm[key][:, k]
             scale = np.abs(wo).max()
             tol = max(1e-14 * np.linalg.cond(R) * max(1, R.shape[0] / 16), 1e-12) * scale
             diff = np.abs(wg - wo)
-            # entries within tol of the 1e-8 zero threshold may legitimately flip to 0
             border = np.abs(np.abs(wo) - 1e-8) <= tol
             assert np.all((diff <= tol) | border), (k, var, diff.max() / scale, np.linalg.cond(R))
 
 
-def test_unit_trace_matches_oracle(ofdm):
+def test_mmse_estimator_matches_oracle(ofdm):
     S, eng, mm = ofdm
-    sc = S.schemes["ofdm"]
-    tr = {}
-    rep, k = 5, 3
-    refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
-                    trace=tr)
-    g = eng.trace_unit(0, SEED, rep, k)
-    np.testing.assert_allclose(g["y"], tr["y"][k], rtol=0, atol=1e-10)
-    np.testing.assert_allclose(g["h"], np.diag(sc.Q.conj().T @ (np.asarray(
-        refsim.conv_matrix(tr["ir"][0], S.channel.PowerDelayProfile, S.N).todense()) @ sc.G)), rtol=0, atol=1e-10)
-    # every stage: LS pilot estimates and diag(D_hat) after the MMSE contraction
-    # (stage s >= 1 depends on y_est of the k_wcontract kernel).  Decisions
-    # are identical here, so the trajectories agree to fp64 rounding.
-    for st in range(S.n_iter + 1):
-        np.testing.assert_allclose(g["hp"][st], tr["hp_stages"][k][st], rtol=0, atol=1e-9)
-        np.testing.assert_allclose(g["hest"][st], tr["hest_stages"][k][st], rtol=0, atol=1e-9)
+    _check_W(eng, mm, len(S.pn_time))
+
+
+# ---------------------------------------------------------------------------
+# The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
+# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_mfma for
+# the perfect-CSI IC chain, k_stage_fused for the one-tap stage).
+# ---------------------------------------------------------------------------
+BENCH_PATH = {"wpair3_fused", "pic_mfma", "stage_fused", "noise_fused"}
+
+
+def _check_trace(g, u, name, tol=1e-9):
+    """Per element, per stage: |gpu - oracle| <= 1e-9 for y, h = diag(D), hP,
+    diag(D_hat) and y_est (all rows); decisions identical except where the
+    oracle's nearest-point margin is below 1e-9 (borderline, none expected)."""
+    ns = len(u["hp"])
+    np.testing.assert_allclose(g["y"], u["y"], rtol=0, atol=1e-10, err_msg=name)
+    np.testing.assert_allclose(g["h"], u["h"], rtol=0, atol=1e-10, err_msg=name)
+    for st in range(ns):
+        np.testing.assert_allclose(g["hp"][st], u["hp"][st], rtol=0, atol=tol, err_msg="%s hp %d" % (name, st))
+        np.testing.assert_allclose(g["hest"][st], u["hest"][st], rtol=0, atol=tol, err_msg="%s hest %d" % (name, st))
+        np.testing.assert_allclose(g["yest"][st], u["yest"][st], rtol=0, atol=tol, err_msg="%s yest %d" % (name, st))
+        for key, mk in (("dec_e", "margin_e"), ("dec_p", "margin_p")):
+            ok = (g[key][st] == u[key][st]) | (u[mk][st] < 1e-9)
+            assert ok.all(), (name, key, st, np.flatnonzero(~ok)[:8])
+    return ns
+
+
+def test_bench_kernels_trace_matches_oracle(ofdm):
+    """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
+    dsce_path_info) and every intermediate of every stage of a unit matches the
+    oracle: the fused contraction's y_est and diag(D_hat), k_pilot_pre's LS
+    pilots, k_pic_mfma's y_perf (data rows: the chain forms only those) and
+    both branches' decisions."""
+    S, eng, mm = ofdm
+    rows = S.schemes["ofdm"]["data_pos"]
+    for rep in (5, 70):
+        tr = {}
+        harness.simulate(S, SEED, rep, 1, ["ofdm"], trace=tr)
+        for k in range(len(S.pn_time)):
+            g = eng.trace_unit(0, SEED, rep, k)
+            assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+            u = tr["units"][k]
+            ns = _check_trace(g, u, "rep %d snr %d" % (rep, k))
+            for st in range(1, ns):
+                np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
 
 
 def test_error_counts_match_oracle(ofdm):
+    """Error counts and MSE sums through the bench path, 64 realisations x 7 SNR
+    points (7 x 14 perfect-CSI chain blocks: not a multiple of the 8 XCDs) and
+    128 x 7; the bench kernels ran (asserted)."""
     S, eng, mm = ofdm
     sc = S.schemes["ofdm"]
-    n = 64
     eng.enable_mse()
-    cg = eng.run(SEED, 0, n)
-    res = refsim.simulate(SEED, 0, n, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm])
-    co = res["err"]
-    diff = np.abs(cg - co).sum()
-    assert diff <= 8 * res["borderline"].sum(), (cg - co)
-    _check_mse(eng, res)
-    eng.enable_mse(False)
+    for first, n in ((0, 64), (128, 128)):
+        eng.set_batch(n)
+        cg = eng.run(SEED, first, n)
+        assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+        res = harness.simulate(S, SEED, first, n, ["ofdm"])
+        assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (first, cg - res["err"])
+        if first == 0:
+            _check_mse(eng, res)
+            eng.enable_mse(False)
+    eng.set_batch(256)
     b = eng.bits_per_rep(0)
-    assert b[0] == sc.n_bits and b[1] == sc.considered_symbols.sum() * sc.bits_per_symbol
+    assert b[0] == sc["n_data"] * sc["bits_per_symbol"] and b[1] == sc["considered"].sum() * sc["bits_per_symbol"]
 
 
 # ---------------------------------------------------------------------------
@@ -105,28 +139,18 @@ def test_error_counts_match_oracle(ofdm):
 # ---------------------------------------------------------------------------
 @pytest.fixture(scope="module", params=["fbmc_aux", "fbmc_cod"])
 def fbmc(request):
-    from dsce.engine import build_engine
-    S = build_setup("default", schemes=(request.param,), snr_db=[15.0, 35.0])
-    eng = build_engine(S, batch=256)
-    mm = harness.oracle_mmse(S, S.schemes[request.param])
+    S = harness.setup("default", schemes=(request.param,), snr_db=[15.0, 35.0])
+    eng = harness.engine(S, batch=256)
+    mm = harness.oracle_mmse(S, request.param)
     yield request.param, S, eng, mm
     eng.close()
 
 
 def test_fbmc_estimator_and_trace(fbmc):
     name, S, eng, mm = fbmc
-    sc = S.schemes[name]
-    for k in range(2):
-        for var, key, R in ((0, "W", mm["R_est"][k]), (1, "W0", mm["R_noI"][k])):
-            wg = eng.W(0, k, var)
-            wo = mm[key][:, k]
-            scale = np.abs(wo).max()
-            tol = max(1e-14 * np.linalg.cond(R) * max(1, R.shape[0] / 16), 1e-12) * scale
-            border = np.abs(np.abs(wo) - 1e-8) <= tol
-            assert np.all((np.abs(wg - wo) <= tol) | border), (name, k, var)
+    _check_W(eng, mm, 2)
     tr = {}
-    refsim.simulate(SEED, 9, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm],
-                    trace=tr)
+    harness.simulate(S, SEED, 9, 1, [name], trace=tr)
     for k in range(2):
         g = eng.trace_unit(0, SEED, 9, k)
         u = tr["units"][k]
@@ -137,11 +161,9 @@ def test_fbmc_estimator_and_trace(fbmc):
 
 def test_fbmc_error_counts(fbmc):
     name, S, eng, mm = fbmc
-    sc = S.schemes[name]
     eng.enable_mse()
     cg = eng.run(SEED, 64, 64)
-    res = refsim.simulate(SEED, 64, 64, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
-                          [mm])
+    res = harness.simulate(S, SEED, 64, 64, [name])
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
     _check_mse(eng, res)
     eng.enable_mse(False)
@@ -161,13 +183,12 @@ def _check_mse(eng, res):
 def test_three_schemes_share_channel_and_noise():
     """script:350-403: one channel draw and one noise draw per (rep, SNR) feed
     all three schemes; a joint engine equals three single-scheme engines."""
-    from dsce.engine import build_engine
-    S = build_setup("default", snr_db=[25.0])
-    joint = build_engine(S, batch=128)
+    S = harness.setup("default", snr_db=[25.0])
+    joint = harness.engine(S, batch=128)
     cj = joint.run(SEED, 0, 128)
     joint.close()
     for i, name in enumerate(S.schemes):
-        e = build_engine(S, schemes=(name,), batch=128)
+        e = harness.engine(S, schemes=(name,), batch=128)
         np.testing.assert_array_equal(e.run(SEED, 0, 128)[0], cj[i])
         e.close()
 
@@ -192,13 +213,15 @@ def test_psace_mmse_plugin(ofdm):
     from dsce.estimation import PilotSymbolAidedChannelEstimation
     S, eng, mm = ofdm
     sc = S.schemes["ofdm"]
-    pm = sc.extras["pilot_matrix"]
-    est = PilotSymbolAidedChannelEstimation("Custom", pm, "MMSE")
+    LK = sc["G"].shape[1]
+    pm = np.zeros(LK)
+    pm[sc["pilot_pos"]] = 1
+    est = PilotSymbolAidedChannelEstimation("Custom", pm.reshape(S.L, LK // S.L, order="F"), "MMSE")
     est.set_mmse_engine(eng, 0, 3)
     rng = np.random.default_rng(4)
     ls = rng.standard_normal(16) + 1j * rng.standard_normal(16)
     got = est.ChannelInterpolation(ls)
-    W3 = mm["W"][:, 3].reshape(sc.LK, sc.LK, 16, order="F")
+    W3 = mm["W"][:, 3].reshape(LK, LK, 16, order="F")
     ref = np.diag((W3 * ls[None, None, :]).sum(axis=2))
     np.testing.assert_allclose(got.reshape(-1, order="F"), ref, rtol=0, atol=1e-11 * np.abs(ref).max())
 
@@ -206,10 +229,9 @@ def test_psace_mmse_plugin(ofdm):
 def test_w_band_trim_is_bit_exact():
     """Trimming W to its non-zero column extent (after the 1e-8 threshold) skips
     exact zeros only: counts are bit-identical and the contracted work shrinks."""
-    from dsce.engine import build_engine
-    S = build_setup("default", schemes=("fbmc_aux",), snr_db=[20.0, 40.0])
-    full = build_engine(S, batch=128, options={"wtrim": 0})
-    trim = build_engine(S, batch=128)
+    S = harness.setup("default", schemes=("fbmc_aux",), snr_db=[20.0, 40.0])
+    full = harness.engine(S, batch=128, options={"wtrim": 0})
+    trim = harness.engine(S, batch=128)
     np.testing.assert_array_equal(full.run(SEED, 0, 128), trim.run(SEED, 0, 128))
     for k in range(2):
         np.testing.assert_array_equal(full.W(0, k, 0), trim.W(0, k, 0))
@@ -228,9 +250,8 @@ def test_stage_variants_agree(name):
     own kernels instead of fused into the contraction, the perfect-CSI chain as
     per-iteration passes / VALU chain instead of k_pic_mfma, the fused
     epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave."""
-    from dsce.engine import build_engine
-    S = build_setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
-    eng = build_engine(S, batch=512)
+    S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
+    eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
     ref = eng.run(SEED, 0, 1024)
     assert "stage_split" in eng.path_info(0)
@@ -263,83 +284,15 @@ def test_options_are_validated():
     eng.close()
 
 
-# ---------------------------------------------------------------------------
-# The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
-# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_mfma for
-# the perfect-CSI IC chain, k_stage_fused for the one-tap stage).
-# ---------------------------------------------------------------------------
-BENCH_PATH = {"wpair3_fused", "pic_mfma", "stage_fused", "noise_fused"}
-
-
-def _check_trace(g, u, name, rtol_ulp=1e-9):
-    """Per element, per stage: |gpu - oracle| <= 1e-9 for y, hP, diag(D_hat),
-    y_est (all rows) and y_perf (data rows: the fused perfect-CSI chain forms
-    only those); decisions identical except where the oracle's nearest-point
-    margin is below 1e-9 (borderline, none expected)."""
-    ns = len(u["hp"])
-    np.testing.assert_allclose(g["y"], u["y"], rtol=0, atol=1e-10, err_msg=name)
-    np.testing.assert_allclose(g["h"], u["h"], rtol=0, atol=1e-10, err_msg=name)
-    for st in range(ns):
-        np.testing.assert_allclose(g["hp"][st], u["hp"][st], rtol=0, atol=rtol_ulp, err_msg="%s hp %d" % (name, st))
-        np.testing.assert_allclose(g["hest"][st], u["hest"][st], rtol=0, atol=rtol_ulp,
-                                   err_msg="%s hest %d" % (name, st))
-        np.testing.assert_allclose(g["yest"][st], u["yest"][st], rtol=0, atol=rtol_ulp,
-                                   err_msg="%s yest %d" % (name, st))
-        for key, mk in (("dec_e", "margin_e"), ("dec_p", "margin_p")):
-            ok = (g[key][st] == u[key][st]) | (u[mk][st] < 1e-9)
-            assert ok.all(), (name, key, st, np.flatnonzero(~ok)[:8])
-    return ns
-
-
-def _data_rows(sc):
-    return np.asarray(sc.data_pos) if not sc.despread else None
-
-
-def test_bench_kernels_trace_matches_oracle(ofdm):
-    """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
-    dsce_path_info) and every intermediate of every stage of a unit matches the
-    oracle: the fused contraction's y_est and diag(D_hat), k_pilot_pre's LS
-    pilots, k_pic_mfma's y_perf and both branches' decisions."""
-    S, eng, mm = ofdm
-    sc = S.schemes["ofdm"]
-    rows = _data_rows(sc)
-    for rep in (5, 70):
-        tr = {}
-        refsim.simulate(SEED, rep, 1, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
-                        [mm], trace=tr)
-        for k in range(len(S.pn_time)):
-            g = eng.trace_unit(0, SEED, rep, k)
-            assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
-            u = tr["units"][k]
-            ns = _check_trace(g, u, "rep %d snr %d" % (rep, k))
-            for st in range(1, ns):
-                np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
-
-
-def test_bench_path_counts_match_oracle(ofdm):
-    """Error counts through the bench path at a shape where every fast kernel
-    is eligible (asserted), 128 realisations x 7 SNR points, and at an odd
-    shape (64 realisations: 7 x 14 blocks of the perfect-CSI chain, not a
-    multiple of the 8 XCDs)."""
-    S, eng, mm = ofdm
-    sc = S.schemes["ofdm"]
-    for first, n in ((128, 128), (320, 64)):
-        eng.set_batch(n)
-        cg = eng.run(SEED, first, n)
-        assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
-        res = refsim.simulate(SEED, first, n, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time,
-                              S.n_iter, [mm])
-        assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (first, cg - res["err"])
-    eng.set_batch(256)
-
-
 @pytest.mark.parametrize("name", ["default", "c5", "paper"])
 def test_tx_matrices_on_gpu_match_host_mirror(name):
     """Row f1: G and Q = GetRXMatrix' produced on the GPU in closed form equal
-    the host mirror's L Modulation() calls (OFDM.m:184-218, FBMC.m:318-354)."""
-    from dsce.engine import Engine
+    the host mirror's L Modulation() calls (OFDM.m:184-218, FBMC.m:318-354)
+    and the oracle's own restatement (oracle/setup.py)."""
     from dsce.configs import build_setup
+    from dsce.engine import Engine
     S = build_setup(name, schemes=("fbmc_aux", "ofdm"))
+    O = harness.setup(name, schemes=("ofdm",))
     eng = Engine()
     for key in ("fbmc_aux", "ofdm"):
         sc = S.schemes[key]
@@ -347,4 +300,6 @@ def test_tx_matrices_on_gpu_match_host_mirror(name):
         scale = np.abs(sc.G).max()
         np.testing.assert_allclose(G, sc.G, rtol=0, atol=1e-13 * scale, err_msg=key)
         np.testing.assert_allclose(Q, sc.Q, rtol=0, atol=1e-13 * np.abs(sc.Q).max(), err_msg=key)
+        if key == "ofdm":
+            np.testing.assert_allclose(G, O.schemes["ofdm"]["G"], rtol=0, atol=1e-13 * scale)
     eng.close()

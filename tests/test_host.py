@@ -166,3 +166,27 @@ def test_theory_module_matches_oracle(M, kind):
     a = bep(snr, c.SymbolMapping, c.BitMapping)
     b = refsim.bit_error_probability_doubly_flat_rayleigh(snr, c.SymbolMapping, c.BitMapping)
     assert np.max(np.abs(a / b - 1)) < 1e-10
+
+
+def test_psace_patterns_use_matlab_round():
+    """PSACE.m:48 rounds half away from zero: Rectangular [[24, 6], [14, 7]]
+    puts pilots on rows 4, 10, 16, 22 (1-based) — mod(23, 6) / 2 = 2.5 -> 3 —
+    and columns 4, 11; Diamond with an odd spacing (sf = 5, :57-60) offsets the
+    second lattice by round(2.5) = 3 and the fourth by round(7.5) = 8."""
+    from dsce.estimation import PilotSymbolAidedChannelEstimation as PSACE
+    from dsce.estimation import mround
+    assert mround(2.5) == 3 and mround(-2.5) == -3 and mround(7.5) == 8
+    r = PSACE("Rectangular", [[24, 6], [14, 7]], "linear")
+    rows, cols = np.nonzero(r.PilotMatrix)
+    assert sorted(set(rows + 1)) == [4, 10, 16, 22] and sorted(set(cols + 1)) == [4, 11]
+    d = PSACE("Diamond", [[24, 5], [14, 4]], "linear")
+    # FrequencyPositionShift = floor((24 - max(1:10:24, 3.5:10:24, 6:10:24, 8.5:10:24)) / 2) + 1 = 1,
+    # TimePositionShift = floor((14 - max(1:8:14, 5:8:14)) / 2) + 1 = 1
+    f, t = 1, 1
+    want = set()
+    for f0, t0 in ((f, t), (f + 3, t + 4), (f + 5, t), (f + 8, t + 4)):
+        for a in range(f0, 25, 10):
+            for b in range(t0, 15, 8):
+                want.add((a - 1, b - 1))
+    got = set(zip(*np.nonzero(d.PilotMatrix)))
+    assert got == want, sorted(got ^ want)

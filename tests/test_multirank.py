@@ -25,17 +25,13 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
 
     import harness as h  # noqa: F401
-    from dsce.configs import build_setup
     from dsce.parallel import allreduce_counts, shard_range
-    from oracle import refsim
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    S = build_setup("default", schemes=("ofdm",), snr_db=[20.0, 35.0])
-    sc = S.schemes["ofdm"]
-    mm = h.oracle_mmse(S, sc)
+    S = h.setup("default", schemes=("ofdm",), snr_db=[20.0, 35.0])
     first, n = shard_range(0, 128, world, rank, align=64)
-    res = refsim.simulate(11, first, n // 32, h.oracle_chan(S), [h.oracle_scheme(sc)], S.pn_time, S.n_iter, [mm])
+    res = h.simulate(S, 11, first, n // 32, ["ofdm"])
     tot = allreduce_counts(res["err"])
     q.put((rank, first, n, tot))
     dist.destroy_process_group()
@@ -57,13 +53,8 @@ def test_two_rank_counter_allreduce():
     out.sort()
     assert np.array_equal(out[0][3], out[1][3])
     # single-process reference over the same realisations (2 per rank)
-    from dsce.configs import build_setup
-    from oracle import refsim
-    S = build_setup("default", schemes=("ofdm",), snr_db=[20.0, 35.0])
-    sc = S.schemes["ofdm"]
-    mm = harness.oracle_mmse(S, sc)
+    S = harness.setup("default", schemes=("ofdm",), snr_db=[20.0, 35.0])
     ref = np.zeros_like(out[0][3])
     for _, first, n, _ in out:
-        ref += refsim.simulate(11, first, n // 32, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time,
-                               S.n_iter, [mm])["err"]
+        ref += harness.simulate(S, 11, first, n // 32, ["ofdm"])["err"]
     assert np.array_equal(out[0][3], ref)

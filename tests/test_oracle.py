@@ -55,16 +55,15 @@ def test_theory_bep_256qam_lower_bound_of_figure5():
 
 def test_jakes_statistics():
     """Sum of sinusoids: E|h_tau|^2 = PDPn[tau], E{h(n) h*(n+k)} ~ J0(2 pi fD k dt)."""
-    from dsce.configs import build_setup
-    S = build_setup("default", schemes=())
-    ch = S.channel
-    irs = np.stack([refsim.jakes_ir(3, r, S.N, ch.dt, ch.PowerDelayProfileNormalized, ch.IndexDelayTaps,
-                                    ch.MaximumDopplerShift, ch.Paths) for r in range(300)])
+    S = harness.setup("default", schemes=())
+    ch = S.chan
+    irs = np.stack([refsim.jakes_ir(3, r, S.N, ch["dt"], ch["pdp_norm"], ch["idx_taps"], ch["fD"], ch["paths"])
+                    for r in range(300)])
     p = np.mean(np.abs(irs) ** 2, axis=(0, 1))
-    np.testing.assert_allclose(p, ch.PowerDelayProfileNormalized, rtol=0.12)
+    np.testing.assert_allclose(p, ch["pdp_norm"], rtol=0.12)
     lag = 200
-    c = np.mean(irs[:, :-lag, 0] * np.conj(irs[:, lag:, 0])) / ch.PowerDelayProfileNormalized[0]
-    tc = refsim.time_correlation(S.N, ch.dt, ch.MaximumDopplerShift)[S.N - 1 + lag]
+    c = np.mean(irs[:, :-lag, 0] * np.conj(irs[:, lag:, 0])) / ch["pdp_norm"][0]
+    tc = refsim.time_correlation(S.N, ch["dt"], ch["fD"])[S.N - 1 + lag]
     assert abs(c.real - tc) < 0.12
 
 
@@ -101,9 +100,8 @@ def test_correlation_matrix_literal_structure():
 
 @pytest.fixture(scope="module")
 def c2():
-    from dsce.configs import build_setup
-    S = build_setup("default", schemes=("ofdm",))
-    return S, harness.oracle_mmse(S, S.schemes["ofdm"])
+    S = harness.setup("default", schemes=("ofdm",))
+    return S, harness.oracle_mmse(S, "ofdm")
 
 
 def test_correlation_invariants(c2):
@@ -117,7 +115,7 @@ def test_correlation_invariants(c2):
     nz = np.abs(w[w != 0])
     assert nz.min() >= 1e-8                               # script:287-289 threshold
     # block-diagonal OFDM estimator: only same-symbol (r, c) pairs survive
-    LK = S.schemes["ofdm"].LK
+    LK = S.schemes["ofdm"]["G"].shape[1]
     W3 = w[:, 0].reshape(LK, LK, -1, order="F")
     r, c = np.nonzero(np.abs(W3).sum(axis=2))
     assert np.all(r // 24 == c // 24)
@@ -126,10 +124,8 @@ def test_correlation_invariants(c2):
 def test_oracle_regression_vectors(c2):
     S, mm = c2
     g = json.load(open(os.path.join(GOLD, "oracle_c2_small.json")))
-    sc = S.schemes["ofdm"]
     tr = {}
-    res = refsim.simulate(g["seed"], 0, 2, harness.oracle_chan(S), [harness.oracle_scheme(sc)], S.pn_time, S.n_iter,
-                          [mm], trace=tr)
+    res = harness.simulate(S, g["seed"], 0, 2, ["ofdm"], trace=tr)
     ir = tr["ir"][0]
     for n, v in g["ir_rep0_samples"].items():
         n = int(n)
@@ -184,7 +180,7 @@ def test_doubly_flat_oracle_vs_theory_low_snr():
     from dsce.configs import build_doubly_flat_setup
     S = build_doubly_flat_setup(snr_db=[0.0, 5.0])
     sc = S.schemes["ofdm"]
-    d = harness.oracle_scheme(sc)
+    d = harness.product_scheme_dict(sc)
     d.update(noise_slot=sc.extras["noise_slot"], interp=sc.extras["interp"])
     n = 150
     r = refsim.simulate_doubly_flat(0x5EED0001, 0, n, S.N, [d], S.pn_time)
@@ -192,3 +188,47 @@ def test_doubly_flat_oracle_vs_theory_low_snr():
     th = refsim.bit_error_probability_doubly_flat_rayleigh(S.snr_db, sc.const.SymbolMapping, sc.const.BitMapping)
     assert np.all(np.abs(ber[1] / th - 1) < 0.15), (ber[1], th)
     assert np.all(ber[0] > ber[1])                 # interpolated channel is worse than perfect CSI
+
+
+# ---------------------------------------------------------------------------
+# SURVEY §8(c)-4 fixtures: the oracle and its setup restatement recomputed and
+# compared with the committed vectors of tests/golden/make_golden.py
+# ---------------------------------------------------------------------------
+def _golden():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLD, "make_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _same(a, b, path="", rtol=1e-10):
+    if isinstance(a, dict):
+        assert set(a) == set(b), path
+        for k in a:
+            _same(a[k], b[k], path + "/" + str(k), rtol)
+    elif isinstance(a, (list, tuple)):
+        assert len(a) == len(b), path
+        for i, (x, y) in enumerate(zip(a, b)):
+            _same(x, y, "%s[%d]" % (path, i), rtol)
+    elif isinstance(a, float) or isinstance(b, float):
+        assert abs(a - b) <= rtol * max(1.0, abs(a), abs(b)), (path, a, b)
+    else:
+        assert a == b, (path, a, b)
+
+
+@pytest.mark.parametrize("name,fname,schemes", [("default", "setup_default.json", ("fbmc_aux", "fbmc_cod", "ofdm")),
+                                                ("c5", "setup_c5.json", ("fbmc_aux", "ofdm"))])
+def test_setup_fixtures(name, fname, schemes):
+    got = json.loads(json.dumps(_golden().setup_fixture(name, schemes)))
+    _same(got, json.load(open(os.path.join(GOLD, fname))))
+
+
+@pytest.mark.parametrize("tag", ["c3", "c4", "c5"])
+def test_oracle_fixtures(tag):
+    """8 realisations of IR / D = Q'HG, R_hP, W slices and int64 counts (C3, C4:
+    FBMC auxiliary / coding 24 x 30; C5: OFDM 48 x 14 at 720 kHz)."""
+    got = json.loads(json.dumps(_golden().oracle_fixture(tag)))
+    ref = json.load(open(os.path.join(GOLD, "oracle_%s_small.json" % tag)))
+    assert got["err_reps_0_2"] == ref["err_reps_0_2"] and got["nbits"] == ref["nbits"]
+    _same(got, ref, rtol=1e-9)

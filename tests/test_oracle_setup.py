@@ -44,7 +44,7 @@ def test_fbmc_structure(both):
     fb = O["fbmc"]
     G, Q = fb.tx_matrix(), fb.rx_matrix().conj().T
     D = Q.conj().T @ G
-    np.testing.assert_allclose(D.real, np.eye(D.shape[0]), atol=1e-7)
+    np.testing.assert_allclose(D.real, np.eye(D.shape[0]), atol=1e-6)   # Hermite prototype: near-orthogonal
     rng = np.random.default_rng(2)
     x = rng.standard_normal(G.shape[1])
     np.testing.assert_allclose(fb.modulation(x), G @ x, atol=1e-12)
@@ -56,9 +56,9 @@ def test_precoders_cancel_pilot_interference(both):
     imaginary interference at the pilots; the power normalisation gives
     ||P||_F^2 = LK (:86, :200)."""
     O, _ = both
-    for key in ("fbmc_aux", "fbmc_cod"):
+    for key, sir in (("fbmc_aux", 38.0), ("fbmc_cod", 28.0)):       # 28 / 20 cancelled interferers
         m = O["schemes"][key]["iic"]
-        assert np.all(m["SIR_dB"] > 30), (key, m["SIR_dB"].min())
+        assert np.all(m["SIR_dB"] > sir), (key, m["SIR_dB"].min())
         assert abs(np.sum(np.abs(m["P"]) ** 2) - m["P"].shape[0]) < 1e-9
     assert O["schemes"]["fbmc_aux"]["iic"]["NA"] == 64
     assert O["schemes"]["fbmc_cod"]["n_data"] == 720 - 32
@@ -68,11 +68,12 @@ def test_precoders_cancel_pilot_interference(both):
 def test_product_host_mirror_equals_oracle_setup(both, key):
     O, S = both
     o, p = O["schemes"][key], S.schemes[key]
-    for f in ("G", "Q", "P"):
+    tie = key == "fbmc_cod"          # P and its no-edge mask: see test_coding_precoder_tie_class
+    for f in (("G", "Q") if tie else ("G", "Q", "P")):
         a, b = o[f], getattr(p, f)
         assert a.shape == b.shape, (key, f)
         np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max(), err_msg="%s %s" % (key, f))
-    for f, g in (("pilot_pos", "pilot_pos"), ("data_pos", "data_pos"), ("considered", "considered_symbols")):
+    for f, g in (("pilot_pos", "pilot_pos"), ("data_pos", "data_pos"), ("considered", "considered_symbols"))[:2 if tie else 3]:
         np.testing.assert_array_equal(np.asarray(getattr(p, g)), np.asarray(o[f]), err_msg="%s %s" % (key, f))
     for f in ("kappa", "data_div"):
         assert abs(getattr(p, f) - o[f]) <= 1e-12 * abs(o[f]), (key, f)
@@ -80,6 +81,39 @@ def test_product_host_mirror_equals_oracle_setup(both, key):
         (o["despread"], o["real_detect"], o["bits_slot"], o["pilot_slot"], o["n_data"])
     np.testing.assert_array_equal(p.const.SymbolMapping, o["symbols"])
     np.testing.assert_array_equal(p.const.BitMapping.astype(np.uint8), o["bitmap"])
+
+
+def test_coding_precoder_tie_class(both):
+    """The 'Coding' precoder is tie-sensitive (SURVEY §7 hard part 4): a
+    pilot's interferer set is |D(pilot, :)| >= the 21st-largest corner
+    interference magnitude (IIC.m:113-114), and at C4 that threshold falls
+    inside a class of 8 interferers whose magnitudes are equal in exact
+    arithmetic (0.0368577...); which 4 of them pass depends on the last bit of
+    the FFTs (MATLAB's FFTW: unknowable offline, so the choice is unpinned).
+    Pinned: per pilot the same number of interferers and the same set outside
+    the tie class, the same data-symbol count and power reduction, and both
+    precoders cancel the imaginary interference at the pilots (SIR)."""
+    O, S = both
+    m = O["schemes"]["fbmc_cod"]["iic"]
+    prod = S.schemes["fbmc_cod"].extras["iic"]
+    D = O["fbmc"].fbmc_matrix()
+    pm = np.zeros(D.shape[0])
+    pm[O["schemes"]["fbmc_cod"]["pilot_pos"]] = 1
+    L, K = O["L"], D.shape[0] // O["L"]
+    thr = None
+    abs_col = lambda j: np.abs(D[:, j]).reshape(L, K, order="F")
+    IM = np.concatenate([np.concatenate([abs_col(L * K - 1), abs_col(L * K - L)[1:, :]], 0),
+                         np.concatenate([abs_col(L - 1)[:, 1:], abs_col(0)[1:, 1:]], 0)], 1)
+    thr = np.sort(osu.col(IM))[::-1][20]
+    ci_o, ci_p = np.asarray(m["considered"]), np.asarray(prod.ConsideredInterferenceMatrix).reshape(-1, order="F")
+    pil = np.flatnonzero(pm == 1)
+    for ip in range(1, len(pil) + 1):
+        so, sp = set(np.flatnonzero(ci_o == -ip)), set(np.flatnonzero(ci_p == -ip))
+        assert len(so) == len(sp)
+        for x in so ^ sp:
+            assert abs(abs(D[pil[ip - 1], x]) - thr) <= 1e-12 * thr, (ip, x)
+    assert m["ND"] == prod.NrDataSymbols and abs(m["DPR"] - prod.DataPowerReduction) < 1e-12
+    assert np.all(prod.SIR_dB > 28.0) and np.all(m["SIR_dB"] > 28.0)
 
 
 def test_channel_and_sizes(both):
