@@ -1,24 +1,40 @@
 /*
- * dsce_mex.c — MEX gateway binding the reference's MATLAB host to libdsce.so.
- * Build (MATLAB R2018a+, interleaved complex):
+ * dsce_mex.c — MEX gateway binding the reference's MATLAB host to libdsce.so
+ * (include/dsce.h).  Build (MATLAB R2018a+, interleaved complex):
  *   mex -R2018a -I../../include dsce_mex.c -L../dsce -ldsce
- * Requires MATLAB's mex.h, which is not part of this image.
+ * MATLAB's mex.h is not part of this image; the gateway's
+ * argument checking is exercised on the CPU by tests/test_mex_gateway.py
+ * against a test-only mex.h stand-in and a recording stub of the C-ABI.
  *
- * Usage from MATLAB (one static context per MATLAB session, device 0 or set):
- *   dsce_mex('create', device)
- *   dsce_mex('set_channel', SamplingRate, PDPnormalized, N, fD, Paths, isUniform)
+ * One static context per MATLAB session.  Every command checks its argument
+ * count and classes; every output is sized from the engine's own state
+ * (dsce_scheme_dims), never from caller arguments.  MATLAB indices (scheme id,
+ * SNR index, pilot / data positions) are 1-based here, 0-based at the ABI.
+ *
+ *   dsce_mex('create' [, device])
+ *   dsce_mex('destroy')
+ *   dsce_mex('set_channel', SamplingRate, PDPnormalized, N, fD, Paths, DopplerModel)
+ *            DopplerModel: 0 'Jakes', 1 'Uniform', 2 'Discrete-Jakes', 3 'Discrete-Uniform'
  *   dsce_mex('set_snr', Pn_time, NrIterations)
  *   id = dsce_mex('add_scheme', L, K, G, Q, P, pilotIdx, dataIdx, considered, symbols,
  *                 kappa, dataDiv, despread, realDetect, bitsSlot, pilotSlot)
- *   dsce_mex('build_mmse', 1e-8)
- *   counts = dsce_mex('run', seed, firstRep, nRep)        % int64 [iter+1, snr, 2, 2, schemes]
- *   IR = dsce_mex('channel_realise', seed, rep)            % N x Ltap complex
- *   W  = dsce_mex('get_W', id, snrIndex, variant)          % LK^2*NP x 1 complex
- *   dsce_mex('destroy')
- * MATLAB indices (pilotIdx, dataIdx, snrIndex, id) are 1-based here and
- * converted to the ABI's 0-based convention.
+ *            G, Q: N x L*K; P: L*K x (NP+ND); pilotIdx: NP; dataIdx: ND (or [] with despread);
+ *            considered: ND logical; symbols: M (SymbolMapping sorted by bit label)
+ *   dsce_mex('build_mmse' [, ZeroThreshold])                      % default 1e-8
+ *   dsce_mex('set_batch', RepsPerBatch)
+ *   counts = dsce_mex('run', seed, firstRep, nRep)                % int64 [iter+1, snr, edge, csi, scheme]
+ *   bits   = dsce_mex('bits_per_rep', id)                         % [all; no-edge] per realisation
+ *   IR     = dsce_mex('channel_realise', seed, rep)               % N x Ltap complex (ImpulseResponse)
+ *   W      = dsce_mex('get_W', id, snrIndex, variant)             % (LK^2 NP) x 1 complex; variant 0 W, 1 W0
+ *   h      = dsce_mex('mmse_onetap', id, snrIndex, variant, hP)   % LK x n complex, hP: NP x n ('MMSE' slot)
+ *   dsce_mex('set_noise_slot', id, slot)
+ *   dsce_mex('set_interpolation', id, I)                          % I: LK x NP
+ *   d      = dsce_mex('scheme_dims', id)                          % [N Ltap LK NP ND Nsym nSchemes nSNR nIter]
+ *   f      = dsce_mex('path_info', id)                            % DSCE_PATH_* bits of the last run
+ *   dsce_mex('set_option', name, value)
  */
 #ifdef MATLAB_MEX_FILE
+#include <math.h>
 #include <string.h>
 
 #include "dsce.h"
@@ -35,123 +51,301 @@ static void check(int rc, const char* what) {
     if (rc != 0) mexErrMsgIdAndTxt("dsce:abi", "%s failed (%d): %s", what, rc, dsce_last_error(g_ctx));
 }
 
-static double* cplx(const mxArray* a, mxArray** tmp) {
-    /* interleaved complex view; real inputs are promoted */
-    if (mxIsComplex(a)) return (double*)mxGetComplexDoubles(a);
-    *tmp = mxDuplicateArray(a);
-    if (!mxMakeArrayComplex(*tmp)) mexErrMsgIdAndTxt("dsce:type", "cannot make complex");
-    return (double*)mxGetComplexDoubles(*tmp);
+/* ---- argument checking ---------------------------------------------------- */
+static const char* g_cmd = "";
+
+static void bad(int i, const char* what) {
+    mexErrMsgIdAndTxt("dsce:args", "dsce_mex('%s'): argument %d must be %s", g_cmd, i + 1, what);
 }
+
+static double scalar(const mxArray* a, int i) {
+    if (!mxIsNumeric(a) || mxIsComplex(a) || mxGetNumberOfElements(a) != 1) bad(i, "a real numeric scalar");
+    return mxGetScalar(a);
+}
+
+static int64_t integer(const mxArray* a, int i, int64_t lo) {
+    const double v = scalar(a, i);
+    if (v != floor(v) || v < (double)lo || v > 9.007199254740992e15) bad(i, "an integer in range");
+    return (int64_t)v;
+}
+
+static const double* real_doubles(const mxArray* a, int i, size_t n_expected) {
+    if (!mxIsDouble(a) || mxIsComplex(a)) bad(i, "a real double array");
+    if (n_expected != (size_t)-1 && mxGetNumberOfElements(a) != n_expected) bad(i, "of the expected length");
+    return mxGetDoubles(a);
+}
+
+/* interleaved complex view of a double array (real inputs promoted into *tmp) */
+static const double* cplx(const mxArray* a, int i, size_t rows, size_t cols, mxArray** tmp) {
+    if (!mxIsDouble(a)) bad(i, "a double array");
+    if ((rows != (size_t)-1 && mxGetM(a) != rows) || (cols != (size_t)-1 && mxGetN(a) != cols))
+        bad(i, "of the expected size");
+    if (mxIsComplex(a)) return (const double*)mxGetComplexDoubles(a);
+    *tmp = mxDuplicateArray(a);
+    if (!mxMakeArrayComplex(*tmp)) mexErrMsgIdAndTxt("dsce:type", "cannot make argument %d complex", i + 1);
+    return (const double*)mxGetComplexDoubles(*tmp);
+}
+
+static dsce_dims dims_of(int32_t id) {
+    dsce_dims d;
+    check(dsce_scheme_dims(g_ctx, id, &d), "dsce_scheme_dims");
+    return d;
+}
+
+static int32_t scheme_id(const mxArray* a, int i) { return (int32_t)(integer(a, i, 1) - 1); }
+
+/* ---- commands --------------------------------------------------------------- */
+typedef void (*cmd_fn)(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]);
+
+static void c_destroy(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    (void)nlhs; (void)plhs; (void)nrhs; (void)prhs;
+    cleanup();
+    mexUnlock();
+}
+
+static void c_set_channel(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    dsce_channel_desc d;
+    (void)nlhs; (void)plhs; (void)nrhs;
+    d.sampling_rate = scalar(prhs[1], 1);
+    d.pdp_norm = real_doubles(prhs[2], 2, (size_t)-1);
+    d.n_taps = (int32_t)mxGetNumberOfElements(prhs[2]);
+    d.n_samples = (int32_t)integer(prhs[3], 3, 2);
+    d.max_doppler = scalar(prhs[4], 4);
+    d.n_paths = (int32_t)integer(prhs[5], 5, 1);
+    d.doppler_model = (int32_t)integer(prhs[6], 6, 0);
+    check(dsce_set_channel(g_ctx, &d), "dsce_set_channel");
+}
+
+static void c_set_snr(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    (void)nlhs; (void)plhs; (void)nrhs;
+    check(dsce_set_snr(g_ctx, real_doubles(prhs[1], 1, (size_t)-1), (int32_t)mxGetNumberOfElements(prhs[1]),
+                       (int32_t)integer(prhs[2], 2, 0)), "dsce_set_snr");
+}
+
+static void c_add_scheme(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    mxArray *t[4] = {NULL, NULL, NULL, NULL};
+    dsce_scheme_desc d;
+    size_t np, nd, i, lk, n;
+    int32_t *pil, *dat, id;
+    uint8_t* cons;
+    const double *pp, *dp;
+    (void)nlhs; (void)nrhs;
+    memset(&d, 0, sizeof d);
+    d.n_subcarriers = (int32_t)integer(prhs[1], 1, 1);
+    d.n_symbols = (int32_t)integer(prhs[2], 2, 1);
+    lk = (size_t)d.n_subcarriers * (size_t)d.n_symbols;
+    n = mxGetM(prhs[3]);
+    np = mxGetNumberOfElements(prhs[6]);
+    nd = mxGetNumberOfElements(prhs[8]);
+    d.despread = (int32_t)integer(prhs[12], 12, 0);
+    if (!mxIsLogical(prhs[8]) && !mxIsDouble(prhs[8])) bad(8, "a logical or double vector");
+    if (mxGetNumberOfElements(prhs[7]) != (d.despread ? mxGetNumberOfElements(prhs[7]) : nd))
+        bad(7, "a vector of ND data positions (or [] with despread)");
+    d.G = cplx(prhs[3], 3, n, lk, &t[0]);
+    d.Q = cplx(prhs[4], 4, n, lk, &t[1]);
+    d.P = cplx(prhs[5], 5, lk, np + nd, &t[2]);
+    pp = real_doubles(prhs[6], 6, np);
+    dp = mxGetNumberOfElements(prhs[7]) ? real_doubles(prhs[7], 7, nd) : NULL;
+    d.symbols = cplx(prhs[9], 9, (size_t)-1, (size_t)-1, &t[3]);
+    pil = mxMalloc((np ? np : 1) * sizeof(int32_t));
+    dat = mxMalloc((nd ? nd : 1) * sizeof(int32_t));
+    cons = mxMalloc(nd ? nd : 1);
+    for (i = 0; i < np; ++i) pil[i] = (int32_t)pp[i] - 1;
+    for (i = 0; i < nd; ++i) {
+        dat[i] = dp ? (int32_t)dp[i] - 1 : 0;
+        cons[i] = mxIsLogical(prhs[8]) ? (mxGetLogicals(prhs[8])[i] ? 1 : 0) : (mxGetDoubles(prhs[8])[i] != 0.0);
+    }
+    d.n_tx_symbols = (int32_t)(np + nd);
+    d.n_pilots = (int32_t)np;
+    d.n_data = (int32_t)nd;
+    d.pilot_pos = pil;
+    d.data_pos = dat;
+    d.considered = cons;
+    d.mod_order = (int32_t)mxGetNumberOfElements(prhs[9]);
+    for (d.bits_per_symbol = 0; (1 << d.bits_per_symbol) < d.mod_order && d.bits_per_symbol < 30; ++d.bits_per_symbol) {}
+    d.kappa = scalar(prhs[10], 10);
+    d.data_div = scalar(prhs[11], 11);
+    d.real_detect = (int32_t)integer(prhs[13], 13, 0);
+    d.bits_slot = (int32_t)integer(prhs[14], 14, 0);
+    d.pilot_slot = (int32_t)integer(prhs[15], 15, 0);
+    {
+        const int rc = dsce_add_scheme(g_ctx, &d, &id);
+        mxFree(pil);
+        mxFree(dat);
+        mxFree(cons);
+        for (i = 0; i < 4; ++i)
+            if (t[i]) mxDestroyArray(t[i]);
+        check(rc, "dsce_add_scheme");
+    }
+    plhs[0] = mxCreateDoubleScalar(id + 1);
+}
+
+static void c_build_mmse(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    (void)nlhs; (void)plhs;
+    check(dsce_build_mmse(g_ctx, nrhs > 1 ? scalar(prhs[1], 1) : 1e-8), "dsce_build_mmse");
+}
+
+static void c_set_batch(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    (void)nlhs; (void)plhs; (void)nrhs;
+    check(dsce_set_batch(g_ctx, (int32_t)integer(prhs[1], 1, 64)), "dsce_set_batch");
+}
+
+static void c_run(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* counts are C-ordered [scheme][csi][edge][snr][stage]: reversed dims in MATLAB */
+    const dsce_dims d = dims_of(0);
+    mwSize dm[5];
+    (void)nlhs; (void)nrhs;
+    dm[0] = (mwSize)(d.n_iter + 1); dm[1] = (mwSize)d.n_snr; dm[2] = 2; dm[3] = 2; dm[4] = (mwSize)d.n_schemes;
+    plhs[0] = mxCreateNumericArray(5, dm, mxINT64_CLASS, mxREAL);
+    if ((int64_t)mxGetNumberOfElements(plhs[0]) != d.n_counters) mexErrMsgIdAndTxt("dsce:state", "counter shape");
+    check(dsce_run(g_ctx, (uint64_t)integer(prhs[1], 1, 0), (uint64_t)integer(prhs[2], 2, 0),
+                   (uint64_t)integer(prhs[3], 3, 0), (int64_t*)mxGetInt64s(plhs[0])), "dsce_run");
+}
+
+static void c_bits_per_rep(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    int64_t b[2];
+    (void)nlhs; (void)nrhs;
+    check(dsce_bits_per_rep(g_ctx, scheme_id(prhs[1], 1), b), "dsce_bits_per_rep");
+    plhs[0] = mxCreateDoubleMatrix(2, 1, mxREAL);
+    mxGetDoubles(plhs[0])[0] = (double)b[0];
+    mxGetDoubles(plhs[0])[1] = (double)b[1];
+}
+
+static void c_channel_realise(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    const dsce_dims d = dims_of(0);
+    (void)nlhs; (void)nrhs;
+    plhs[0] = mxCreateDoubleMatrix((mwSize)d.n_samples, (mwSize)d.n_taps, mxCOMPLEX);
+    check(dsce_channel_realise(g_ctx, (uint64_t)integer(prhs[1], 1, 0), (uint64_t)integer(prhs[2], 2, 0),
+                               (double*)mxGetComplexDoubles(plhs[0])), "dsce_channel_realise");
+}
+
+static void c_get_W(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    const int32_t id = scheme_id(prhs[1], 1);
+    const dsce_dims d = dims_of(id);
+    (void)nlhs; (void)nrhs;
+    plhs[0] = mxCreateDoubleMatrix((mwSize)d.lk * (mwSize)d.lk * (mwSize)d.n_pilots, 1, mxCOMPLEX);
+    check(dsce_get_W(g_ctx, id, (int32_t)integer(prhs[2], 2, 1) - 1, (int32_t)integer(prhs[3], 3, 0),
+                     (double*)mxGetComplexDoubles(plhs[0])), "dsce_get_W");
+}
+
+static void c_mmse_onetap(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* the 'MMSE' slot of PilotSymbolAidedChannelEstimation (PSACE.m:128-129) */
+    const int32_t id = scheme_id(prhs[1], 1);
+    const dsce_dims d = dims_of(id);
+    mxArray* t = NULL;
+    const double* hp;
+    size_t n;
+    (void)nlhs; (void)nrhs;
+    if (mxGetM(prhs[4]) != (size_t)d.n_pilots) bad(4, "an NP x n matrix of LS pilot estimates");
+    n = mxGetN(prhs[4]);
+    if (n < 1) bad(4, "non-empty");
+    hp = cplx(prhs[4], 4, (size_t)d.n_pilots, n, &t);
+    plhs[0] = mxCreateDoubleMatrix((mwSize)d.lk, (mwSize)n, mxCOMPLEX);
+    {
+        const int rc = dsce_mmse_onetap(g_ctx, id, (int32_t)integer(prhs[2], 2, 1) - 1,
+                                        (int32_t)integer(prhs[3], 3, 0), hp, (int32_t)n,
+                                        (double*)mxGetComplexDoubles(plhs[0]));
+        if (t) mxDestroyArray(t);
+        check(rc, "dsce_mmse_onetap");
+    }
+}
+
+static void c_set_noise_slot(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* SimpleVersion_DoublyFlat.m:125-126 */
+    (void)nlhs; (void)plhs; (void)nrhs;
+    check(dsce_set_noise_slot(g_ctx, scheme_id(prhs[1], 1), (int32_t)integer(prhs[2], 2, 0)), "dsce_set_noise_slot");
+}
+
+static void c_set_interpolation(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* I = LK x NP weights of a PilotSymbolAidedChannelEstimation ('linear',
+       'MovingBlockAverage', ...), e.g. ChannelInterpolation of the NP unit vectors */
+    const int32_t id = scheme_id(prhs[1], 1);
+    const dsce_dims d = dims_of(id);
+    mxArray* t = NULL;
+    const double* I;
+    (void)nlhs; (void)plhs; (void)nrhs;
+    I = cplx(prhs[2], 2, (size_t)d.lk, (size_t)d.n_pilots, &t);
+    {
+        const int rc = dsce_set_interpolation(g_ctx, id, I);
+        if (t) mxDestroyArray(t);
+        check(rc, "dsce_set_interpolation");
+    }
+}
+
+static void c_scheme_dims(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    const dsce_dims d = dims_of(scheme_id(prhs[1], 1));
+    double* o;
+    (void)nlhs; (void)nrhs;
+    plhs[0] = mxCreateDoubleMatrix(1, 9, mxREAL);
+    o = mxGetDoubles(plhs[0]);
+    o[0] = d.n_samples; o[1] = d.n_taps; o[2] = d.lk; o[3] = d.n_pilots; o[4] = d.n_data;
+    o[5] = d.n_tx_symbols; o[6] = d.n_schemes; o[7] = d.n_snr; o[8] = d.n_iter;
+}
+
+static void c_path_info(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    uint32_t f = 0;
+    (void)nlhs; (void)nrhs;
+    check(dsce_path_info(g_ctx, scheme_id(prhs[1], 1), &f), "dsce_path_info");
+    plhs[0] = mxCreateDoubleScalar((double)f);
+}
+
+static void c_set_option(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    char name[64];
+    (void)nlhs; (void)plhs; (void)nrhs;
+    if (!mxIsChar(prhs[1]) || mxGetString(prhs[1], name, sizeof name)) bad(1, "an option name");
+    check(dsce_set_option(g_ctx, name, integer(prhs[2], 2, -1)), "dsce_set_option");
+}
+
+static const struct {
+    const char* name;
+    int nrhs_min, nrhs_max, nlhs;
+    cmd_fn fn;
+} CMDS[] = {
+    {"destroy", 1, 1, 0, c_destroy},
+    {"set_channel", 7, 7, 0, c_set_channel},
+    {"set_snr", 3, 3, 0, c_set_snr},
+    {"add_scheme", 16, 16, 1, c_add_scheme},
+    {"build_mmse", 1, 2, 0, c_build_mmse},
+    {"set_batch", 2, 2, 0, c_set_batch},
+    {"run", 4, 4, 1, c_run},
+    {"bits_per_rep", 2, 2, 1, c_bits_per_rep},
+    {"channel_realise", 3, 3, 1, c_channel_realise},
+    {"get_W", 4, 4, 1, c_get_W},
+    {"mmse_onetap", 5, 5, 1, c_mmse_onetap},
+    {"set_noise_slot", 3, 3, 0, c_set_noise_slot},
+    {"set_interpolation", 3, 3, 0, c_set_interpolation},
+    {"scheme_dims", 2, 2, 1, c_scheme_dims},
+    {"path_info", 2, 2, 1, c_path_info},
+    {"set_option", 3, 3, 0, c_set_option},
+};
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     char cmd[32];
-    if (nrhs < 1 || mxGetString(prhs[0], cmd, sizeof cmd)) mexErrMsgIdAndTxt("dsce:usage", "dsce_mex(cmd, ...)");
+    size_t i;
+    if (nrhs < 1 || !mxIsChar(prhs[0]) || mxGetString(prhs[0], cmd, sizeof cmd))
+        mexErrMsgIdAndTxt("dsce:usage", "dsce_mex(cmd, ...): cmd must be a command name");
+    g_cmd = cmd;
     if (!strcmp(cmd, "create")) {
-        cleanup();
-        check(dsce_create(nrhs > 1 ? (int)mxGetScalar(prhs[1]) : 0, &g_ctx), "dsce_create");
+        if (nrhs > 2) mexErrMsgIdAndTxt("dsce:usage", "dsce_mex('create' [, device])");
+        {
+            const int dev = nrhs > 1 ? (int)integer(prhs[1], 1, 0) : 0;
+            cleanup();
+            check(dsce_create(dev, &g_ctx), "dsce_create");
+        }
         mexAtExit(cleanup);
         mexLock();
         return;
     }
-    if (!g_ctx) mexErrMsgIdAndTxt("dsce:state", "call dsce_mex('create') first");
-    if (!strcmp(cmd, "destroy")) {
-        cleanup();
-        mexUnlock();
-    } else if (!strcmp(cmd, "set_channel")) {
-        dsce_channel_desc d;
-        d.sampling_rate = mxGetScalar(prhs[1]);
-        d.pdp_norm = mxGetDoubles(prhs[2]);
-        d.n_taps = (int32_t)mxGetNumberOfElements(prhs[2]);
-        d.n_samples = (int32_t)mxGetScalar(prhs[3]);
-        d.max_doppler = mxGetScalar(prhs[4]);
-        d.n_paths = (int32_t)mxGetScalar(prhs[5]);
-        d.doppler_model = (int32_t)mxGetScalar(prhs[6]);
-        check(dsce_set_channel(g_ctx, &d), "dsce_set_channel");
-    } else if (!strcmp(cmd, "set_snr")) {
-        check(dsce_set_snr(g_ctx, mxGetDoubles(prhs[1]), (int32_t)mxGetNumberOfElements(prhs[1]),
-                           (int32_t)mxGetScalar(prhs[2])), "dsce_set_snr");
-    } else if (!strcmp(cmd, "add_scheme")) {
-        mxArray *t1 = NULL, *t2 = NULL, *t3 = NULL, *t4 = NULL;
-        dsce_scheme_desc d;
-        size_t np = mxGetNumberOfElements(prhs[6]), nd = mxGetNumberOfElements(prhs[8]), i;
-        int32_t *pil = mxMalloc(np * sizeof(int32_t)), *dat = mxMalloc(nd * sizeof(int32_t));
-        uint8_t* cons = mxMalloc(nd);
-        const double* pp = mxGetDoubles(prhs[6]);
-        const double* dp = mxGetNumberOfElements(prhs[7]) ? mxGetDoubles(prhs[7]) : NULL;
-        const mxLogical* cp = mxGetLogicals(prhs[8]);
-        int32_t id;
-        for (i = 0; i < np; ++i) pil[i] = (int32_t)pp[i] - 1;
-        for (i = 0; i < nd; ++i) { dat[i] = dp ? (int32_t)dp[i] - 1 : 0; cons[i] = cp[i] ? 1 : 0; }
-        d.n_subcarriers = (int32_t)mxGetScalar(prhs[1]);
-        d.n_symbols = (int32_t)mxGetScalar(prhs[2]);
-        d.G = cplx(prhs[3], &t1);
-        d.Q = cplx(prhs[4], &t2);
-        d.P = cplx(prhs[5], &t3);
-        d.n_tx_symbols = (int32_t)mxGetN(prhs[5]);
-        d.n_pilots = (int32_t)np;
-        d.n_data = (int32_t)nd;
-        d.pilot_pos = pil;
-        d.data_pos = dat;
-        d.considered = cons;
-        d.symbols = cplx(prhs[9], &t4);
-        d.mod_order = (int32_t)mxGetNumberOfElements(prhs[9]);
-        for (d.bits_per_symbol = 0; (1 << d.bits_per_symbol) < d.mod_order; ++d.bits_per_symbol) {}
-        d.kappa = mxGetScalar(prhs[10]);
-        d.data_div = mxGetScalar(prhs[11]);
-        d.despread = (int32_t)mxGetScalar(prhs[12]);
-        d.real_detect = (int32_t)mxGetScalar(prhs[13]);
-        d.bits_slot = (int32_t)mxGetScalar(prhs[14]);
-        d.pilot_slot = (int32_t)mxGetScalar(prhs[15]);
-        check(dsce_add_scheme(g_ctx, &d, &id), "dsce_add_scheme");
-        plhs[0] = mxCreateDoubleScalar(id + 1);
-        mxFree(pil); mxFree(dat); mxFree(cons);
-        if (t1) mxDestroyArray(t1);
-        if (t2) mxDestroyArray(t2);
-        if (t3) mxDestroyArray(t3);
-        if (t4) mxDestroyArray(t4);
-    } else if (!strcmp(cmd, "build_mmse")) {
-        check(dsce_build_mmse(g_ctx, mxGetScalar(prhs[1])), "dsce_build_mmse");
-    } else if (!strcmp(cmd, "run")) {
-        /* counts are C-ordered [scheme][csi][edge][snr][stage]: reversed dims in MATLAB */
-        mwSize dims[5];
-        int32_t nsch = (int32_t)mxGetScalar(prhs[4]), nsnr = (int32_t)mxGetScalar(prhs[5]),
-                nst = (int32_t)mxGetScalar(prhs[6]);
-        dims[0] = nst; dims[1] = nsnr; dims[2] = 2; dims[3] = 2; dims[4] = nsch;
-        plhs[0] = mxCreateNumericArray(5, dims, mxINT64_CLASS, mxREAL);
-        check(dsce_run(g_ctx, (uint64_t)mxGetScalar(prhs[1]), (uint64_t)mxGetScalar(prhs[2]),
-                       (uint64_t)mxGetScalar(prhs[3]), (int64_t*)mxGetInt64s(plhs[0])), "dsce_run");
-    } else if (!strcmp(cmd, "channel_realise")) {
-        plhs[0] = mxCreateDoubleMatrix((mwSize)mxGetScalar(prhs[3]), (mwSize)mxGetScalar(prhs[4]), mxCOMPLEX);
-        check(dsce_channel_realise(g_ctx, (uint64_t)mxGetScalar(prhs[1]), (uint64_t)mxGetScalar(prhs[2]),
-                                   (double*)mxGetComplexDoubles(plhs[0])), "dsce_channel_realise");
-    } else if (!strcmp(cmd, "get_W")) {
-        plhs[0] = mxCreateDoubleMatrix((mwSize)mxGetScalar(prhs[4]), 1, mxCOMPLEX);
-        check(dsce_get_W(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, (int32_t)mxGetScalar(prhs[2]) - 1,
-                         (int32_t)mxGetScalar(prhs[3]), (double*)mxGetComplexDoubles(plhs[0])), "dsce_get_W");
-    } else if (!strcmp(cmd, "mmse_onetap")) {
-        /* h = dsce_mex('mmse_onetap', id, snrIndex, variant, hP_LS [, LK]) */
-        mxArray* t = NULL;
-        const int32_t n = 1;
-        const mwSize lk = nrhs > 5 ? (mwSize)mxGetScalar(prhs[5]) : 0;
-        plhs[0] = mxCreateDoubleMatrix(lk, 1, mxCOMPLEX);
-        check(dsce_mmse_onetap(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, (int32_t)mxGetScalar(prhs[2]) - 1,
-                               (int32_t)mxGetScalar(prhs[3]), cplx(prhs[4], &t), n,
-                               (double*)mxGetComplexDoubles(plhs[0])), "dsce_mmse_onetap");
-        if (t) mxDestroyArray(t);
-    } else if (!strcmp(cmd, "set_noise_slot")) {
-        /* dsce_mex('set_noise_slot', id, slot)  (SimpleVersion_DoublyFlat.m:125-126) */
-        check(dsce_set_noise_slot(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, (int32_t)mxGetScalar(prhs[2])),
-              "dsce_set_noise_slot");
-    } else if (!strcmp(cmd, "set_interpolation")) {
-        /* dsce_mex('set_interpolation', id, I): I = LK x NP weights of a
-           PilotSymbolAidedChannelEstimation ('linear', 'MovingBlockAverage', ...),
-           e.g. obtained by applying ChannelInterpolation to the NP unit vectors */
-        mxArray* t = NULL;
-        check(dsce_set_interpolation(g_ctx, (int32_t)mxGetScalar(prhs[1]) - 1, cplx(prhs[2], &t)),
-              "dsce_set_interpolation");
-        if (t) mxDestroyArray(t);
-    } else {
-        mexErrMsgIdAndTxt("dsce:usage", "unknown command '%s'", cmd);
+    for (i = 0; i < sizeof CMDS / sizeof CMDS[0]; ++i) {
+        if (strcmp(cmd, CMDS[i].name)) continue;
+        if (nrhs < CMDS[i].nrhs_min || nrhs > CMDS[i].nrhs_max)
+            mexErrMsgIdAndTxt("dsce:usage", "dsce_mex('%s'): expected %d to %d arguments, got %d", cmd,
+                              CMDS[i].nrhs_min, CMDS[i].nrhs_max, nrhs);
+        if (nlhs > CMDS[i].nlhs) mexErrMsgIdAndTxt("dsce:usage", "dsce_mex('%s'): too many outputs", cmd);
+        if (!g_ctx) mexErrMsgIdAndTxt("dsce:state", "call dsce_mex('create') first");
+        CMDS[i].fn(nlhs, plhs, nrhs, prhs);
+        return;
     }
+    mexErrMsgIdAndTxt("dsce:usage", "unknown command '%s'", cmd);
 }
 #endif /* MATLAB_MEX_FILE */
