@@ -402,6 +402,39 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
             s.k.pm_stride = stride;
             s.k.pm_a = dupload(c, pa);
         }
+        // FFT form (SchemeK::pf_ok): 24-row blocks, 24-sample windows, G / Q^H
+        // equal to gs w^(l m) / qs w^(-l m) (w = e^(2 pi i / 24), m = n - klo) to
+        // 1e-12 relative, and the md samples before the window a cyclic prefix
+        bool fok = s.k.pic_ok && md <= 1 && nb > 0;
+        double2 gsc = make_double2(0, 0), qsc = make_double2(0, 0);
+        if (fok) {
+            gsc = s.G[(size_t)s.qband.row0[0] * N + s.qband.klo[0]];
+            qsc = s.qband.vals[s.qband.off[0]];
+            fok = std::hypot(gsc.x, gsc.y) > 0 && std::hypot(qsc.x, qsc.y) > 0;
+        }
+        const double gm = std::hypot(gsc.x, gsc.y), qm = std::hypot(qsc.x, qsc.y);
+        for (int b = 0; b < nb && fok; ++b) {
+            const int r0 = s.qband.row0[b], klo = s.qband.klo[b], khi = s.qband.khi[b];
+            if (s.qband.nrows[b] != 24 || khi - klo != 24 || klo - md < 0 || r0 + 24 > LK) {
+                fok = false;
+                break;
+            }
+            for (int lr = 0; lr < 24 && fok; ++lr)
+                for (int m = -md; m < 24 && fok; ++m) {
+                    const int e = (((lr * m) % 24) + 24) % 24;
+                    const double ang = 2.0 * M_PI * e / 24.0;
+                    const double2 wv = make_double2(std::cos(ang), std::sin(ang));
+                    const double2 gmod = make_double2(gsc.x * wv.x - gsc.y * wv.y, gsc.x * wv.y + gsc.y * wv.x);
+                    const double2 gv = s.G[(size_t)(r0 + lr) * N + klo + m];
+                    if (std::hypot(gv.x - gmod.x, gv.y - gmod.y) > 1e-12 * gm) fok = false;
+                    if (m < 0) continue;
+                    const double2 qmod = make_double2(qsc.x * wv.x + qsc.y * wv.y, qsc.y * wv.x - qsc.x * wv.y);
+                    const double2 qv = s.qband.vals[s.qband.off[b] + (size_t)m * DSCE_RB + lr];
+                    if (std::hypot(qv.x - qmod.x, qv.y - qmod.y) > 1e-12 * qm) fok = false;
+                }
+        }
+        s.k.pf_ok = fok ? 1 : 0;
+        s.k.pf_scale = make_double2(qsc.x * gsc.x - qsc.y * gsc.y, qsc.x * gsc.y + qsc.y * gsc.x);
     }
     // W band: rows r, k = (c, p); c overlaps where Q-support(r) meets (H G)-support(c)
     int maxd = 0;
@@ -480,6 +513,8 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.grid_sym = dupload(c, grid);
     k.slI = lvI.size() > 1 ? 1.0 / (lvI[1] - lvI[0]) : 1.0;
     k.slQ = lvQ.size() > 1 ? 1.0 / (lvQ[1] - lvQ[0]) : 1.0;
+    k.lv0I = lvI.empty() ? 0.0 : lvI[0];
+    k.lv0Q = lvQ.empty() ? 0.0 : lvQ[0];
     k.p_ptr = dupload(c, pptr);
     k.p_col = dupload(c, pcol);
     k.p_val = dupload(c, pval);
@@ -827,14 +862,16 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.R = R;
     b.nsnr = c->nsnr;
     b.U = (int)U;
-    b.ir = dalloc<double2>(c, (size_t)c->ch.ntap * N * R, L);
+    // k_pic_mfma reads whole 32-row tiles of y and h and up to 3 samples past N
+    // of the taps through block-based buffer views: pad those allocations (zeroed)
+    b.ir = dalloc<double2>(c, (size_t)c->ch.ntap * N * R + 4 * (size_t)R, L);
     b.xp = dalloc<double2>(c, NP * R, L);
     b.sidx = dalloc<uint16_t>(c, ND * R, L);
     b.r0 = dalloc<double2>(c, N * R, L);
-    b.h = dalloc<double2>(c, LK * R, L);
+    b.h = dalloc<double2>(c, (LK + 32) * R, L);
     b.xs = dalloc<double2>(c, LK * R, L);
     b.ss = dalloc<double2>(c, N * R, L);
-    b.y = dalloc<double2>(c, LK * U, L);
+    b.y = dalloc<double2>(c, (LK + 32) * U, L);
     b.yest = dalloc<double2>(c, LK * U, L);
     b.yperf = dalloc<double2>(c, LK * U, L);
     b.hp = dalloc<double2>(c, NP * U, L);
@@ -847,6 +884,9 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.e2 = dalloc<double2>(c, LK * U, L);
     b.qe = dalloc<uint16_t>(c, ND * U, L);
     b.qp = dalloc<uint16_t>(c, ND * U, L);
+    DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
+    DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));
+    DSCE_HIP_CHECK(hipMemsetAsync(b.y + LK * U, 0, 32 * U * sizeof(double2), c->stream));
 }
 
 // One traced unit (dsce_trace_unit_ex): realisation lane `lane` of the batch at
@@ -923,7 +963,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
             const bool two = pfuse && op.streams == 2 && !tracing;
             // pic_ok schemes (OFDM): the whole perfect-CSI chain is one kernel
             // (k_pic_mfma / k_pic_chain, u in registers across the iterations)
-            const bool chain = pfuse && perfect_chain_ok(op, s.k, c->ch, b);
+            const bool chain = pfuse && perfect_chain_ok(op, s.k, c->ch, b, c->niter);
             // block-diagonal W + row-local P (OFDM): the MMSE stage of every IC
             // iteration rides in the contraction's epilogue (k_pilot_pre +
             // k_wpair3<..., true>); hP alternates between hp and hp2
@@ -1664,7 +1704,7 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     if (!slot) throw ApiError(DSCE_EINVAL, "unknown option '" + n + "'");
     if (n == "stage_rb" && value != 4 && value != 8 && value != 16) throw ApiError(DSCE_EINVAL, "stage_rb: 4 | 8 | 16");
     if (n == "jakes_rpw" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "jakes_rpw: 1 | 2");
-    if (n == "pic_chain" && (value < 0 || value > 2)) throw ApiError(DSCE_EINVAL, "pic_chain: 0 | 1 | 2");
+    if (n == "pic_chain" && (value < 0 || value > 3)) throw ApiError(DSCE_EINVAL, "pic_chain: 0 | 1 | 2 | 3");
     if (n == "streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "streams: 1 | 2");
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;

@@ -124,6 +124,7 @@ struct SchemeK {
     const double* lvQ;            // nQ ascending imag levels (nQ = 1, {0} for PAM)
     const int* grid_sym;          // nI * nQ -> symbol index
     double slI, slQ;              // 1 / level step (1 for a single level)
+    double lv0I, lv0Q;            // lowest levels (host copies of lvI[0], lvQ[0])
     // precoder P (LK x Nsym) and P^H (Nsym x LK), CSR
     const int* p_ptr;
     const int* p_col;
@@ -168,6 +169,11 @@ struct SchemeK {
     int pm_ok, pm_ksq;
     long long pm_stride;
     const double2* pm_a;
+    // FFT form of the chain (k_pic_fft): every Q^H block is qs DFT24 over its
+    // 24-sample window and every G block gs IDFT24 with a cyclic prefix >= the
+    // max tap delay (checked entry by entry at pack time); pf_scale = qs gs
+    int pf_ok;
+    double2 pf_scale;
 };
 
 struct ChannelK {

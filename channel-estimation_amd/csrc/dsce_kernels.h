@@ -12,7 +12,7 @@ struct Opts {
     int fuse_stage = 1;       // MMSE stage of the IC iterations fused into the contraction
     int wpair_3m = -1;        // 3M complex products in k_wpair3: -1 auto, 0 off (4 MFMAs), 1 on
     int wda_3m = 1;           // fused epilogue's diag(D_hat) in 3M form
-    int pic_chain = 2;        // perfect-CSI IC: 0 per-iteration passes, 1 VALU chain, 2 MFMA chain
+    int pic_chain = 3;        // perfect-CSI IC: 0 per-iteration passes, 1 VALU chain, 2 MFMA chain, 3 FFT chain
     int pfuse = 1;            // perfect-CSI detection fused into the second banded pass
     int stage_split = 0;      // 1: 3-kernel stage (k_ls_hest, k_detect, k_precode) for every scheme
     int stage_rb = 8;         // rows per wave of k_stage_fused: 4 | 8 | 16
@@ -37,6 +37,7 @@ enum : unsigned {
     PATH_STAGE_FUSED = 1u << 7,    // k_ls + k_stage_fused
     PATH_STAGE_SPLIT = 1u << 8,    // k_ls_hest + k_detect + k_precode
     PATH_NOISE_FUSED = 1u << 9,    // noise drawn inside the Q^H pass
+    PATH_PIC_FFT = 1u << 10,       // k_pic_fft (perfect-CSI chain by FFT, OFDM)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -134,7 +135,7 @@ unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, con
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
 // registers (pic_ok schemes); perfect_chain_ok tells when it applies.
-bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
+bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                               const PerfectDetectArgs* pd, int niter);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);

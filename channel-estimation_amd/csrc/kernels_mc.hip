@@ -630,6 +630,9 @@ struct StorePerfectDetect {
     int cstride_edge, cstride_snr;
     int U, R, snr0, last, M, nI, nQ, real_detect;
     double idd, sI, sQ;
+    // k_pic_mfma's folded slicer (nearest_lin): f = z scale + offset, top = n - 1
+    double scI, ofI, topI, scQ, ofQ, topQ;
+    double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
     double2* sym;
@@ -1084,9 +1087,68 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // counters is written.  Block = 4 waves = 64 units of one Q^H block (its A
 // tables staged in LDS once); grid: Q^H blocks x units/64, SNR-fastest
 // XCD-aware order.
-template <int KSQ, int NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))) k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
-                                                  int d0, int d1, StorePerfectDetect o, int niter) {
+// f64 MFMA with the A operand negated: the f64 form's blgp field is its neg
+// modifier (bit 0 = neg:[1,0,0]), so -a costs no v_xor / v_mov per k-step
+#define MFMA64NA(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 1)
+
+// Raw buffer view of a wave-uniform base (T8): a 32-bit per-lane byte offset plus
+// a wave-uniform one (SGPR) per load instead of 64-bit address arithmetic.
+// Callers keep every access inside the allocation (no reliance on the range check).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             (int)(unsigned)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull), 0x00020000);
+}
+__device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+}
+
+// Nearest level of a uniform level grid lv0 + i step (i < n) by rounding
+// f = (x - lv0) / step + 0.5, folded into one FMA.  An exact mid-point (f
+// integral, inside the grid) flags the lower neighbour as the tie alternative
+// (first-minimum rule of SignalConstellation.m:88, resolved on the grid by the
+// caller: a flag at level 0 reads level 0 twice); NaN / inf (h == 0) clamp into
+// the grid.
+__device__ __forceinline__ int nearest_lin(double x, double scale, double offset, double top, int& tie) {
+    const double f = fma(x, scale, offset);              // (x - lv0) / step + 0.5
+    const double c = fmin(fmax(floor(f), 0.0), top);
+    tie = f == c ? 1 : 0;                                // on the mid-point below level c
+    return (int)c;
+}
+
+// SH: bit q set when tap q reads the shifted sample (maxd - d_q = 1), so the
+// tap-delay selects are compile-time.
+//
+// Schedule (software-pipelined across the two row tiles, so the epilogue's
+// VALU / LDS / memory work has independent MFMAs to hide behind):
+//   before the loop      GEMM1 of iteration 1
+//   per iteration it     GEMM2 tile 0 (X formed on the fly and kept)
+//                        GEMM2 tile 1  ||  epilogue tile 0 of it
+//                        GEMM1 k-steps 0-3 of it + 1 (need tile-0 decisions only)
+//                                       ||  epilogue tile 1 of it
+//                        GEMM1 k-steps 4-5 of it + 1
+// Error counts go through LDS per (wave, iteration) and are added to the
+// counters once at the end (no divergent atomic inside the pipelined loop).
+static constexpr int PM_MAXIT = 32;
+static constexpr int PM_EPI_VALU = 6;
+
+// N x {1 MFMA, V VALU (+ D LDS reads)} scheduling groups (LLVM SchedGroupMask:
+// MFMA 0x8, VALU 0x2, DS_READ 0x100): the order the compiler emits this
+// region's matrix-core and vector work in
+template <int N, int V, int D>
+__device__ __forceinline__ void sched_interleave() {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x2, V, 0);
+        if (D) __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+    }
+}
+
+template <int KSQ, int NT, int SH, bool TRACE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     extern __shared__ double2 pm_lds[];
     int ug, blk;
     band_block(ord, sk.QH.nblk, ug, blk);
@@ -1104,6 +1166,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
     // padding), no-edge flag — read by the epilogue every iteration
     __shared__ double2 rpv[32];
     __shared__ int rdc[32];
+    __shared__ double hidl[8][256];                             // 1 / |h|^2 per lane row
+    __shared__ int cntl[4][PM_MAXIT];                           // per wave: n0 + (n1 << 16)
     {
         // every global load of the prologue is issued before the first wait
         // (clamped indices, masked values): guarded loads would each be a branch
@@ -1115,8 +1179,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
         for (int k = 0; k < NIT; ++k) av[k] = src[min(tid + 256 * k, NA - 1)];
         const double2 sv = o.symbols[min(tid, o.M - 1)];
         const int gv = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
-        const int lt = min(tid, 15);
-        const double li = o.lvI[min(lt, o.nI - 1)], lq = o.lvQ[min(lt, o.nQ - 1)];
         const int rt = min(tid, 31);
         const int row = row0 + (rt < nrows ? rt : 0);
         const double2 pv = o.row_pval[row];
@@ -1126,10 +1188,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
             if (tid + 256 * k < NA) sa[tid + 256 * k] = av[k];
         sym[tid] = make_double2(tid < o.M ? sv.x : 0.0, tid < o.M ? sv.y : 0.0);
         slt->grid[tid] = tid < o.nI * o.nQ ? gv : 0;
-        if (tid < 16) {
-            slt->lvI[tid] = tid < o.nI ? li : 0.0;
-            slt->lvQ[tid] = tid < o.nQ ? lq : 0.0;
-        }
         if (tid < 32) {
             rpv[tid] = pv;
             // data index << 1 | no-edge flag, or -1
@@ -1138,22 +1196,38 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
     }
     const double2* ga = sa;
     const double2* qa = sa + 2 * 6 * 64;
+    // y, h and the taps through buffer views based at the block (32-bit offsets;
+    // pic_mfma_ok bounds them).  Rows past the block's last and samples past N
+    // stay inside the allocations (ensure_buffers pads y, h by 32 rows and the
+    // taps by 4 samples, zeroed) and are masked / multiplied by zero columns.
+    const int rmax = nrows - 1;
+    const int ybase = row0 * U + unit, hbase = row0 * R + rl;
+    const __amdgpu_buffer_rsrc_t yrs = buf_rsrc(o.y + (size_t)row0 * U, (size_t)32 * U * sizeof(double2));
+    const __amdgpu_buffer_rsrc_t hrs = buf_rsrc(o.h + (size_t)row0 * R, (size_t)32 * R * sizeof(double2));
+    const __amdgpu_buffer_rsrc_t trs =
+        buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo) + 4) * R * sizeof(double2));
+    const unsigned yv0 = (unsigned)(kq * U + unit) * 16u, hv0 = (unsigned)(kq * R + rl) * 16u;
     // U in D layout: ur[t][r] = u[row0 + 16 t + kq + 4 r][unit]
-    // (loads unconditional, clamped row, then masked: a conditional load would be
-    // a branch with its own wait, eight serial round trips)
     double2 ur[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int row = 16 * t + kq + 4 * r;
-            ur[t][r] = o.u[(size_t)(row0 + (row < nrows ? row : 0)) * U + unit];
+            const int rr = 16 * t + kq + 4 * r;
+            ur[t][r] = o.u[(unsigned)(ybase + min(rr, rmax) * U)];
         }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             if (16 * t + kq + 4 * r >= nrows) ur[t][r] = make_double2(0.0, 0.0);
+    // 1 / |h|^2 of the lane's 8 rows (iteration-invariant; LDS, not registers)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int rr = 16 * (i >> 2) + kq + 4 * (i & 3);
+        const double2 hh = o.h[(unsigned)(hbase + min(rr, rmax) * R)];
+        hidl[i][tid] = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+    }
     __syncthreads();
     // transmitted symbol indices of the lane's 8 rows, fixed for the whole chain:
     // loaded once, 8 bits each, packed 4 per register (M <= 256)
@@ -1168,66 +1242,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
 #pragma unroll
         for (int i = 0; i < 8; ++i) txp[i >> 2] |= ((unsigned)tv[i] & 0xffu) << (8 * (i & 3));
     }
-    // tap delay offsets into T: X[j] uses T[j + maxd - d_q] (maxd <= 1)
-    const int maxd = max(d0, NT > 1 ? d1 : 0);
-    const int c0 = maxd - d0, c1 = maxd - d1;
     const int src_lane = (l + 16) & 63;
-    const int snr = o.snr0 + (ug * WAVE) / R;
-    // 1 / |h|^2 of the lane's 8 rows: iteration-invariant, computed once (the
-    // IEEE division is ~12 FP64 instructions per row); not for KSQ 7, where the
-    // 16 extra registers would cost the third wave per SIMD
-    constexpr bool HID = KSQ <= 6;
-    double hid[2][4];
+
+    d4 tre[2], tim[2], are[2], aim[2];
+    double2 xs[KSQ];            // X of every k-step (GEMM2's B operand, reused by tile 1)
+    double2 hnext[NT];          // taps of GEMM2's first k-step, requested during GEMM1
+    int ncnt = 0;               // this lane's errors of the current iteration: n0 + (n1 << 16)
+
+    // tap q, sample klo + 4 k + kq: (q N + 4 k) R + kq R + rl past the block base
+    auto ld_taps = [&](int k, double2(&hv)[NT], int oz) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+        for (int q = 0; q < NT; ++q) hv[q] = buf_ld2(trs, hv0 + (unsigned)oz, (unsigned)((q * N + 4 * k) * R) * 16u);
+    };
+    // GEMM1 k-steps [KB, KE): T += G U (both row tiles)
+    auto gemm1 = [&](auto kb, auto ke) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int rr = 16 * t + kq + 4 * r;
-            const double2 hh = HID ? o.h[(size_t)(row0 + (rr < nrows ? rr : 0)) * R + rl] : make_double2(1.0, 0.0);
-            hid[t][r] = HID ? 1.0 / (hh.x * hh.x + hh.y * hh.y) : 1.0;
-        }
-    for (int it = 1; it <= niter; ++it) {
-        // the loads below are the same every iteration: an opaque zero keeps the
-        // compiler from hoisting them out of the loop (they would stay live
-        // across it and triple the register footprint)
-        int oz = 0;
-        asm volatile("" : "+v"(oz));
-        // taps of GEMM2's first k-step, requested now so GEMM1 covers their latency;
-        // every later k-step's taps are requested one step ahead
-        auto ld_taps = [&](int k, double2 (&hv)[NT]) {
-            const int n = klo + 4 * k + kq + oz;
-            const int nc = n < N ? n : N - 1;
-#pragma unroll
-            for (int q = 0; q < NT; ++q) hv[q] = ir[((size_t)q * N + nc) * R + rl];
-        };
-        double2 hnext[NT];
-        ld_taps(0, hnext);
-        // GEMM1: T = G U (2 row tiles x 6 k-steps)
-        d4 tre[2], tim[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            tre[t] = (d4){0.0, 0.0, 0.0, 0.0};
-            tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
-        }
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = decltype(kb)::value; k < decltype(ke)::value; ++k) {
             const double2 b = ur[k >> 2][k & 3];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const double2 a = ga[(t * 6 + k) * 64 + l];
                 tre[t] = MFMA64(a.x, b.x, tre[t]);
-                tre[t] = MFMA64(-a.y, b.y, tre[t]);
+                tre[t] = MFMA64NA(a.y, b.y, tre[t]);
                 tim[t] = MFMA64(a.x, b.y, tim[t]);
                 tim[t] = MFMA64(a.y, b.x, tim[t]);
             }
         }
-        // X in B layout (k-step s: sample klo + 4 s + kq) and GEMM2: acc = Q^H X
-        d4 are[2], aim[2];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            are[t] = (d4){0.0, 0.0, 0.0, 0.0};
-            aim[t] = (d4){0.0, 0.0, 0.0, 0.0};
-        }
+    };
+    // GEMM2 tile 0 with X in B layout formed on the fly (k-step s: sample
+    // klo + 4 s + kq): X[j] = sum_q IR_q[klo + j] T[j + maxd - d_q]
+    auto gemm2_t0 = [&](int oz) {
 #pragma unroll
         for (int k = 0; k < KSQ; ++k) {
             // T row j = 4k + kq is register (k&3) of tile k>>2 in this lane; row
@@ -1241,84 +1285,402 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3))
             double2 hcur[NT];
 #pragma unroll
             for (int q = 0; q < NT; ++q) hcur[q] = hnext[q];
-            if (k + 1 < KSQ) ld_taps(k + 1, hnext);
+            if (k + 1 < KSQ) ld_taps(k + 1, hnext, oz);
             double2 x = make_double2(0.0, 0.0);
-            c_fma(x, hcur[0], c0 ? t1 : tc);
-            if (NT > 1) c_fma(x, hcur[NT > 1 ? 1 : 0], c1 ? t1 : tc);
+            c_fma(x, hcur[0], (SH & 1) ? t1 : tc);
+            if (NT > 1) c_fma(x, hcur[NT > 1 ? 1 : 0], (SH & 2) ? t1 : tc);
+            xs[k] = x;
+            const double2 a = qa[k * 64 + l];
+            are[0] = MFMA64(a.x, x.x, are[0]);
+            are[0] = MFMA64NA(a.y, x.y, are[0]);
+            aim[0] = MFMA64(a.x, x.y, aim[0]);
+            aim[0] = MFMA64(a.y, x.x, aim[0]);
+        }
+    };
+    auto gemm2_t1 = [&]() {
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const double2 a = qa[(t * KSQ + k) * 64 + l];
-                are[t] = MFMA64(a.x, x.x, are[t]);
-                are[t] = MFMA64(-a.y, x.y, are[t]);
-                aim[t] = MFMA64(a.x, x.y, aim[t]);
-                aim[t] = MFMA64(a.y, x.x, aim[t]);
+        for (int k = 0; k < KSQ; ++k) {
+            const double2 a = qa[(KSQ + k) * 64 + l];
+            const double2 x = xs[k];
+            are[1] = MFMA64(a.x, x.x, are[1]);
+            are[1] = MFMA64NA(a.y, x.y, are[1]);
+            aim[1] = MFMA64(a.x, x.y, aim[1]);
+            aim[1] = MFMA64(a.y, x.x, aim[1]);
+        }
+    };
+    // epilogue of tile t on the D layout of acc: the lane's rows 16 t + kq + 4 r
+    // (register r), branch-free: y_perf = y - acc + h u, one-tap by h, slicer,
+    // counts, re-precoded decision into ur (pilot / padding rows are computed and
+    // masked; after the last iteration the new decisions are simply unused)
+    auto epi = [&](auto tcst, int it, int oz) {
+        constexpr int t = decltype(tcst)::value;
+        double2 yv[4], hv[4];
+        int dc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            dc[r] = rdc[16 * t + kq + 4 * r];
+            yv[r] = buf_ld2(yrs, yv0 + (unsigned)oz, (unsigned)((16 * t + 4 * r) * U) * 16u);
+            hv[r] = buf_ld2(hrs, hv0 + (unsigned)oz, (unsigned)((16 * t + 4 * r) * R) * 16u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            // one-tap z = y_perf / h with y_perf = y - acc + h u, as (y - acc) / h + u
+            const double2 d = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
+            const double id = hidl[4 * t + r][tid];
+            const double zx = fma(fma(d.x, hv[r].x, d.y * hv[r].y), id, ur[t][r].x);
+            const double zy = fma(fma(d.y, hv[r].x, -(d.x * hv[r].y)), id, ur[t][r].y);
+            int tI, tQ;
+            const int iI = nearest_lin(zx, o.scI, o.ofI, o.topI, tI);
+            const int iQ = nearest_lin(zy, o.scQ, o.ofQ, o.topQ, tQ);
+            // a decision exactly on a mid-point: the smallest symbol index among the
+            // tied grid points (MATLAB min's first index); otherwise all four
+            // reads are the same entry
+            const int jI = max(iI - tI, 0), jQ = max(iQ - tQ, 0);
+            const int iIn = __umul24(iI, o.nQ), jIn = __umul24(jI, o.nQ);
+            const int dp = min(min(slt->grid[iIn + iQ], slt->grid[jIn + iQ]),
+                               min(slt->grid[iIn + jQ], slt->grid[jIn + jQ]));
+            const bool data = dc[r] >= 0;
+            const int ne = data ? __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu))) : 0;
+            ncnt += ne + ((dc[r] & 1) ? ne << 16 : 0);
+            if (TRACE && data && unit == o.tr->unit) {
+                o.tr->yperf[(size_t)it * o.tr->LK + row0 + 16 * t + kq + 4 * r] = c_add(d, c_mul(hv[r], ur[t][r]));
+                o.tr->dec_p[(size_t)it * o.tr->ND + (dc[r] >> 1)] = dp;
+            }
+            double2 av = make_double2(0.0, 0.0);
+            c_fma(av, rpv[16 * t + kq + 4 * r], sym[dp]);
+            // component-wise select (a struct-valued ?: became an address select
+            // through scratch)
+            ur[t][r].x = data ? av.x : ur[t][r].x;
+            ur[t][r].y = data ? av.y : ur[t][r].y;
+        }
+    };
+    auto flush = [&](int it) {
+        // wave total of iteration it (uniform: every lane writes the same word)
+        cntl[w][it - 1] = wave_sum(ncnt);
+        ncnt = 0;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I4 = std::integral_constant<int, 4>;
+    using I6 = std::integral_constant<int, 6>;
+
+    {
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) tre[t] = tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
+        ld_taps(0, hnext, oz);
+        gemm1(I0{}, I6{});
+    }
+    for (int it = 1;; ++it) {
+        // the loads below are the same every iteration: an opaque zero keeps the
+        // compiler from hoisting them out of the loop (they would stay live
+        // across it and triple the register footprint)
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) are[t] = aim[t] = (d4){0.0, 0.0, 0.0, 0.0};
+        gemm2_t0(oz);
+        gemm2_t1();
+        epi(I0{}, it, oz);
+        // interleave: GEMM2 tile 0 with the X formation, then one MFMA of tile 1
+        // between every few epilogue instructions of tile 0
+        sched_interleave<KSQ * 4, 5, 0>();
+        sched_interleave<KSQ * 4, PM_EPI_VALU, 1>();
+        if (it == niter) break;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) tre[t] = tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
+        ld_taps(0, hnext, oz);
+        gemm1(I0{}, I4{});
+        epi(I1{}, it, oz);
+        flush(it);
+        gemm1(I4{}, I6{});
+        sched_interleave<32, PM_EPI_VALU, 1>();
+    }
+    {
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+        epi(I1{}, niter, oz);
+        flush(niter);
+    }
+    // counters of every iteration: lane 2 (it - 1) + edge of each wave
+    if (l < 2 * niter) {
+        const int it = (l >> 1) + 1, edge = l & 1;
+        const int v = (cntl[w][it - 1] >> (16 * edge)) & 0xffff;
+        const int snr = o.snr0 + (ug * WAVE) / R;
+        const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
+        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The perfect-CSI IC chain of OFDM by FFT on the VALU (k_pic_fft, SchemeK::pf_ok).
+// For OFDM with FFT size = subcarriers = 24 and no intermediate frequency, the
+// Q^H block of symbol k is qs * DFT and its G block is gs * IDFT with a cyclic
+// prefix (OFDM.m GetTXMatrix / GetRXMatrix; pack_scheme verifies every entry),
+// so (Q'HG u)_blk = qs gs FFT24(h_0 .* t + h_1 .* t(-1)), t = IFFT24(u): ~10x
+// fewer flops than the two dense 24 x 24 products k_pic_mfma runs on the matrix
+// cores — and on gfx950 f64 MFMA and VALU work do not overlap
+// (profiles/r02_mfma_valu_overlap.txt), so the flop count is what matters.
+// ---------------------------------------------------------------------------
+__constant__ double2 kW24[12] = {
+    {1.0, 0.0},
+    {0.96592582628906829, 0.25881904510252076},
+    {0.86602540378443865, 0.5},
+    {0.70710678118654752, 0.70710678118654752},
+    {0.5, 0.86602540378443865},
+    {0.25881904510252076, 0.96592582628906829},
+    {0.0, 1.0},
+    {-0.25881904510252076, 0.96592582628906829},
+    {-0.5, 0.86602540378443865},
+    {-0.70710678118654752, 0.70710678118654752},
+    {-0.86602540378443865, 0.5},
+    {-0.96592582628906829, 0.25881904510252076}};
+
+// x * (c + S i s) for compile-time c, s
+template <int S>
+__device__ __forceinline__ double2 cmul_const(double2 x, double c, double s) {
+    return make_double2(fma(x.x, c, -(S * s) * x.y), fma(x.y, c, (S * s) * x.x));
+}
+
+// DFT-3 with sign S (S = +1: sum x[n] e^{+2 pi i nk/3})
+template <int S>
+__device__ __forceinline__ void dft3(double2& a, double2& b, double2& c) {
+    constexpr double H = 0.86602540378443865;           // sin(60 deg)
+    const double2 t = c_add(b, c), d = c_sub(b, c);
+    const double2 m = make_double2(fma(-0.5, t.x, a.x), fma(-0.5, t.y, a.y));
+    const double2 r = make_double2((-S * H) * d.y, (S * H) * d.x);   // S i H (b - c)
+    a = c_add(a, t);
+    b = c_add(m, r);
+    c = c_sub(m, r);
+}
+
+// a * b with two FMAs (2 mul + 2 fma instead of 4 mul + 2 add under -ffp-contract=off)
+__device__ __forceinline__ double2 c_mulf(double2 a, double2 b) {
+    return make_double2(fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x));
+}
+
+// DPP move of a double / complex within each quad of lanes (quad_perm control)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double2 dpp_c(double2 v) { return make_double2(dpp_d<CTRL>(v.x), dpp_d<CTRL>(v.y)); }
+static constexpr int QP_XOR1 = 0xb1;    // quad_perm [1, 0, 3, 2]
+static constexpr int QP_XOR2 = 0x4e;    // quad_perm [2, 3, 0, 1]
+static constexpr int QP_PREV = 0x4b;    // quad_perm [3, 2, 0, 1]: the lane holding the previous time quarter
+
+// position of output k of dft6 in the array (k = k1 + 3 k2 lands at k2 + 2 k1)
+__host__ __device__ constexpr int p6(int k) { return k / 3 + 2 * (k % 3); }
+
+// DFT-6 with sign S in place, natural-order input, output k at x[p6(k)]:
+// n = 2 n1 + n2, k = k1 + 3 k2; DFT-3 over n1, twiddle w6^(S n2 k1), DFT-2 over n2
+template <int S>
+__device__ __forceinline__ void dft6(double2 (&x)[6]) {
+    constexpr double C60 = 0.86602540378443865;
+    dft3<S>(x[0], x[2], x[4]);
+    dft3<S>(x[1], x[3], x[5]);
+    x[3] = cmul_const<S>(x[3], 0.5, C60);                // w6^1
+    x[5] = cmul_const<S>(x[5], -0.5, C60);               // w6^2
+#pragma unroll
+    for (int k1 = 0; k1 < 3; ++k1) {
+        const double2 a = x[2 * k1], b = x[2 * k1 + 1];
+        x[2 * k1] = c_add(a, b);
+        x[2 * k1 + 1] = c_sub(a, b);
+    }
+}
+
+// k_pic_fft: a lane QUAD owns a unit.  Lane r holds the rows 4a + r (a = 0..5)
+// — u (the decisions), the iteration-invariant y / h and 1 / h, and the channel
+// taps of its samples, all in registers, so the iteration loop reads no memory
+// — and, in the time domain, the samples 6c + m' with c = bitrev2(r).  DFT-24 =
+// DFT-6 per lane x a radix-2 x 2 network across the quad (DPP quad_perm), lane
+// twiddles w24^(r m') from LDS; the output scale qs gs is folded into the
+// forward twiddles.  One-tap z = y_perf / h = y / h - acc / h + u.
+// 198 VGPRs, 2 waves / SIMD (3 waves forced spills or per-iteration reloads of
+// y, h and the taps: 4.45 / 5.25 ms vs 2.57 ms per 65536-realisation launch).
+// Block = 256 threads = 64 units of one symbol; grid: symbols x units/64,
+// SNR-fastest XCD-aware order.
+template <int NT, int SH, bool TRACE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 3;
+    const int U = o.U, R = o.R;
+    const int unit = ug * WAVE + w * 16 + (l >> 2);
+    const int rl = unit % R;
+    const int cq = (r >> 1) + 2 * (r & 1);                     // time quarter of this lane
+    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    __shared__ double2 sym[256];
+    __shared__ int sgrid[256];
+    __shared__ double2 rpv[24];
+    __shared__ int rdc[24];
+    __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
+    __shared__ double2 twb[2][4];                               // quad-network twiddle of lane r
+    __shared__ int cntl[4][PM_MAXIT];
+    {
+        // every global load of the prologue before the first LDS write (clamped)
+        const double2 a = o.symbols[min(tid, o.M - 1)];
+        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int rt = min(tid, 23);
+        const double2 pv = o.row_pval[row0 + rt];
+        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        const int e = ((tid / 6) % 4) * (tid % 6);              // twa: w24^(r m')
+        const double2 tw = kW24[e % 12];
+        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+        sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
+        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
+        if (tid < 24) {
+            rpv[tid] = pv;
+            rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;  // data index << 1 | no-edge, or -1
+        }
+        if (tid < 48) {
+            // IFFT w24^(r m'); FFT qs gs w24^-(r m') (the output scale of Q' H G)
+            const int dir = tid / 24;
+            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+        } else if (tid < 56) {
+            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
+            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
+        }
+    }
+    // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows
+    double2 u[6], yh[6], hc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int row = row0 + 4 * a + r;
+        u[a] = o.u[(size_t)row * U + unit];
+        const double2 yv = o.y[(size_t)row * U + unit];
+        const double2 hh = o.h[(size_t)row * R + rl];
+        const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+        hc[a] = make_double2(hh.x * id, -hh.y * id);            // 1 / h
+        yh[a] = c_mulf(yv, hc[a]);                               // y / h
+    }
+    __syncthreads();
+    // transmitted symbol indices (8 bits each) and data / no-edge masks
+    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int dc = rdc[4 * a + r];
+        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
+        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
+        dmask |= dc >= 0 ? 1u << a : 0u;
+        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
+    }
+    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
+    const __amdgpu_buffer_rsrc_t trs =
+        buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo)) * R * sizeof(double2));
+    const unsigned tv0 = (unsigned)(6 * cq * R + rl) * 16u;
+    // the channel taps of the lane's samples, iteration-invariant: registers
+    double2 taps[6][NT];
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+#pragma unroll
+        for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
+    int ncnt = 0;
+    for (int it = 1; it <= niter; ++it) {
+        // an opaque zero keeps the per-iteration LDS twiddle reads inside the loop
+        // (hoisted, they would hold 56 more registers)
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+        const int ro = r + oz;
+        // t = IDFT24(u): DFT-6 per lane, twiddle w24^(r m'), 4-point network
+        // across the quad (xor 2, lane twiddle, xor 1): lane r ends with the time
+        // samples 6 cq + m'
+        double2 x[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) x[a] = u[a];
+        dft6<1>(x);
+        double2 t[6];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const double2 p = c_mulf(x[p6(m)], twa[0][ro][m]);
+            const double2 pv = dpp_c<QP_XOR2>(p);
+            double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+            e = c_mulf(e, twb[0][ro]);
+            const double2 qv = dpp_c<QP_XOR1>(e);
+            t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+        }
+        // channel, in place, last sample first: x[m] = sum_q IR_q[m] t[m - d_q];
+        // t[-1] of the quarter is sample 5 of the previous quarter's lane (the
+        // cyclic prefix for quarter 0)
+        const double2 tprev = dpp_c<QP_PREV>(t[5]);
+#pragma unroll
+        for (int m = 5; m >= 0; --m) {
+            const double2 tp = m ? t[m - 1] : tprev;
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
+            t[m] = acc;
+        }
+        // acc = qs gs DFT24(x): network across the quad (xor 1, lane twiddle,
+        // xor 2) back to lane r = output residue, twiddle qs gs w24^-(r m'), DFT-6
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const double2 pv = dpp_c<QP_XOR1>(t[m]);
+            double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+            f = c_mulf(f, twb[1][ro]);
+            const double2 qv = dpp_c<QP_XOR2>(f);
+            x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][ro][m]);
+        }
+        dft6<-1>(x);
+        // epilogue per row 4a + r: z = y / h - acc / h + u, slicer, counts,
+        // re-precoded decision into u
+        int code[6], dp[6];
+        int anytie = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const double2 ah = c_mulf(x[p6(a)], hc[a]);
+            const double zx = (yh[a].x - ah.x) + u[a].x;
+            const double zy = (yh[a].y - ah.y) + u[a].y;
+            int tI, tQ;
+            const int iI = nearest_lin(zx, o.scI, o.ofI, o.topI, tI);
+            const int iQ = nearest_lin(zy, o.scQ, o.ofQ, o.topQ, tQ);
+            code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
+            anytie |= tI | tQ;
+            dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+            if (TRACE && ((dmask >> a) & 1) && unit == o.tr->unit) {
+                const int row = row0 + 4 * a + r;
+                const double2 yv = o.y[(size_t)row * U + unit], hh = o.h[(size_t)row * R + rl];
+                o.tr->yperf[(size_t)it * o.tr->LK + row] = c_add(c_sub(yv, x[p6(a)]), c_mul(hh, u[a]));
             }
         }
-        // epilogue on the D layout of acc: 8 rows per lane, one tile at a time
-        // (a lambda per tile with a compile-time tile index: as a loop the
-        // compiler declined to unroll it and indexed ur through scratch)
-        int e0 = 0, e1 = 0;
-        const bool last = it == niter;
-        auto epi_tile = [&](auto tcst) {
-            constexpr int t = decltype(tcst)::value;
-            double2 yv[4], hv[4];
-            int dc[4], dps[4];
+        // a decision exactly on a mid-point (measure zero): the smallest symbol
+        // index among the tied grid points (one uniform branch)
+        if (__ballot(anytie)) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int rr = 16 * t + kq + 4 * r;
-                const int row = row0 + (rr < nrows ? rr : 0) + oz;
-                dc[r] = rdc[rr];
-                yv[r] = o.y[(size_t)row * U + unit];
-                hv[r] = o.h[(size_t)row * R + rl];
+            for (int a = 0; a < 6; ++a) {
+                const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
+                const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
+                dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
+                            min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
             }
-            // every row is computed and the pilot / padding rows masked out
-            // afterwards: with a per-row branch the compiler sinks each row's y
-            // and h loads into it, one serial round trip per load
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                double2 yp = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
-                yp = c_add(yp, c_mul(hv[r], ur[t][r]));
-                // = c_div1(yp, hv[r]), with the hoisted reciprocal when HID
-                const double id = HID ? hid[t][r] : 1.0 / (hv[r].x * hv[r].x + hv[r].y * hv[r].y);
-                const double2 z = make_double2((yp.x * hv[r].x + yp.y * hv[r].y) * id,
-                                               (yp.y * hv[r].x - yp.x * hv[r].y) * id);
-                const int dp = slice_fast(*slt, o.nI, o.nQ,
-                                          o.real_detect ? make_double2(z.x * o.idd, 0.0)
-                                                        : make_double2(z.x * o.idd, z.y * o.idd),
-                                          o.sI, o.sQ);
-                const bool data = dc[r] >= 0;
-                const int ne = data ? __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu))) : 0;
-                e0 += ne;
-                e1 += (dc[r] & 1) ? ne : 0;
-                dps[r] = dp;
-                if (o.tr && data && unit == o.tr->unit) {
-                    o.tr->yperf[(size_t)it * o.tr->LK + row0 + 16 * t + kq + 4 * r] = yp;
-                    o.tr->dec_p[(size_t)it * o.tr->ND + (dc[r] >> 1)] = dp;
-                }
-            }
-            // one uniform branch per tile, after all its rows (a branch per row
-            // splits the rows into separate blocks the scheduler cannot interleave)
-            if (!last) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    double2 av = make_double2(0.0, 0.0);
-                    c_fma(av, rpv[16 * t + kq + 4 * r], sym[dps[r]]);
-                    // component-wise select (a struct-valued ?: became an
-                    // address select through scratch)
-                    const bool data = dc[r] >= 0;
-                    ur[t][r].x = data ? av.x : ur[t][r].x;
-                    ur[t][r].y = data ? av.y : ur[t][r].y;
-                }
-            }
-        };
-        epi_tile(std::integral_constant<int, 0>{});
-        epi_tile(std::integral_constant<int, 1>{});
-        const int s_0 = wave_sum(e0), s_1 = wave_sum(e1);
-        if (l < 2) {
-            const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (l ? (size_t)o.cstride_edge : 0);
-            const int v = l ? s_1 : s_0;
-            if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
         }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const bool data = (dmask >> a) & 1;
+            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
+            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)it * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+            double2 nv = make_double2(0.0, 0.0);
+            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
+            u[a].x = data ? nv.x : u[a].x;
+            u[a].y = data ? nv.y : u[a].y;
+        }
+        cntl[w][it - 1] = wave_sum(ncnt);    // uniform: every lane writes the same word
+        ncnt = 0;
+    }
+    // counters of every iteration: lane 2 (it - 1) + edge of each wave
+    if (l < 2 * niter) {
+        const int it = (l >> 1) + 1, edge = l & 1;
+        const int v = (cntl[w][it - 1] >> (16 * edge)) & 0xffff;
+        const int snr = o.snr0 + (ug * WAVE) / R;
+        const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
+        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
     }
 }
 
@@ -1360,14 +1722,46 @@ static int pic_chain_variant(const ChannelK& ch) {
     return 0;
 }
 
-// Opts::pic_chain: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 (default) =
-// k_pic_mfma where the scheme allows it, else k_pic_chain
-static bool pic_mfma_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch) {
-    return sk.pm_ok && op.pic_chain == 2 && ch.ntap <= 2 && (sk.pm_ksq == 6 || sk.pm_ksq == 7);
+// Opts::pic_chain: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 = k_pic_mfma
+// where the scheme allows it, else k_pic_chain, 3 (default) = k_pic_fft where the
+// scheme allows it, else as 2
+// k_pic_mfma's SH for the channel's taps (-1: no instance)
+static int pic_mfma_shift(const ChannelK& ch) {
+    if (ch.ntap == 1) return 0;
+    if (ch.ntap != 2) return -1;
+    const int maxd = std::max(ch.tap_delay[0], ch.tap_delay[1]);
+    const int sh = (maxd - ch.tap_delay[0]) | ((maxd - ch.tap_delay[1]) << 1);
+    return sh == 1 || sh == 2 ? sh : -1;
 }
 
-bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
-    if (pic_mfma_ok(op, sk, ch)) return true;
+static bool pic_mfma_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
+    // k_pic_mfma's 32-bit offsets: u / h element offsets, buffer byte offsets of
+    // 32 rows of y and of the taps (ensure_buffers pads y, h and the taps)
+    const bool fits = (long long)sk.LK * b.U < (1ll << 31) && (long long)32 * b.U * 16 < (1ll << 32) &&
+                      ((long long)ch.ntap * ch.N + 4) * b.R * 16 < (1ll << 32);
+    return sk.pm_ok && op.pic_chain >= 2 && pic_mfma_shift(ch) >= 0 && (sk.pm_ksq == 6 || sk.pm_ksq == 7) && fits &&
+           niter >= 1 && niter <= PM_MAXIT;
+}
+
+// k_pic_fft's SH for the channel's taps (-1: no instance): delays <= 1
+static int pic_fft_shift(const ChannelK& ch) {
+    if (ch.ntap < 1 || ch.ntap > 2) return -1;
+    int sh = 0;
+    for (int q = 0; q < ch.ntap; ++q) {
+        if (ch.tap_delay[q] > 1) return -1;
+        sh |= ch.tap_delay[q] << q;
+    }
+    return (ch.ntap == 1 && sh == 0) || (ch.ntap == 2 && (sh == 1 || sh == 2)) ? sh : -1;
+}
+
+static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
+    const bool fits = (long long)24 * b.U * 16 < (1ll << 32) && (long long)ch.ntap * ch.N * b.R * 16 < (1ll << 32) &&
+                      (long long)sk.LK * b.U < (1ll << 62);
+    return sk.pf_ok && op.pic_chain == 3 && pic_fft_shift(ch) >= 0 && fits && niter >= 1 && niter <= PM_MAXIT;
+}
+
+bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
+    if (pic_fft_ok(op, sk, ch, b, niter) || pic_mfma_ok(op, sk, ch, b, niter)) return true;
     return sk.pic_ok && pic_chain_variant(ch) && op.pic_chain != 0 && b.R % PCH_UNITS == 0;
 }
 
@@ -1400,21 +1794,54 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
+    // nearest_lin's folded scale / offset
+    o.scI = o.idd * o.sI;
+    o.ofI = 0.5 - sk.lv0I * o.sI;
+    o.topI = sk.nI - 1;
+    o.scQ = sk.real_detect ? 0.0 : o.idd * o.sQ;
+    o.ofQ = 0.5 - sk.lv0Q * o.sQ;
+    o.topQ = sk.nQ - 1;
     TapDelays dl{};
     for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
-    if (pic_mfma_ok(op, sk, ch)) {
+    if (pic_fft_ok(op, sk, ch, b, niter)) {
+        o.pf_scale_re = sk.pf_scale.x;
+        o.pf_scale_im = sk.pf_scale.y;
+        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
+        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+#define LAUNCH_PF(NTV, SHV)                                                                                      \
+    do {                                                                                                         \
+        if (b.tr)                                                                                                \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);      \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);     \
+    } while (0)
+        const int sh = pic_fft_shift(ch);
+        if (ch.ntap == 1) LAUNCH_PF(1, 0);
+        else if (sh == 1) LAUNCH_PF(2, 1);
+        else LAUNCH_PF(2, 2);
+#undef LAUNCH_PF
+        return PATH_PIC_FFT;
+    }
+    if (pic_mfma_ok(op, sk, ch, b, niter)) {
         const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
         const size_t lds = ((size_t)(2 * 6 + 2 * sk.pm_ksq) * 64 + 256) * sizeof(double2) + sizeof(SlicerLds);
         const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-        const int d1 = ch.ntap > 1 ? ch.tap_delay[1] : 0;
-#define LAUNCH_PM(KS, NTV) \
-    hipLaunchKernelGGL((k_pic_mfma<KS, NTV>), grid, blk, lds, s, sk, om, b.ir, ch.N, ch.tap_delay[0], d1, o, niter)
+#define LAUNCH_PM(KS, NTV, SHV)                                                                                   \
+    do {                                                                                                          \
+        if (b.tr)                                                                                                 \
+            hipLaunchKernelGGL((k_pic_mfma<KS, NTV, SHV, true>), grid, blk, lds, s, sk, om, b.ir, ch.N, o, niter); \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_pic_mfma<KS, NTV, SHV, false>), grid, blk, lds, s, sk, om, b.ir, ch.N, o, niter);\
+    } while (0)
+        const int sh = pic_mfma_shift(ch);
         if (sk.pm_ksq == 6) {
-            if (ch.ntap == 2) LAUNCH_PM(6, 2);
-            else LAUNCH_PM(6, 1);
+            if (ch.ntap == 1) LAUNCH_PM(6, 1, 0);
+            else if (sh == 1) LAUNCH_PM(6, 2, 1);
+            else LAUNCH_PM(6, 2, 2);
         } else {
-            if (ch.ntap == 2) LAUNCH_PM(7, 2);
-            else LAUNCH_PM(7, 1);
+            if (ch.ntap == 1) LAUNCH_PM(7, 1, 0);
+            else if (sh == 1) LAUNCH_PM(7, 2, 1);
+            else LAUNCH_PM(7, 2, 2);
         }
 #undef LAUNCH_PM
         return PATH_PIC_MFMA;

@@ -192,6 +192,7 @@ typedef struct {
 #define DSCE_PATH_STAGE_FUSED     (1u << 7)   /* k_ls + k_stage_fused                                      */
 #define DSCE_PATH_STAGE_SPLIT     (1u << 8)   /* k_ls_hest + k_detect + k_precode                          */
 #define DSCE_PATH_NOISE_FUSED     (1u << 9)   /* AWGN drawn inside the Q^H pass                            */
+#define DSCE_PATH_PIC_FFT         (1u << 10)  /* k_pic_fft: perfect-CSI IC chain by FFT (OFDM, VALU)       */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -282,7 +283,7 @@ int dsce_scheme_dims(dsce_ctx* ctx, int32_t scheme_id, dsce_dims* dims);
 int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
 /* Kernel-selection options (defaults = the measured-best path; for A/B runs and
  * tests): xcd, fuse_stage, wpair_3m (-1 auto), wda_3m, pic_chain (0 passes,
- * 1 VALU chain, 2 MFMA chain), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
+ * 1 VALU chain, 2 MFMA chain, 3 FFT chain where the scheme's G / Q allow it), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
  * snr_chunk (0 all), streams (1|2), jakes_rpw (1|2), wtrim (read by
  * dsce_build_mmse), wcontract_valu.  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);

@@ -69,10 +69,10 @@ def test_mmse_estimator_matches_oracle(ofdm):
 
 # ---------------------------------------------------------------------------
 # The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
-# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_mfma for
+# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_fft for
 # the perfect-CSI IC chain, k_stage_fused for the one-tap stage).
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"wpair3_fused", "pic_mfma", "stage_fused", "noise_fused"}
+BENCH_PATH = {"wpair3_fused", "pic_fft", "stage_fused", "noise_fused"}
 
 
 def _check_trace(g, u, name, tol=1e-9):
@@ -96,20 +96,24 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
     """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
     dsce_path_info) and every intermediate of every stage of a unit matches the
     oracle: the fused contraction's y_est and diag(D_hat), k_pilot_pre's LS
-    pilots, k_pic_mfma's y_perf (data rows: the chain forms only those) and
-    both branches' decisions."""
+    pilots, k_pic_fft's y_perf (data rows: the chain forms only those) and
+    both branches' decisions; the same for the matrix-core chain k_pic_mfma
+    (pic_chain 2)."""
     S, eng, mm = ofdm
     rows = S.schemes["ofdm"]["data_pos"]
-    for rep in (5, 70):
-        tr = {}
-        harness.simulate(S, SEED, rep, 1, ["ofdm"], trace=tr)
-        for k in range(len(S.pn_time)):
-            g = eng.trace_unit(0, SEED, rep, k)
-            assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
-            u = tr["units"][k]
-            ns = _check_trace(g, u, "rep %d snr %d" % (rep, k))
-            for st in range(1, ns):
-                np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
+    for chain, path in ((3, BENCH_PATH), (2, BENCH_PATH - {"pic_fft"} | {"pic_mfma"})):
+        eng.set_option("pic_chain", chain)
+        for rep in (5, 70):
+            tr = {}
+            harness.simulate(S, SEED, rep, 1, ["ofdm"], trace=tr)
+            for k in range(len(S.pn_time)):
+                g = eng.trace_unit(0, SEED, rep, k)
+                assert path <= eng.path_info(0), eng.path_info(0)
+                u = tr["units"][k]
+                ns = _check_trace(g, u, "chain %d rep %d snr %d" % (chain, rep, k))
+                for st in range(1, ns):
+                    np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
+    eng.set_option("pic_chain", 3)
 
 
 def test_error_counts_match_oracle(ofdm):
@@ -248,8 +252,9 @@ def test_stage_variants_agree(name):
     XCD-aware work order on/off, SNR-chunked receiver, two streams, 4-MFMA
     instead of 3M complex products, the VALU contraction, the MMSE stage as its
     own kernels instead of fused into the contraction, the perfect-CSI chain as
-    per-iteration passes / VALU chain instead of k_pic_mfma, the fused
-    epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave."""
+    per-iteration passes / VALU chain instead of k_pic_fft, the fused
+    epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave,
+    the matrix-core perfect-CSI chain (k_pic_mfma) instead of the FFT chain."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -261,7 +266,7 @@ def test_stage_variants_agree(name):
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(rb))
     eng.set_option("stage_rb", 8)
     variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2}, {"streams": 2}, {"wpair_3m": 0},
-                {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1},
+                {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
