@@ -149,16 +149,17 @@ def run_cpu_baseline(seconds, workload):
 
 def stored_traffic(kernel_tag, workload):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
-    summary (profiles/*_pmc_wcontract.json, tools/prof_summary.py), used only
-    when it was measured on a build of these exact sources and this workload."""
+    summary (profiles/*_pmc_*.json, tools/prof_summary.py), used only when it
+    was measured on a build of these exact sources, this workload and kernel."""
     src = source_hash()
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_wcontract.json")), key=os.path.getmtime)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json")), key=os.path.getmtime)
     for f in reversed(cands):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("source_hash") == src and d.get("workload", "c2") == workload:
+        if d.get("source_hash") == src and d.get("workload", "c2") == workload and \
+                d.get("kernel", "k_wcontract") == kernel_tag:
             return d.get("hbm_bytes_per_launch"), "profiles/" + os.path.basename(f)
     return None, "no PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
 
@@ -266,9 +267,12 @@ def main():
     total_reps = B * args.steps * world
     value = total_reps / el
 
-    # roofline of the dominant kernel (the MMSE contraction, timed as k_wcontract
-    # with HIP events on the engine's stream)
-    launches, wc_ms = eng.kernel_time("k_wcontract")
+    # roofline of the dominant kernel (the MMSE IC: k_mic_fft where the scheme is
+    # FFT-form OFDM, else the W contraction k_wcontract; HIP events on the
+    # engine's stream)
+    mic_l, mic_ms = eng.kernel_time("k_mic_fft")
+    kname = "k_mic_fft" if mic_l else "k_wcontract"
+    launches, wc_ms = eng.kernel_time(kname)
     flops = 0.0
     executed = 0.0
     paths = []
@@ -280,13 +284,13 @@ def main():
         flops += f
         # matrix-core flops actually executed per counted flop: 3 real MFMAs per
         # complex product in the 3M form, 4 in the 4M form
-        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) else 1.0)
+        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and "mic_fft" not in p else 1.0)
     achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     peak_meas = eng.fp64_mfma_peak()
-    traffic, traffic_src = stored_traffic("k_wcontract", args.config)
+    traffic, traffic_src = stored_traffic(kname, args.config)
     kernels = {}
-    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "perfect_ic", "k_stage"):
+    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_fft", "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
         kernels[k] = {"launches": n, "ms": round(ms, 3)}
     ber = {}
@@ -324,20 +328,25 @@ def main():
         "data": "synthetic (Philox4x32-10 streams, include/dsce.h)",
         "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
                    "parallelism": "dp%d" % world, "options": options},
-        "roofline": {"bound": "mfma",
-                     "kernel": "k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
-                               "diag(D_hat) + detection in its epilogue)",
+        "roofline": {"bound": "valu" if mic_l else "mfma",
+                     "kernel": ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v, H_hat = Bv hP, "
+                                "DFT-24 chain + one-tap + detection (FP64 VALU)") if mic_l else
+                               ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
+                                "diag(D_hat) + detection in its epilogue)"),
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
-                     "peak_measured": peak_meas,
-                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas else None,
-                     "mfma_busy": (exec_tf / peak_meas) if exec_tf and peak_meas else None,
+                     "peak_measured": None if mic_l else peak_meas,
+                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas and not mic_l else None,
+                     "mfma_busy": (exec_tf / peak_meas) if exec_tf and peak_meas and not mic_l else None,
                      "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
                      "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
                      "flops_per_launch": flops / launches if launches else None,
-                     "work_model": "support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
-                                   "fused diag(D_hat)), 8 real flops per CMAC; mfma_busy = executed matrix-core "
-                                   "flops (6 of 8 in the 3M form) / measured peak",
+                     "work_model": ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
+                                    "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
+                                    "at 5 n log2 n flops; peak = FP64 vector spec (= FP64 matrix spec)") if mic_l else
+                                   ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
+                                    "fused diag(D_hat)), 8 real flops per CMAC; mfma_busy = executed matrix-core "
+                                    "flops (6 of 8 in the 3M form) / measured peak"),
                      "paths": paths},
         "cpu_baseline": cpu,
         "setup_s": setup_s,

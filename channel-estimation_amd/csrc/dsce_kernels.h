@@ -22,6 +22,7 @@ struct Opts {
     int jakes_rpw = 2;        // realisations per Jakes wave (1 | 2)
     int wtrim = 1;            // trim W to its non-zero column extent (read by dsce_build_mmse)
     int wcontract_valu = 0;   // 1: VALU contraction instead of the MFMA pair tiles
+    int mmse_ic = 1;          // MMSE IC of OFDM as Q' H_hat G by FFT (k_mic_fft) where eligible; 0: W contraction
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -38,6 +39,7 @@ enum : unsigned {
     PATH_STAGE_SPLIT = 1u << 8,    // k_ls_hest + k_detect + k_precode
     PATH_NOISE_FUSED = 1u << 9,    // noise drawn inside the Q^H pass
     PATH_PIC_FFT = 1u << 10,       // k_pic_fft (perfect-CSI chain by FFT, OFDM)
+    PATH_MIC_FFT = 1u << 11,       // k_pilot_pre + k_mic_fft (MMSE IC as Q' H_hat G by FFT, OFDM)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -100,6 +102,9 @@ struct MmseK {
     const double2* Wpil;  // [var][snr][NP pilots][24 columns][NP]
     const double2* WdA;   // [var][snr][blk][2][NP/4][64] diag(W) rows, MFMA A layout
     const int* pil_c0;    // NP: first column of each pilot row's block
+    // structured MMSE IC (k_mic_fft): H_hat taps = Bv hP; null when not eligible
+    const double2* Bv;    // [var][snr][ntap][N][NP]
+    const double2* Bs;    // [var][snr][QH blk][ntap][NP]: Bv summed over each block's FFT window
 };
 
 // Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
@@ -131,6 +136,12 @@ struct PerfectDetectArgs {
     int scheme, stage, nstage, nsnr, last;
     double sI, sQ;   // 1 / slicer step (I, Q)
 };
+// MMSE IC iteration `stage` of an OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v
+// by FFT with the stage in its epilogue (after k_pilot_pre formed hp_new)
+bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b);
+unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
+                         int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
@@ -162,6 +173,11 @@ void setup_rhp(hipStream_t s, const SetupArgs& a, const double2* m, double2* rhp
 void setup_gp(hipStream_t s, const SetupArgs& a, double2* gp /* N x Nsym */);
 void setup_rest_diag(hipStream_t s, const SetupArgs& a, const double2* gp, const int* q_start, int QL, double* diag);
 void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv);
+// H_hat operator of the structured MMSE IC: bv[sl][q][n][p] = sum_p' m[p'][q][n - d_q]
+// Rinv_sl[p'][p] for the nsl = 2 nsnr inverses; bs[sl][blk][q][p] = its sums over
+// the FFT windows [klo[blk], klo[blk] + win)
+void setup_bv(hipStream_t s, const SetupArgs& a, int nsl, const double2* m, const double2* rinv, double2* bv,
+              int nblk, const int* klo, int win, double2* bs);
 void setup_rdij(hipStream_t s, const SetupArgs& a, const Band& Wb, const double2* m, const int* g_start, int GL,
                 const int* q_start, int QL, double2* rd /* packed, w_elems */);
 struct TxDesc {

@@ -1684,6 +1684,272 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     }
 }
 
+// ---------------------------------------------------------------------------
+// The MMSE IC iteration of OFDM in structured form (k_mic_fft, rows a13-a16).
+// The estimate D_hat = reshape(W hP), W = R_Dij,hP pinv(R) (script:259-313,
+// :493-511), is Q' H_hat G: column p of R_Dij,hP is vec(Q' M_p G) with
+// M_p = reshape(R_vecH x_p) (script:260), so D_hat = Q' (sum_p M_p z_p) G with
+// z = pinv(R) hP, and every M_p lives on the support of the convolution matrix.
+// H_hat is therefore a channel estimate with IR's taps,
+//   hhat[q][n] = sum_p Bv[q][n][p] hP_p,   Bv = m pinv(R)   (k_bv, m of k_mcoef),
+// and y_ic = y - (D_hat - diag D_hat) v (script:482-484) = y - Q'(H_hat (G v)) +
+// diag(D_hat) .* v runs as k_pic_fft's DFT-24 chain with the estimated taps.
+// For OFDM the 1e-8 thresholds of R_Dij and W (script:264-265, :287-289) only
+// drop structural zeros and rounding-level entries (|D_hat - Q' H_hat G| <=
+// 4e-11 at C2; dsce_build_mmse verifies diag(D_hat) against the thresholded
+// W's diagonal and keeps the contraction otherwise).  diag(D_hat)[l] =
+// qs gs sum_q w^(-l d_q) S_q with S_q the sum of hhat[q] over the symbol's FFT
+// window: the previous stage's from its taps, this stage's from Bs (window sums
+// of Bv) and hP_new.  Per unit and symbol: NT x 24 x NP CMACs for the taps
+// instead of the contraction's 24 x 23 x NP.
+// Phase A (lane = unit): wave w forms the taps of window samples 6w..6w+5,
+// Bv rows wave-uniform (scalar loads), hP in registers -> LDS.  Phase B (lane
+// quad = unit): k_pic_fft's DFT-24 chain and epilogue for one iteration, then
+// one-tap with diag(D_hat_new), slicer, counts, decisions written over v.
+// Block = 256 threads = 64 units of one symbol; SNR-fastest XCD-aware order.
+// ---------------------------------------------------------------------------
+struct MicArgs {
+    const double2* __restrict__ bv;       // [var][snr][NT][N][NP]
+    const double2* __restrict__ bs;       // [var][snr][nblk][NT][NP]
+    const double2* __restrict__ hp_prev;  // [NP][U]: the previous stage's LS pilots (its D_hat)
+    const double2* __restrict__ hp_new;   // [NP][U]: this stage's (k_pilot_pre)
+    double2* v;                           // [LK][U]: P [xP; Q(x_est)], in / out
+    double* mse_err;
+    double* mse_pow;
+    int var_prev, var_cur, nsnr, N, nblk, stage, nstage, last, scheme;
+};
+
+template <int NT, int SH, int NP, bool TRACE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int U = o.U, R = o.R;
+    const int snr = o.snr0 + (ug * WAVE) / R;
+    const int ul = w * 16 + (l >> 2);                           // phase-B unit of this lane quad
+    const int unit = ug * WAVE + ul;
+    const int rl = unit % R;
+    const int cq = (r >> 1) + 2 * (r & 1);                     // time quarter of this lane
+    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    __shared__ double2 hh[NT][24][64];                          // estimated taps [q][window sample][unit]
+    __shared__ double2 snw[NT][64];                             // S_q of this stage's estimate
+    __shared__ double2 sym[256];
+    __shared__ int sgrid[256];
+    __shared__ double2 rpv[24];
+    __shared__ int rdc[24];
+    __shared__ double2 wrow[24];                                // qs gs w^(-l): diag(D_hat) weight of a delayed tap
+    __shared__ double2 twa[2][4][6];
+    __shared__ double2 twb[2][4];
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    {
+        // every global load of the prologue before the first LDS write (clamped)
+        const double2 a = o.symbols[min(tid, o.M - 1)];
+        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int rt = min(tid, 23);
+        const double2 pv = o.row_pval[row0 + rt];
+        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        const int e = ((tid / 6) % 4) * (tid % 6);
+        const double2 tw = kW24[e % 12];
+        sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
+        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
+        if (tid < 24) {
+            rpv[tid] = pv;
+            rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+        }
+        if (tid < 48) {
+            const int dir = tid / 24;
+            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+        } else if (tid < 56) {
+            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
+            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
+        } else if (tid >= 64 && tid < 88) {
+            const int lr = tid - 64;
+            const double2 t0 = kW24[lr % 12];
+            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            wrow[lr] = c_mul(scale, make_double2(wl.x, -wl.y));
+        }
+    }
+    // phase-B operands that do not depend on phase A, requested first
+    double2 u[6], yv[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int row = row0 + 4 * a + r;
+        u[a] = ma.v[(size_t)row * U + unit];
+        yv[a] = o.y[(size_t)row * U + unit];
+    }
+    // ---- phase A: the estimated taps of window samples 6w..6w+5 (lane = unit)
+    {
+        const int ua = ug * WAVE + l;
+        double2 hq[NP];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + ua];
+        const double2* __restrict__ b0 =
+            ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo + 6 * w) * NP;
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) {
+                const double2* __restrict__ bq = b0 + ((size_t)q * ma.N + jj) * NP;
+                double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
+#pragma unroll
+                for (int p = 0; p < NP; p += 2) {
+                    c_fma(acc0, bq[p], hq[p]);
+                    c_fma(acc1, bq[p + 1], hq[p + 1]);
+                }
+                hh[q][6 * w + jj][l] = c_add(acc0, acc1);
+            }
+        if (w < NT) {
+            const double2* __restrict__ bsq =
+                ma.bs + (((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT + w) * NP;
+            double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
+#pragma unroll
+            for (int p = 0; p < NP; p += 2) {
+                c_fma(acc0, bsq[p], ma.hp_new[(size_t)p * U + ua]);
+                c_fma(acc1, bsq[p + 1], ma.hp_new[(size_t)(p + 1) * U + ua]);
+            }
+            snw[w][l] = c_add(acc0, acc1);
+        }
+    }
+    __syncthreads();
+    // transmitted symbol indices (8 bits each) and data / no-edge masks
+    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int dc = rdc[4 * a + r];
+        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
+        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
+        dmask |= dc >= 0 ? 1u << a : 0u;
+        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
+    }
+    // the quad's taps (samples 6 cq + m) and the window sums S_q of both stages
+    double2 taps[6][NT];
+    double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        double2 s = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            taps[m][q] = hh[q][6 * cq + m][ul];
+            s = c_add(s, taps[m][q]);
+        }
+        s = c_add(s, dpp_c<QP_XOR1>(s));
+        s = c_add(s, dpp_c<QP_XOR2>(s));
+        const double2 sq = snw[q][ul];
+        if ((SH >> q) & 1) {
+            sp1 = c_add(sp1, s);
+            sn1 = c_add(sn1, sq);
+        } else {
+            sp0 = c_add(sp0, s);
+            sn0 = c_add(sn0, sq);
+        }
+    }
+    sp0 = c_mul(scale, sp0);
+    sn0 = c_mul(scale, sn0);
+    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
+    // ---- phase B: acc = Q' H_hat G u for the symbol (k_pic_fft's chain)
+    double2 x[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) x[a] = u[a];
+    dft6<1>(x);
+    double2 t[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
+        const double2 pv = dpp_c<QP_XOR2>(p);
+        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+        e = c_mulf(e, twb[0][r]);
+        const double2 qv = dpp_c<QP_XOR1>(e);
+        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+    }
+    const double2 tprev = dpp_c<QP_PREV>(t[5]);
+#pragma unroll
+    for (int m = 5; m >= 0; --m) {
+        const double2 tp = m ? t[m - 1] : tprev;
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
+        t[m] = acc;
+    }
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double2 pv = dpp_c<QP_XOR1>(t[m]);
+        double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+        f = c_mulf(f, twb[1][r]);
+        const double2 qv = dpp_c<QP_XOR2>(f);
+        x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+    }
+    dft6<-1>(x);
+    // ---- epilogue per row 4a + r: y_ic = y - acc + diag(D_hat_prev) u, one-tap
+    // with diag(D_hat_new), slicer, counts, re-precoded decision into v
+    int code[6], dp[6];
+    int anytie = 0;
+    double me = 0.0;
+    double2 hn[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int lr = 4 * a + r;
+        const double2 wl = wrow[lr];
+        double2 hpv = sp0, hnv = sn0;
+        c_fma(hpv, wl, sp1);
+        c_fma(hnv, wl, sn1);
+        hn[a] = hnv;
+        double2 ye = c_sub(yv[a], x[p6(a)]);
+        c_fma(ye, hpv, u[a]);
+        const double2 z = c_div1(ye, hnv);
+        int tI, tQ;
+        const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
+        const int iQ = nearest_lin(z.y, o.scQ, o.ofQ, o.topQ, tQ);
+        code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
+        anytie |= tI | tQ;
+        dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+        if (TRACE && unit == o.tr->unit) {
+            const int row = row0 + lr;
+            o.tr->yest[(size_t)ma.stage * o.tr->LK + row] = ye;
+            o.tr->hest[(size_t)ma.stage * o.tr->LK + row] = hnv;
+        }
+    }
+    if (ma.mse_err) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const double2 hv = o.h[(size_t)(row0 + 4 * a + r) * R + rl];
+            const double dx = hn[a].x - hv.x, dy = hn[a].y - hv.y;
+            me += dx * dx + dy * dy;
+        }
+    }
+    if (__ballot(anytie)) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
+            const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
+            dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
+                        min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
+        }
+    }
+    int ncnt = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const bool data = (dmask >> a) & 1;
+        const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
+        ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+        if (TRACE && data && unit == o.tr->unit) o.tr->dec_e[(size_t)ma.stage * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+        if (!ma.last && data) {
+            double2 nv = make_double2(0.0, 0.0);
+            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
+            ma.v[(size_t)(row0 + 4 * a + r) * U + unit] = nv;
+        }
+    }
+    const int tot = wave_sum(ncnt);
+    if (l < 2) {
+        const int v = (tot >> (16 * l)) & 0xffff;
+        const size_t i0 = o.cidx0 + (size_t)ma.stage + (size_t)snr * o.cstride_snr + (l ? (size_t)o.cstride_edge : 0);
+        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+    }
+    if (ma.mse_err) flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage);
+}
+
 template <int NT, class Out>
 static void launch_pass2(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
                          const Out& o, size_t lds) {
@@ -1763,6 +2029,92 @@ static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, co
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
     if (pic_fft_ok(op, sk, ch, b, niter) || pic_mfma_ok(op, sk, ch, b, niter)) return true;
     return sk.pic_ok && pic_chain_variant(ch) && op.pic_chain != 0 && b.R % PCH_UNITS == 0;
+}
+
+// Detection operands of the chain kernels (k_pic_fft / k_pic_mfma / k_pic_chain /
+// k_mic_fft): tables, slicer folded for nearest_lin, counters of branch `csi`
+// (0 MMSE, 1 perfect CSI; the stage is added per iteration).
+static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, const PerfectDetectArgs* pd, int csi) {
+    StorePerfectDetect o{};
+    o.tr = b.tr;
+    o.y = b.y;
+    o.h = b.h;
+    o.u = b.u;
+    o.sidx = b.sidx;
+    o.row_data = sk.row_data;
+    o.row_cons = sk.row_cons;
+    o.row_pval = sk.row_pval;
+    o.symbols = sk.symbols;
+    o.lvI = sk.lvI;
+    o.lvQ = sk.lvQ;
+    o.grid_sym = sk.grid_sym;
+    o.counters = pd->counters;
+    o.cidx0 = ((((size_t)pd->scheme * 2 + csi) * 2 + 0) * pd->nsnr) * pd->nstage;
+    o.cstride_edge = pd->nsnr * pd->nstage;
+    o.cstride_snr = pd->nstage;
+    o.U = b.U;
+    o.R = b.R;
+    o.snr0 = b.snr0;
+    o.M = sk.M;
+    o.nI = sk.nI;
+    o.nQ = sk.nQ;
+    o.real_detect = sk.real_detect;
+    o.idd = 1.0 / sk.data_div;
+    o.sI = pd->sI;
+    o.sQ = pd->sQ;
+    o.scI = o.idd * o.sI;
+    o.ofI = 0.5 - sk.lv0I * o.sI;
+    o.topI = sk.nI - 1;
+    o.scQ = sk.real_detect ? 0.0 : o.idd * o.sQ;
+    o.ofQ = 0.5 - sk.lv0Q * o.sQ;
+    o.topQ = sk.nQ - 1;
+    o.pf_scale_re = sk.pf_scale.x;
+    o.pf_scale_im = sk.pf_scale.y;
+    return o;
+}
+
+bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b) {
+    const bool fits = (long long)ch.ntap * ch.N * 16 < (1ll << 31) && (long long)sk.LK * b.U < (1ll << 62);
+    return op.mmse_ic == 1 && mm.Bv && mm.Bs && mm.Wpil && sk.pf_ok && sk.NP == 16 && pic_fft_shift(ch) >= 0 &&
+           (b.U % 64) == 0 && (b.R % 64) == 0 && fits;
+}
+
+unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
+                         int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd) {
+    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
+    MicArgs ma{};
+    ma.bv = mm.Bv;
+    ma.bs = mm.Bs;
+    ma.hp_prev = hp_prev;
+    ma.hp_new = hp_new;
+    ma.v = b.v;
+    ma.mse_err = b.mse_err;
+    ma.mse_pow = b.mse_pow;
+    ma.var_prev = var_prev;
+    ma.var_cur = var_cur;
+    ma.nsnr = mm.nsnr;
+    ma.N = ch.N;
+    ma.nblk = sk.QH.nblk;
+    ma.stage = stage;
+    ma.nstage = n_iter + 1;
+    ma.last = last ? 1 : 0;
+    ma.scheme = pd->scheme;
+    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
+    const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+#define LAUNCH_MIC(NTV, SHV)                                                                                          \
+    do {                                                                                                              \
+        if (b.tr)                                                                                                     \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o);                      \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o);                     \
+    } while (0)
+    const int sh = pic_fft_shift(ch);
+    if (ch.ntap == 1) LAUNCH_MIC(1, 0);
+    else if (sh == 1) LAUNCH_MIC(2, 1);
+    else LAUNCH_MIC(2, 2);
+#undef LAUNCH_MIC
+    return PATH_MIC_FFT;
 }
 
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,

@@ -235,6 +235,47 @@ void setup_rinv(hipStream_t s, int NP, int nmat, const double2* R, double2* Rinv
     hipLaunchKernelGGL(k_rinv, dim3(nmat), dim3(256), (size_t)NP * 3 * NP * sizeof(double2), s, NP, R, Rinv);
 }
 
+// The channel-estimate operator of the structured MMSE IC (k_mic_fft):
+// D_hat = sum_p W_p hP_p = Q' H_hat G with H_hat = sum_p' M_p' z_p', z = pinv(R) hP
+// (script:260, :283-285), so the estimated tap q at output sample n is
+//   hhat[q][n] = sum_p bv[q][n][p] hP_p,  bv[q][n][p] = sum_p' m[p'][q][n - d_q] Rinv[p'][p]
+// (m: k_mcoef's band of M_p', column n - d_q of the convolution matrix).
+// grid (ceil(N NP / 256), ntap, nsl); Rinv column-major per slice.
+__global__ void k_bv(SetupArgs a, const double2* __restrict__ m, const double2* __restrict__ rinv,
+                     double2* __restrict__ bv) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = blockIdx.y, sl = blockIdx.z;
+    if (e >= a.N * a.NP) return;
+    const int n = e / a.NP, p = e % a.NP, b = n - a.tap_delay[q];
+    const double2* __restrict__ ri = rinv + (size_t)sl * a.NP * a.NP + (size_t)p * a.NP;
+    double2 acc = make_double2(0.0, 0.0);
+    if (b >= 0)
+        for (int pp = 0; pp < a.NP; ++pp) c_fma(acc, m[((size_t)pp * a.ntap + q) * a.N + b], ri[pp]);
+    bv[(((size_t)sl * a.ntap + q) * a.N + n) * a.NP + p] = acc;
+}
+
+// bs[sl][blk][q][p] = sum_{j < win} bv[sl][q][klo[blk] + j][p]; one thread per entry
+__global__ void k_bs(SetupArgs a, int nblk, const int* __restrict__ klo, int win, const double2* __restrict__ bv,
+                     double2* __restrict__ bs) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int sl = blockIdx.y;
+    if (e >= nblk * a.ntap * a.NP) return;
+    const int p = e % a.NP, q = (e / a.NP) % a.ntap, blk = e / (a.NP * a.ntap);
+    const double2* __restrict__ src = bv + (((size_t)sl * a.ntap + q) * a.N) * a.NP + p;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int j = 0; j < win; ++j) {
+        const int n = klo[blk] + j;
+        if (n < a.N) acc = c_add(acc, src[(size_t)n * a.NP]);
+    }
+    bs[(size_t)sl * nblk * a.ntap * a.NP + e] = acc;
+}
+
+void setup_bv(hipStream_t s, const SetupArgs& a, int nsl, const double2* m, const double2* rinv, double2* bv,
+              int nblk, const int* klo, int win, double2* bs) {
+    hipLaunchKernelGGL(k_bv, dim3((a.N * a.NP + 255) / 256, a.ntap, nsl), dim3(256), 0, s, a, m, rinv, bv);
+    hipLaunchKernelGGL(k_bs, dim3((nblk * a.ntap * a.NP + 255) / 256, nsl), dim3(256), 0, s, a, nblk, klo, win, bv, bs);
+}
+
 // R_Dij,hP column i = vec(Q' M_i G) with |.| < thr -> 0 (script:259-268), written
 // straight into the packed band layout of W: off[blk] + ((c-c_lo)*NP + i)*RB + r.
 __global__ void k_rdij(SetupArgs a, Band Wb, const double2* __restrict__ m, const int* __restrict__ g_start, int GL,

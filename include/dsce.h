@@ -193,6 +193,7 @@ typedef struct {
 #define DSCE_PATH_STAGE_SPLIT     (1u << 8)   /* k_ls_hest + k_detect + k_precode                          */
 #define DSCE_PATH_NOISE_FUSED     (1u << 9)   /* AWGN drawn inside the Q^H pass                            */
 #define DSCE_PATH_PIC_FFT         (1u << 10)  /* k_pic_fft: perfect-CSI IC chain by FFT (OFDM, VALU)       */
+#define DSCE_PATH_MIC_FFT         (1u << 11)  /* k_pilot_pre + k_mic_fft: MMSE IC as Q' H_hat G by FFT (OFDM) */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -285,7 +286,11 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  * tests): xcd, fuse_stage, wpair_3m (-1 auto), wda_3m, pic_chain (0 passes,
  * 1 VALU chain, 2 MFMA chain, 3 FFT chain where the scheme's G / Q allow it), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
  * snr_chunk (0 all), streams (1|2), jakes_rpw (1|2), wtrim (read by
- * dsce_build_mmse), wcontract_valu.  Unknown names return DSCE_EINVAL. */
+ * dsce_build_mmse), wcontract_valu, mmse_ic (1: the MMSE IC iterations of an FFT-form
+ * OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}
+ * (k_mic_fft; equal to the W contraction of script:482-511 to rounding, checked
+ * at dsce_build_mmse), 0: the W contraction everywhere).  Unknown names return
+ * DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);
 int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 

@@ -69,10 +69,12 @@ def test_mmse_estimator_matches_oracle(ofdm):
 
 # ---------------------------------------------------------------------------
 # The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
-# k_pilot_pre + fused k_wpair3 epilogue for the MMSE IC stages, k_pic_fft for
-# the perfect-CSI IC chain, k_stage_fused for the one-tap stage).
+# k_pilot_pre + k_mic_fft (Q' H_hat G by FFT) for the MMSE IC stages, k_pic_fft
+# for the perfect-CSI IC chain, k_stage_fused for the one-tap stage); the W
+# contraction (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"wpair3_fused", "pic_fft", "stage_fused", "noise_fused"}
+BENCH_PATH = {"mic_fft", "pic_fft", "stage_fused", "noise_fused"}
+W_PATH = BENCH_PATH - {"mic_fft"} | {"wpair3_fused"}
 
 
 def _check_trace(g, u, name, tol=1e-9):
@@ -95,14 +97,15 @@ def _check_trace(g, u, name, tol=1e-9):
 def test_bench_kernels_trace_matches_oracle(ofdm):
     """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
     dsce_path_info) and every intermediate of every stage of a unit matches the
-    oracle: the fused contraction's y_est and diag(D_hat), k_pilot_pre's LS
-    pilots, k_pic_fft's y_perf (data rows: the chain forms only those) and
-    both branches' decisions; the same for the matrix-core chain k_pic_mfma
-    (pic_chain 2)."""
+    oracle (literal W of script:493-511): k_mic_fft's y_est and diag(D_hat),
+    k_pilot_pre's LS pilots, k_pic_fft's y_perf (data rows: the chain forms
+    only those) and both branches' decisions; the same for the fused W
+    contraction (mmse_ic 0) and the matrix-core chain k_pic_mfma (pic_chain 2)."""
     S, eng, mm = ofdm
     rows = S.schemes["ofdm"]["data_pos"]
-    for chain, path in ((3, BENCH_PATH), (2, BENCH_PATH - {"pic_fft"} | {"pic_mfma"})):
+    for chain, mic, path in ((3, 1, BENCH_PATH), (3, 0, W_PATH), (2, 1, BENCH_PATH - {"pic_fft"} | {"pic_mfma"})):
         eng.set_option("pic_chain", chain)
+        eng.set_option("mmse_ic", mic)
         for rep in (5, 70):
             tr = {}
             harness.simulate(S, SEED, rep, 1, ["ofdm"], trace=tr)
@@ -114,6 +117,7 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
                 for st in range(1, ns):
                     np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
     eng.set_option("pic_chain", 3)
+    eng.set_option("mmse_ic", 1)
 
 
 def test_error_counts_match_oracle(ofdm):
@@ -132,6 +136,11 @@ def test_error_counts_match_oracle(ofdm):
         if first == 0:
             _check_mse(eng, res)
             eng.enable_mse(False)
+    eng.set_option("mmse_ic", 0)        # the W contraction on the same realisations
+    cw = eng.run(SEED, 128, 128)
+    assert W_PATH <= eng.path_info(0), eng.path_info(0)
+    assert np.abs(cw - res["err"]).sum() <= 8 * res["borderline"].sum(), cw - res["err"]
+    eng.set_option("mmse_ic", 1)
     eng.set_batch(256)
     b = eng.bits_per_rep(0)
     assert b[0] == sc["n_data"] * sc["bits_per_symbol"] and b[1] == sc["considered"].sum() * sc["bits_per_symbol"]
@@ -254,7 +263,8 @@ def test_stage_variants_agree(name):
     own kernels instead of fused into the contraction, the perfect-CSI chain as
     per-iteration passes / VALU chain instead of k_pic_fft, the fused
     epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave,
-    the matrix-core perfect-CSI chain (k_pic_mfma) instead of the FFT chain."""
+    the matrix-core perfect-CSI chain (k_pic_mfma) instead of the FFT chain,
+    the W contraction instead of the structured MMSE IC (k_mic_fft)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -267,7 +277,7 @@ def test_stage_variants_agree(name):
     eng.set_option("stage_rb", 8)
     variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2}, {"streams": 2}, {"wpair_3m": 0},
                 {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
-                {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1})
+                {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
