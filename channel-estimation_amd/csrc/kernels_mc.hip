@@ -1702,10 +1702,13 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
 // window: the previous stage's from its taps, this stage's from Bs (window sums
 // of Bv) and hP_new.  Per unit and symbol: NT x 24 x NP CMACs for the taps
 // instead of the contraction's 24 x 23 x NP.
-// Phase A (lane = unit): wave w forms the taps of window samples 6w..6w+5,
-// Bv rows wave-uniform (scalar loads), hP in registers -> LDS.  Phase B (lane
-// quad = unit): k_pic_fft's DFT-24 chain and epilogue for one iteration, then
-// one-tap with diag(D_hat_new), slicer, counts, decisions written over v.
+// Lane quad = unit (k_pic_fft's layout): lane r forms the estimated taps of its
+// six window samples from the symbol's Bv rows (staged in LDS once per block,
+// broadcast to the 16 quads of a wave) and the unit's hP (registers), then
+// one iteration of the DFT-24 chain, one-tap with diag(D_hat_new), slicer,
+// counts, decisions written over v.  (A first version formed the taps lane =
+// unit with Bv through scalar loads and parked them in LDS: 3.8 ms per launch,
+// 65 % of wave time waiting on the serial s_load chain.)
 // Block = 256 threads = 64 units of one symbol; SNR-fastest XCD-aware order.
 // ---------------------------------------------------------------------------
 struct MicArgs {
@@ -1733,8 +1736,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     const int rl = unit % R;
     const int cq = (r >> 1) + 2 * (r & 1);                     // time quarter of this lane
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
-    __shared__ double2 hh[NT][24][64];                          // estimated taps [q][window sample][unit]
-    __shared__ double2 snw[NT][64];                             // S_q of this stage's estimate
+    constexpr int BVS = NP + 1;                                 // padded sample stride: the quad's 4 rows in distinct banks
+    __shared__ double2 sbv[NT][24][BVS];                        // Bv of the symbol's window samples (previous stage's var)
+    __shared__ double2 sbs[NT][NP];                             // Bs of the symbol (this stage's var)
     __shared__ double2 sym[256];
     __shared__ int sgrid[256];
     __shared__ double2 rpv[24];
@@ -1750,6 +1754,17 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         const int rt = min(tid, 23);
         const double2 pv = o.row_pval[row0 + rt];
         const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        // the operator slices: Bv rows klo..klo+23 of every tap (NT x 24 x NP,
+        // contiguous per tap) and Bs of the block
+        constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
+        const double2* __restrict__ bvb = ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo) * NP;
+        double2 bvr[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
+            bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
+        }
+        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
         const int e = ((tid / 6) % 4) * (tid % 6);
         const double2 tw = kW24[e % 12];
         sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
@@ -1758,6 +1773,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             rpv[tid] = pv;
             rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
         }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = tid + 256 * k;
+            if (i < NBV) sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
+        }
+        if (tid < NT * NP) sbs[tid / NP][tid % NP] = bsv;
         if (tid < 48) {
             const int dir = tid / 24;
             const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
@@ -1772,47 +1793,20 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             wrow[lr] = c_mul(scale, make_double2(wl.x, -wl.y));
         }
     }
-    // phase-B operands that do not depend on phase A, requested first
-    double2 u[6], yv[6];
+    // per-unit operands, all requested before the barrier: the rows' v and y,
+    // the previous stage's pilots (all NP, shared by the quad) and a quarter of
+    // this stage's (lane r: pilots 4r..4r+3 of the window sums)
+    double2 u[6], yv[6], hq[NP], hn4[NP / 4];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
         u[a] = ma.v[(size_t)row * U + unit];
         yv[a] = o.y[(size_t)row * U + unit];
     }
-    // ---- phase A: the estimated taps of window samples 6w..6w+5 (lane = unit)
-    {
-        const int ua = ug * WAVE + l;
-        double2 hq[NP];
 #pragma unroll
-        for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + ua];
-        const double2* __restrict__ b0 =
-            ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo + 6 * w) * NP;
+    for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
 #pragma unroll
-        for (int q = 0; q < NT; ++q)
-#pragma unroll
-            for (int jj = 0; jj < 6; ++jj) {
-                const double2* __restrict__ bq = b0 + ((size_t)q * ma.N + jj) * NP;
-                double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
-#pragma unroll
-                for (int p = 0; p < NP; p += 2) {
-                    c_fma(acc0, bq[p], hq[p]);
-                    c_fma(acc1, bq[p + 1], hq[p + 1]);
-                }
-                hh[q][6 * w + jj][l] = c_add(acc0, acc1);
-            }
-        if (w < NT) {
-            const double2* __restrict__ bsq =
-                ma.bs + (((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT + w) * NP;
-            double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
-#pragma unroll
-            for (int p = 0; p < NP; p += 2) {
-                c_fma(acc0, bsq[p], ma.hp_new[(size_t)p * U + ua]);
-                c_fma(acc1, bsq[p + 1], ma.hp_new[(size_t)(p + 1) * U + ua]);
-            }
-            snw[w][l] = c_add(acc0, acc1);
-        }
-    }
+    for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
     // transmitted symbol indices (8 bits each) and data / no-edge masks
     unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
@@ -1824,7 +1818,8 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    // the quad's taps (samples 6 cq + m) and the window sums S_q of both stages
+    // the estimated taps of the lane's samples 6 cq + m (Bv rows from LDS,
+    // broadcast to the 16 quads) and the window sums S_q of both stages
     double2 taps[6][NT];
     double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
 #pragma unroll
@@ -1832,12 +1827,23 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         double2 s = make_double2(0.0, 0.0);
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            taps[m][q] = hh[q][6 * cq + m][ul];
+            const double2* bq = sbv[q][6 * cq + m];
+            double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
+#pragma unroll
+            for (int p = 0; p < NP; p += 2) {
+                c_fma(acc0, bq[p], hq[p]);
+                c_fma(acc1, bq[p + 1], hq[p + 1]);
+            }
+            taps[m][q] = c_add(acc0, acc1);
             s = c_add(s, taps[m][q]);
         }
+        double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
         s = c_add(s, dpp_c<QP_XOR1>(s));
         s = c_add(s, dpp_c<QP_XOR2>(s));
-        const double2 sq = snw[q][ul];
+        sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+        sq = c_add(sq, dpp_c<QP_XOR2>(sq));
         if ((SH >> q) & 1) {
             sp1 = c_add(sp1, s);
             sn1 = c_add(sn1, sq);
