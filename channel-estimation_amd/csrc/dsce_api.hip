@@ -1031,6 +1031,10 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
             const bool mfuse = pfuse && mmse_fused_ok(op, s.k, mm, b);
             // OFDM: the MMSE IC as Q' H_hat G by FFT (k_pilot_pre + k_mic_fft)
             const bool mic = pfuse && mmse_fft_ok(op, s.k, mm, c->ch, b);
+            // both IC chains index-based (k_mic_fft + k_pic_fft): the stage and the
+            // chains pass decisions as symbol indices (qe / qp), not as v / u
+            const bool qidx = mic && chain && !two && s.k.M <= 65536 && op.qidx &&
+                              perfect_chain_fft(op, s.k, c->ch, b, c->niter);
             double2* hp_prev = b.hp;
             double2* hp_cur = b.hp2;
             for (int it = 0; it <= c->niter; ++it) {
@@ -1043,7 +1047,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                     if (chain) {
                         Timed t(c, "perfect_ic", ps);
                         PerfectDetectArgs pd{c->d_counters, (int)si, 1, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
-                        s.path |= launch_perfect_chain(ps, op, s.k, c->ch, b, &pd, c->niter);
+                        s.path |= launch_perfect_chain(ps, op, s.k, c->ch, b, &pd, c->niter, qidx);
                     } else {
                         for (int jt = 1; jt <= c->niter; ++jt) {
                             Timed t(c, "perfect_ic", ps);
@@ -1057,7 +1061,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                 if (it > 0 && mic) {
                     {
                         Timed t(c, "k_pilot_pre");
-                        launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur);
+                        launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur, qidx);
                     }
                     if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, hp_cur, NP, b.U, tunit);
                     {
@@ -1066,7 +1070,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                                              s.k.slI, s.k.slQ};
                         s.path |= launch_mmse_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter),
                                                   var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
-                                                  hp_prev, hp_cur, &pd, op.xcd);
+                                                  hp_prev, hp_cur, &pd, op.xcd, qidx);
                     }
                     std::swap(hp_prev, hp_cur);
                     if (!two && !chain) {
@@ -1116,8 +1120,14 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                 }
                 {
                     Timed t(c, "k_stage");
-                    s.path |= launch_stage(c->stream, op, s.k, mm, it, var_of_stage(it, c->niter), c->niter,
-                                           it == c->niter, b, c->d_counters, (int)si, !(pfuse && it > 0));
+                    if (it == 0 && qidx && op.stage0_fft) {
+                        PerfectDetectArgs pd{c->d_counters, (int)si, 0, c->niter + 1, c->nsnr, c->niter == 0,
+                                             s.k.slI, s.k.slQ};
+                        s.path |= launch_stage0_fft(c->stream, s.k, mm, c->ch, c->niter, c->niter == 0, b, &pd, op.xcd);
+                    } else {
+                        s.path |= launch_stage(c->stream, op, s.k, mm, it, var_of_stage(it, c->niter), c->niter,
+                                               it == c->niter, b, c->d_counters, (int)si, !(pfuse && it > 0), qidx);
+                    }
                 }
                 if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, b.hp, NP, b.U, tunit);
             }
@@ -1785,7 +1795,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

@@ -23,6 +23,8 @@ struct Opts {
     int wtrim = 1;            // trim W to its non-zero column extent (read by dsce_build_mmse)
     int wcontract_valu = 0;   // 1: VALU contraction instead of the MFMA pair tiles
     int mmse_ic = 1;          // MMSE IC of OFDM as Q' H_hat G by FFT (k_mic_fft) where eligible; 0: W contraction
+    int qidx = 1;             // k_mic_fft + k_pic_fft: decisions between stages as symbol indices, not v / u
+    int stage0_fft = 1;       // with qidx: stage 0 as k_stage0_fft (symbol blocks, structured diag(D_hat))
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -114,9 +116,12 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
                uint64_t rep0, McBuffers& b);
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
                          uint64_t seed, uint64_t rep0, McBuffers& b);
+// qidx: a row-local (p_diag) scheme's decisions leave the stage as symbol
+// indices qe / qp ([ND][U]) for the index-based chains (k_pilot_pre / k_mic_fft /
+// k_pic_fft), pilot rows implicit (P xP), instead of the re-precoded v / u
 unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
                       int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
-                      bool perfect);
+                      bool perfect, bool qidx = false);
 // true when launch_stage uses the fused select-mode pass and the precoder is
 // row-local, so the perfect-CSI branch of IC iterations can ride on perfect_ic
 bool perfect_fusable(const Opts& op, const SchemeK& sk);
@@ -126,7 +131,7 @@ unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, cons
 // stage's detection in its epilogue (no y_est, no separate stage kernel).
 bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b);
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
-                      const double2* hp_prev, double2* hp_new);
+                      const double2* hp_prev, double2* hp_new, bool qidx = false);
 unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
                            int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                            double2* hp_new, unsigned long long* counters, int scheme_index);
@@ -139,16 +144,23 @@ struct PerfectDetectArgs {
 // MMSE IC iteration `stage` of an OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v
 // by FFT with the stage in its epilogue (after k_pilot_pre formed hp_new)
 bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b);
+// stage 0 (one-tap + detection of both branches) of such a scheme when both IC
+// chains are index-based: k_ls + k_stage0_fft, decisions into qe / qp
+unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
+                           bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd);
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd);
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
 // registers (pic_ok schemes); perfect_chain_ok tells when it applies.
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
+// true when the chain is k_pic_fft (the only chain with index-based decisions)
+bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
+// qidx: u from the stage's decision indices (StageArgs::qidx; k_pic_fft only)
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter);
+                              const PerfectDetectArgs* pd, int niter, bool qidx = false);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)

@@ -633,6 +633,8 @@ struct StorePerfectDetect {
     // k_pic_mfma's folded slicer (nearest_lin): f = z scale + offset, top = n - 1
     double scI, ofI, topI, scQ, ofQ, topQ;
     double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
+    uint16_t* qd;                      // QIDX chains: the branch's decisions [ND][U] (qe / qp)
+    const double2* xp;                 // pilots [NP][R] (QIDX: P xP rows of v / u)
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
     double2* sym;
@@ -1117,6 +1119,32 @@ __device__ __forceinline__ int nearest_lin(double x, double scale, double offset
     return (int)c;
 }
 
+// Index-based decisions (QIDX chains, StageArgs::qidx): row `row` of
+// v = P [xP; Q(x)] for a row-local precoder is row_pval * (xP[pcol] if pcol < NP,
+// else the decided symbol qd[pcol - NP]).  qidx_issue requests the operands
+// (clamped, unconditional: both candidates), qidx_value combines them once the
+// constellation is in LDS.
+struct QRow {
+    int pc;
+    double2 pv, xv;
+    unsigned q;
+};
+__device__ __forceinline__ QRow qidx_issue(const SchemeK& sk, int row, const uint16_t* __restrict__ qd,
+                                           const double2* __restrict__ xp, int NPV, int U, int R, int unit, int rl) {
+    QRow o;
+    o.pc = sk.row_pcol[row];
+    o.pv = sk.row_pval[row];
+    o.q = qd[(size_t)max(o.pc - NPV, 0) * U + unit];
+    o.xv = xp[(size_t)min(max(o.pc, 0), NPV - 1) * R + rl];
+    return o;
+}
+__device__ __forceinline__ double2 qidx_value(const QRow& q, const double2* sym, int NPV) {
+    const double2 x = q.pc < NPV ? q.xv : sym[q.q];
+    double2 v = make_double2(0.0, 0.0);
+    c_fma(v, q.pv, x);
+    return q.pc < 0 ? make_double2(0.0, 0.0) : v;
+}
+
 // SH: bit q set when tap q reads the shifted sample (maxd - d_q = 1), so the
 // tap-delay selects are compile-time.
 //
@@ -1504,7 +1532,7 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // y, h and the taps: 4.45 / 5.25 ms vs 2.57 ms per 65536-realisation launch).
 // Block = 256 threads = 64 units of one symbol; grid: symbols x units/64,
 // SNR-fastest XCD-aware order.
-template <int NT, int SH, bool TRACE>
+template <int NT, int SH, bool TRACE, bool QIDX>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     int ug, blk;
@@ -1550,10 +1578,12 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     }
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows
     double2 u[6], yh[6], hc[6];
+    QRow qr[QIDX ? 6 : 1];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
-        u[a] = o.u[(size_t)row * U + unit];
+        if (QIDX) qr[a] = qidx_issue(sk, row, o.qd, o.xp, sk.NP, U, R, unit, rl);
+        else u[a] = o.u[(size_t)row * U + unit];
         const double2 yv = o.y[(size_t)row * U + unit];
         const double2 hh = o.h[(size_t)row * R + rl];
         const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
@@ -1561,6 +1591,9 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         yh[a] = c_mulf(yv, hc[a]);                               // y / h
     }
     __syncthreads();
+    if (QIDX)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) u[a] = qidx_value(qr[a], sym, sk.NP);
     // transmitted symbol indices (8 bits each) and data / no-edge masks
     unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
 #pragma unroll
@@ -1722,7 +1755,7 @@ struct MicArgs {
     int var_prev, var_cur, nsnr, N, nblk, stage, nstage, last, scheme;
 };
 
-template <int NT, int SH, int NP, bool TRACE>
+template <int NT, int SH, int NP, bool TRACE, bool QIDX>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     int ug, blk;
@@ -1797,10 +1830,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // the previous stage's pilots (all NP, shared by the quad) and a quarter of
     // this stage's (lane r: pilots 4r..4r+3 of the window sums)
     double2 u[6], yv[6], hq[NP], hn4[NP / 4];
+    QRow qr[QIDX ? 6 : 1];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
-        u[a] = ma.v[(size_t)row * U + unit];
+        if (QIDX) qr[a] = qidx_issue(sk, row, o.qd, o.xp, NP, U, R, unit, rl);
+        else u[a] = ma.v[(size_t)row * U + unit];
         yv[a] = o.y[(size_t)row * U + unit];
     }
 #pragma unroll
@@ -1808,6 +1843,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
     for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
+    if (QIDX)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) u[a] = qidx_value(qr[a], sym, NP);
     // transmitted symbol indices (8 bits each) and data / no-edge masks
     unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
 #pragma unroll
@@ -1942,9 +1980,13 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
         if (TRACE && data && unit == o.tr->unit) o.tr->dec_e[(size_t)ma.stage * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
         if (!ma.last && data) {
-            double2 nv = make_double2(0.0, 0.0);
-            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
-            ma.v[(size_t)(row0 + 4 * a + r) * U + unit] = nv;
+            if (QIDX) {
+                o.qd[(size_t)(rdc[4 * a + r] >> 1) * U + unit] = (uint16_t)dp[a];
+            } else {
+                double2 nv = make_double2(0.0, 0.0);
+                c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
+                ma.v[(size_t)(row0 + 4 * a + r) * U + unit] = nv;
+            }
         }
     }
     const int tot = wave_sum(ncnt);
@@ -1954,6 +1996,140 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
     }
     if (ma.mse_err) flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage);
+}
+
+// ---------------------------------------------------------------------------
+// Stage 0 of an FFT-form OFDM scheme on the index-based chains (k_stage0_fft):
+// one-tap + detection of both branches (script:428-466) for 64 units x one
+// symbol in k_mic_fft's layout.  diag(D_hat_0) = qs gs sum_q w^(-l d_q) S_q with
+// S_q = Bs hP_0 (the structured diagonal, equal to Wd hP_0 to rounding, checked
+// by build_mic), so the stage reads y, h and a quarter of hP per lane and
+// writes the decision indices qe / qp (pilot rows stay implicit).  MSE sums
+// |h_hat - h|^2 and |h|^2 at stage 0 when enabled.
+// ---------------------------------------------------------------------------
+template <int NT, int SH, int NP, bool TRACE>
+__global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o,
+                                                    uint16_t* __restrict__ qp, unsigned long long* __restrict__ counters) {
+    int ug, blk;
+    band_block(ord, sk.QH.nblk, ug, blk);
+    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int U = o.U, R = o.R;
+    const int snr = o.snr0 + (ug * WAVE) / R;
+    const int unit = ug * WAVE + w * 16 + (l >> 2);
+    const int rl = unit % R;
+    const int row0 = sk.QH.row0[blk];
+    __shared__ double2 sbs[NT][NP];
+    __shared__ int sgrid[256];
+    __shared__ int rdc[24];
+    __shared__ double2 wrow[24];
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    {
+        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int rt = min(tid, 23);
+        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
+        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
+        if (tid < 24) rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+        if (tid < NT * NP) sbs[tid / NP][tid % NP] = bsv;
+        if (tid >= 64 && tid < 88) {
+            const int lr = tid - 64;
+            const double2 t0 = kW24[lr % 12];
+            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            wrow[lr] = c_mul(scale, make_double2(wl.x, -wl.y));
+        }
+    }
+    double2 yv[6], hv[6], hn4[NP / 4];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int row = row0 + 4 * a + r;
+        yv[a] = o.y[(size_t)row * U + unit];
+        hv[a] = o.h[(size_t)row * R + rl];
+    }
+#pragma unroll
+    for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
+    __syncthreads();
+    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int dc = rdc[4 * a + r];
+        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
+        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
+        dmask |= dc >= 0 ? 1u << a : 0u;
+        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
+    }
+    double2 sn0 = make_double2(0.0, 0.0), sn1 = sn0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
+        sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+        sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+        if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
+        else sn0 = c_add(sn0, sq);
+    }
+    sn0 = c_mul(scale, sn0);
+    // both branches: code = iI | iQ << 8 | tie flags << 16 (MMSE), << 18 (perfect)
+    int ce[6], cp[6], de[6], dq[6];
+    int anytie = 0;
+    double me = 0.0, mp = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int lr = 4 * a + r;
+        double2 hd = sn0;
+        c_fma(hd, wrow[lr], sn1);
+        const double2 ze = c_div1(yv[a], hd), zp = c_div1(yv[a], hv[a]);
+        int t0, t1, t2, t3;
+        const int iI = nearest_lin(ze.x, o.scI, o.ofI, o.topI, t0), iQ = nearest_lin(ze.y, o.scQ, o.ofQ, o.topQ, t1);
+        const int jI = nearest_lin(zp.x, o.scI, o.ofI, o.topI, t2), jQ = nearest_lin(zp.y, o.scQ, o.ofQ, o.topQ, t3);
+        ce[a] = iI | (iQ << 8) | (t0 << 16) | (t1 << 17);
+        cp[a] = jI | (jQ << 8) | (t2 << 16) | (t3 << 17);
+        anytie |= t0 | t1 | t2 | t3;
+        de[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+        dq[a] = sgrid[__umul24(jI, o.nQ) + jQ];
+        if (ma.mse_err) {
+            const double dx = hd.x - hv[a].x, dy = hd.y - hv[a].y;
+            me += dx * dx + dy * dy;
+            mp += hv[a].x * hv[a].x + hv[a].y * hv[a].y;
+        }
+        if (TRACE && unit == o.tr->unit) o.tr->hest[row0 + lr] = hd;
+    }
+    if (__ballot(anytie)) {
+        auto tie = [&](int code) {
+            const int iI = code & 0xff, iQ = (code >> 8) & 0xff;
+            const int jI = max(iI - ((code >> 16) & 1), 0), jQ = max(iQ - ((code >> 17) & 1), 0);
+            return min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
+                       min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
+        };
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            de[a] = tie(ce[a]);
+            dq[a] = tie(cp[a]);
+        }
+    }
+    int cnt[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const bool data = (dmask >> a) & 1, ne = (emask >> a) & 1;
+        const int tx = (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu);
+        const int ee = data ? __popc((unsigned)(de[a] ^ tx)) : 0, ep = data ? __popc((unsigned)(dq[a] ^ tx)) : 0;
+        cnt[0] += ee;
+        cnt[1] += ne ? ee : 0;
+        cnt[2] += ep;
+        cnt[3] += ne ? ep : 0;
+        const int d = rdc[4 * a + r] >> 1;
+        if (TRACE && data && unit == o.tr->unit) {
+            o.tr->dec_e[d] = de[a];
+            o.tr->dec_p[d] = dq[a];
+        }
+        if (!ma.last && data) {
+            o.qd[(size_t)d * U + unit] = (uint16_t)de[a];
+            qp[(size_t)d * U + unit] = (uint16_t)dq[a];
+        }
+    }
+    flush_counts(cnt, counters, (((size_t)ma.scheme * 4) * ma.nsnr + snr) * ma.nstage, (size_t)ma.nsnr * ma.nstage, 2);
+    if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0);
 }
 
 template <int NT, class Out>
@@ -2032,6 +2208,10 @@ static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, co
     return sk.pf_ok && op.pic_chain == 3 && pic_fft_shift(ch) >= 0 && fits && niter >= 1 && niter <= PM_MAXIT;
 }
 
+bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
+    return pic_fft_ok(op, sk, ch, b, niter);
+}
+
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
     if (pic_fft_ok(op, sk, ch, b, niter) || pic_mfma_ok(op, sk, ch, b, niter)) return true;
     return sk.pic_ok && pic_chain_variant(ch) && op.pic_chain != 0 && b.R % PCH_UNITS == 0;
@@ -2068,6 +2248,8 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
+    o.qd = csi ? b.qp : b.qe;
+    o.xp = b.xp;
     o.scI = o.idd * o.sI;
     o.ofI = 0.5 - sk.lv0I * o.sI;
     o.topI = sk.nI - 1;
@@ -2087,7 +2269,7 @@ bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Chann
 
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd) {
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     MicArgs ma{};
     ma.bv = mm.Bv;
@@ -2110,10 +2292,14 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
 #define LAUNCH_MIC(NTV, SHV)                                                                                          \
     do {                                                                                                              \
-        if (b.tr)                                                                                                     \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o);                      \
+        if (b.tr && qidx)                                                                                             \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, om, ma, o);                \
+        else if (b.tr)                                                                                                \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false>), grid, blk, 0, s, sk, om, ma, o);               \
+        else if (qidx)                                                                                                \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, om, ma, o);               \
         else                                                                                                          \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o);                     \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false>), grid, blk, 0, s, sk, om, ma, o);              \
     } while (0)
     const int sh = pic_fft_shift(ch);
     if (ch.ntap == 1) LAUNCH_MIC(1, 0);
@@ -2124,41 +2310,9 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
 }
 
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter) {
-    StorePerfectDetect o{};
-    o.tr = b.tr;
-    o.y = b.y;
-    o.h = b.h;
-    o.u = b.u;
-    o.sidx = b.sidx;
-    o.row_data = sk.row_data;
-    o.row_cons = sk.row_cons;
-    o.row_pval = sk.row_pval;
-    o.symbols = sk.symbols;
-    o.lvI = sk.lvI;
-    o.lvQ = sk.lvQ;
-    o.grid_sym = sk.grid_sym;
-    o.counters = pd->counters;
-    o.cidx0 = ((((size_t)pd->scheme * 2 + 1) * 2 + 0) * pd->nsnr) * pd->nstage;   // stage added per iteration
-    o.cstride_edge = pd->nsnr * pd->nstage;
-    o.cstride_snr = pd->nstage;
-    o.U = b.U;
-    o.R = b.R;
-    o.snr0 = b.snr0;
-    o.M = sk.M;
-    o.nI = sk.nI;
-    o.nQ = sk.nQ;
-    o.real_detect = sk.real_detect;
-    o.idd = 1.0 / sk.data_div;
-    o.sI = pd->sI;
-    o.sQ = pd->sQ;
-    // nearest_lin's folded scale / offset
-    o.scI = o.idd * o.sI;
-    o.ofI = 0.5 - sk.lv0I * o.sI;
-    o.topI = sk.nI - 1;
-    o.scQ = sk.real_detect ? 0.0 : o.idd * o.sQ;
-    o.ofQ = 0.5 - sk.lv0Q * o.sQ;
-    o.topQ = sk.nQ - 1;
+                              const PerfectDetectArgs* pd, int niter, bool qidx) {
+    StorePerfectDetect o = chain_detect(sk, b, pd, 1);
+    qidx = qidx && pic_fft_ok(op, sk, ch, b, niter);
     TapDelays dl{};
     for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
     if (pic_fft_ok(op, sk, ch, b, niter)) {
@@ -2168,10 +2322,15 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
         const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
 #define LAUNCH_PF(NTV, SHV)                                                                                      \
     do {                                                                                                         \
-        if (b.tr)                                                                                                \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);      \
+        if (b.tr && qidx)                                                                                        \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+        else if (b.tr)                                                                                           \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);\
+        else if (qidx)                                                                                           \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);\
         else                                                                                                     \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);     \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o,      \
+                               niter);                                                                           \
     } while (0)
         const int sh = pic_fft_shift(ch);
         if (ch.ntap == 1) LAUNCH_PF(1, 0);
@@ -2710,15 +2869,38 @@ __global__ void __launch_bounds__(256)
 // before any row can be detected.  Lane = unit; the pilot rows of W stream
 // with wave-uniform (scalar) loads.  NP x 24 x (NP + 1) CMACs per unit, 5 % of
 // the contraction.
-template <int NP>
+template <int NP, bool QIDX>
 __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __restrict__ Wpil,
                                                   const int* __restrict__ pil_c0, int var_prev, int nsnr, int snr0,
                                                   int R, int U, const double2* __restrict__ hp_prev,
-                                                  const double2* __restrict__ v, const double2* __restrict__ y,
+                                                  const double2* __restrict__ v, const uint16_t* __restrict__ qd,
+                                                  const double2* __restrict__ y,
                                                   const double2* __restrict__ xp, double2* __restrict__ hp_new) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int rl = unit % R;
     const int snr = snr0 + (blockIdx.x * WAVE) / R;
+    __shared__ double2 sym[QIDX ? 256 : 1];
+    if (QIDX) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + 64 * k;
+            const double2 a = sk.symbols[min(i, sk.M - 1)];
+            sym[i] = make_double2(i < sk.M ? a.x : 0.0, i < sk.M ? a.y : 0.0);
+        }
+        __syncthreads();
+    }
+    // column c of v = P [xP; Q(x_est)]: the stored vector, or (QIDX) rebuilt
+    // from the decision indices; c is wave-uniform, so the row tables are
+    // scalar loads and the pilot / data branch is uniform
+    auto vcol = [&](int c) -> double2 {
+        if (!QIDX) return v[(size_t)c * U + unit];
+        const int pc = sk.row_pcol[c];
+        if (pc < 0) return make_double2(0.0, 0.0);
+        const double2 x = pc < NP ? xp[(size_t)pc * R + rl] : sym[qd[(size_t)(pc - NP) * U + unit]];
+        double2 r = make_double2(0.0, 0.0);
+        c_fma(r, sk.row_pval[c], x);
+        return r;
+    };
     double2 hq[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) hq[p] = hp_prev[(size_t)p * U + unit];
@@ -2731,8 +2913,8 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
         // two columns per step
         double2 acc = make_double2(0.0, 0.0);
         for (int cc = 0; cc < 24; cc += 2) {
-            const double2 va = v[(size_t)(c0 + cc) * U + unit];
-            const double2 vb = v[(size_t)(c0 + cc + 1) * U + unit];
+            const double2 va = vcol(c0 + cc);
+            const double2 vb = vcol(c0 + cc + 1);
             double2 d[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) d[k] = make_double2(0.0, 0.0);
@@ -2761,9 +2943,13 @@ bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McB
 }
 
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
-                      const double2* hp_prev, double2* hp_new) {
-    hipLaunchKernelGGL(k_pilot_pre<16>, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev, mm.nsnr,
-                       b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.xp, hp_new);
+                      const double2* hp_prev, double2* hp_new, bool qidx) {
+    if (qidx)
+        hipLaunchKernelGGL((k_pilot_pre<16, true>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev,
+                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qe, b.y, b.xp, hp_new);
+    else
+        hipLaunchKernelGGL((k_pilot_pre<16, false>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0,
+                           var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qe, b.y, b.xp, hp_new);
 }
 
 unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
@@ -2868,6 +3054,7 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
 
 struct StageArgs {
     int stage, var, nsnr, nstage, scheme, last, perfect, R, U, snr0, xcd_order;
+    int qidx;                  // p_diag schemes: decisions as symbol indices (qe / qp) instead of v / u
     const TraceK* tr;          // null unless tracing (dsce_trace_unit_ex)
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
@@ -3161,7 +3348,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                     if (PERF) st.tr->dec_p[(size_t)st.stage * st.tr->ND + i] = dp;
                 }
                 if (!st.last) {
-                    if (sk.p_diag) {
+                    if (sk.p_diag && !st.qidx) {
                         const double2 pv = rpval[r];
                         double2 av = make_double2(0.0, 0.0), au = av;
                         if (rpcol[r] >= 0) {
@@ -3175,7 +3362,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                         qp[(size_t)i * U + unit] = (uint16_t)dp;
                     }
                 }
-            } else if (!st.last && sk.p_diag && st.stage == 0) {   // pilot / empty row: constant P xP
+            } else if (!st.last && sk.p_diag && st.stage == 0 && !st.qidx) {   // pilot / empty row: constant P xP
                 const int kc = rpcol[r];
                 double2 av = make_double2(0.0, 0.0);
                 if (kc >= 0) c_fma(av, rpval[r], xp[(size_t)kc * R + rl]);
@@ -3226,9 +3413,10 @@ bool perfect_fusable(const Opts& op, const SchemeK& sk) { return stage_fused_ok(
 
 unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
                       int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
-                      bool perfect) {
+                      bool perfect, bool qidx) {
     StageArgs st;
     st.perfect = perfect ? 1 : 0;
+    st.qidx = qidx && sk.p_diag && stage_fused_ok(op, sk) ? 1 : 0;
     st.stage = stage;
     st.var = var;
     st.nsnr = mm.nsnr;
@@ -3264,6 +3452,47 @@ unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const Mm
     if (!last)
         hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v, b.u);
     return PATH_STAGE_SPLIT;
+}
+
+// Stage 0 of the index-based OFDM chains (k_ls + k_stage0_fft)
+unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
+                           bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd) {
+    // LS pilot estimates of stage 0 into b.hp (k_ls), then the symbol-block stage
+    StageArgs st{};
+    st.R = b.R;
+    st.U = b.U;
+    st.ysrc_e = b.y;
+    hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);
+    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
+    MicArgs ma{};
+    ma.bs = mm.Bs;
+    ma.hp_new = b.hp;
+    ma.mse_err = b.mse_err;
+    ma.mse_pow = b.mse_pow;
+    ma.var_cur = 0;
+    ma.nsnr = mm.nsnr;
+    ma.N = ch.N;
+    ma.nblk = sk.QH.nblk;
+    ma.stage = 0;
+    ma.nstage = n_iter + 1;
+    ma.last = last ? 1 : 0;
+    ma.scheme = pd->scheme;
+    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
+    const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+#define LAUNCH_S0(NTV, SHV)                                                                                           \
+    do {                                                                                                              \
+        if (b.tr)                                                                                                     \
+            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o, b.qp, pd->counters); \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o, b.qp,            \
+                               pd->counters);                                                                         \
+    } while (0)
+    const int sh = pic_fft_shift(ch);
+    if (ch.ntap == 1) LAUNCH_S0(1, 0);
+    else if (sh == 1) LAUNCH_S0(2, 1);
+    else LAUNCH_S0(2, 2);
+#undef LAUNCH_S0
+    return PATH_STAGE_FUSED;
 }
 
 // MMSE one-tap channel h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p for n LS
