@@ -1070,7 +1070,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                                              s.k.slI, s.k.slQ};
                         s.path |= launch_mmse_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter),
                                                   var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
-                                                  hp_prev, hp_cur, &pd, op.xcd, qidx);
+                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0);
                     }
                     std::swap(hp_prev, hp_cur);
                     if (!two && !chain) {
@@ -1795,7 +1795,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

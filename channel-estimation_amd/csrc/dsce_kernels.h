@@ -25,6 +25,7 @@ struct Opts {
     int mmse_ic = 1;          // MMSE IC of OFDM as Q' H_hat G by FFT (k_mic_fft) where eligible; 0: W contraction
     int qidx = 1;             // k_mic_fft + k_pic_fft: decisions between stages as symbol indices, not v / u
     int stage0_fft = 1;       // with qidx: stage 0 as k_stage0_fft (symbol blocks, structured diag(D_hat))
+    int mic_mfma = 1;         // k_mic_fft's estimated taps as an MFMA GEMM (3M) instead of VALU dot products
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -150,7 +151,8 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
                            bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd);
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false);
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,
+                         bool tapm = true);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in

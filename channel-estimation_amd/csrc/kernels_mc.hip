@@ -1755,7 +1755,7 @@ struct MicArgs {
     int var_prev, var_cur, nsnr, N, nblk, stage, nstage, last, scheme;
 };
 
-template <int NT, int SH, int NP, bool TRACE, bool QIDX>
+template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     int ug, blk;
@@ -1829,8 +1829,22 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // per-unit operands, all requested before the barrier: the rows' v and y,
     // the previous stage's pilots (all NP, shared by the quad) and a quarter of
     // this stage's (lane r: pilots 4r..4r+3 of the window sums)
-    double2 u[6], yv[6], hq[NP], hn4[NP / 4];
+    double2 u[6], yv[6], hq[TAPM ? 1 : NP], hn4[NP / 4];
     QRow qr[QIDX ? 6 : 1];
+    // TAPM: the taps as an MFMA GEMM, A = Bv rows (tap row R = q 24 + j, 16 per
+    // tile), B = hP_prev (k = pilot, column = the wave's 16 units), 3M complex
+    // products; lane (g = l >> 4, jc = l & 15) holds B[4 ks + g][unit jc]
+    constexpr int NTILE = (NT * 24 + 15) / 16, NKS = NP / 4;
+    double br[TAPM ? NKS : 1], bi[TAPM ? NKS : 1], bsm[TAPM ? NKS : 1];
+    if (TAPM) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const double2 hv = ma.hp_prev[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
+            br[ks] = hv.x;
+            bi[ks] = hv.y;
+            bsm[ks] = hv.x + hv.y;
+        }
+    }
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
@@ -1838,8 +1852,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         else u[a] = ma.v[(size_t)row * U + unit];
         yv[a] = o.y[(size_t)row * U + unit];
     }
+    if (!TAPM)
 #pragma unroll
-    for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
+        for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
 #pragma unroll
     for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
@@ -1856,8 +1871,34 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    // the estimated taps of the lane's samples 6 cq + m (Bv rows from LDS,
-    // broadcast to the 16 quads) and the window sums S_q of both stages
+    // the estimated taps of the lane's samples 6 cq + m and the window sums S_q
+    // of both stages.  TAPM: the MFMA GEMM's D tiles (row 16 t + g + 4 reg, unit
+    // jc) go through the wave's own LDS slab into the quad layout; otherwise
+    // each lane forms its 12 taps on the VALU (Bv rows broadcast from LDS)
+    __shared__ double2 hhs[TAPM ? 4 : 1][TAPM ? NTILE * 16 : 1][17];
+    if (TAPM) {
+        const int g = l >> 4, jc = l & 15;
+        const int R = jc;                                   // A row of this lane within a tile
+#pragma unroll
+        for (int t = 0; t < NTILE; ++t) {
+            const int Rt = 16 * t + R;
+            const bool okr = Rt < NT * 24;
+            const int q = okr ? Rt / 24 : 0, jj = okr ? Rt % 24 : 0;
+            d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                const double2 a = sbv[q][jj][4 * ks + g];
+                const double ar = okr ? a.x : 0.0, ai = okr ? a.y : 0.0;
+                p1 = MFMA64(ar, br[ks], p1);
+                p2 = MFMA64(ai, bi[ks], p2);
+                p3 = MFMA64(ar + ai, bsm[ks], p3);
+            }
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg)
+                hhs[w][16 * t + g + 4 * reg][jc] = make_double2(p1[reg] - p2[reg], p3[reg] - p1[reg] - p2[reg]);
+        }
+        __syncthreads();
+    }
     double2 taps[6][NT];
     double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
 #pragma unroll
@@ -1865,14 +1906,18 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         double2 s = make_double2(0.0, 0.0);
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            const double2* bq = sbv[q][6 * cq + m];
-            double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
+            if (TAPM) {
+                taps[m][q] = hhs[w][q * 24 + 6 * cq + m][l >> 2];
+            } else {
+                const double2* bq = sbv[q][6 * cq + m];
+                double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
 #pragma unroll
-            for (int p = 0; p < NP; p += 2) {
-                c_fma(acc0, bq[p], hq[p]);
-                c_fma(acc1, bq[p + 1], hq[p + 1]);
+                for (int p = 0; p < NP; p += 2) {
+                    c_fma(acc0, bq[p], hq[p]);
+                    c_fma(acc1, bq[p + 1], hq[p + 1]);
+                }
+                taps[m][q] = c_add(acc0, acc1);
             }
-            taps[m][q] = c_add(acc0, acc1);
             s = c_add(s, taps[m][q]);
         }
         double2 sq = make_double2(0.0, 0.0);
@@ -2269,7 +2314,7 @@ bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Chann
 
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx) {
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx, bool tapm) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     MicArgs ma{};
     ma.bv = mm.Bv;
@@ -2290,22 +2335,28 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     ma.scheme = pd->scheme;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_MIC(NTV, SHV)                                                                                          \
+#define LAUNCH_MIC3(NTV, SHV, TM)                                                                                     \
     do {                                                                                                              \
         if (b.tr && qidx)                                                                                             \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, om, ma, o);                \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true, TM>), grid, blk, 0, s, sk, om, ma, o);            \
         else if (b.tr)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false>), grid, blk, 0, s, sk, om, ma, o);               \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false, TM>), grid, blk, 0, s, sk, om, ma, o);           \
         else if (qidx)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, om, ma, o);               \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, TM>), grid, blk, 0, s, sk, om, ma, o);           \
         else                                                                                                          \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false>), grid, blk, 0, s, sk, om, ma, o);              \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, TM>), grid, blk, 0, s, sk, om, ma, o);          \
+    } while (0)
+#define LAUNCH_MIC(NTV, SHV)                                                                                          \
+    do {                                                                                                              \
+        if (tapm) LAUNCH_MIC3(NTV, SHV, true);                                                                        \
+        else LAUNCH_MIC3(NTV, SHV, false);                                                                            \
     } while (0)
     const int sh = pic_fft_shift(ch);
     if (ch.ntap == 1) LAUNCH_MIC(1, 0);
     else if (sh == 1) LAUNCH_MIC(2, 1);
     else LAUNCH_MIC(2, 2);
 #undef LAUNCH_MIC
+#undef LAUNCH_MIC3
     return PATH_MIC_FFT;
 }
 
