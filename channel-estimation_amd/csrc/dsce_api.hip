@@ -105,6 +105,8 @@ struct Scheme {
     int* pil_c0 = nullptr;
     double2* Bv = nullptr;          // structured MMSE IC operator (k_mic_fft; null: not eligible)
     double2* Bs = nullptr;
+    int* pblk = nullptr;            // QH blocks with pilot rows (k_pilot_fft)
+    int npb = 0;
     long long wp_elems = 0, wp_exec = 0;
     long long w_diag = 0;           // (r, r) pairs inside the band (stored as zeros: diag(D_hat) comes from Wd)
     unsigned path = 0;              // PATH_* bits of the last dsce_run / trace (dsce_path_info)
@@ -755,7 +757,16 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
         free_alloc(c, s.Bv);
         free_alloc(c, s.Bs);
         s.Bv = s.Bs = nullptr;
+        return;
     }
+    std::vector<int> pb;
+    for (int b = 0; b < nblk; ++b) {
+        bool has = false;
+        for (int p : s.pilot_pos) has |= p >= s.qband.row0[b] && p < s.qband.row0[b] + s.qband.nrows[b];
+        if (has) pb.push_back(b);
+    }
+    s.npb = (int)pb.size();
+    if (s.npb) s.pblk = dupload(c, pb);
 }
 
 // ---------------------------------------------------------------------------
@@ -779,7 +790,10 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         if (s.pil_c0) free_alloc(c, s.pil_c0);
         if (s.Bv) free_alloc(c, s.Bv);
         if (s.Bs) free_alloc(c, s.Bs);
+        if (s.pblk) free_alloc(c, s.pblk);
         s.Bv = s.Bs = nullptr;
+        s.pblk = nullptr;
+        s.npb = 0;
         s.W = s.Wd = s.Wp = nullptr;
         s.Wp3 = nullptr;
         s.Wpil = s.WdA = nullptr;
@@ -994,6 +1008,8 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
         mm.pil_c0 = s.pil_c0;
         mm.Bv = s.Bv;
         mm.Bs = s.Bs;
+        mm.pblk = s.pblk;
+        mm.npb = s.npb;
         {
             Timed t(c, "tx");
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
@@ -1061,7 +1077,12 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                 if (it > 0 && mic) {
                     {
                         Timed t(c, "k_pilot_pre");
-                        launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur, qidx);
+                        if (op.pilot_fft && mm.npb > 0)
+                            launch_pilot_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter), b, hp_prev,
+                                             hp_cur, op.xcd, qidx);
+                        else
+                            launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur,
+                                             qidx);
                     }
                     if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, hp_cur, NP, b.U, tunit);
                     {
@@ -1795,7 +1816,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

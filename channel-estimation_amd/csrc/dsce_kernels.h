@@ -26,6 +26,7 @@ struct Opts {
     int qidx = 1;             // k_mic_fft + k_pic_fft: decisions between stages as symbol indices, not v / u
     int stage0_fft = 1;       // with qidx: stage 0 as k_stage0_fft (symbol blocks, structured diag(D_hat))
     int mic_mfma = 1;         // k_mic_fft's estimated taps as an MFMA GEMM (3M) instead of VALU dot products
+    int pilot_fft = 1;        // structured pilot pre-pass (k_mic_fft PILOT mode) instead of k_pilot_pre's W rows
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -108,6 +109,8 @@ struct MmseK {
     // structured MMSE IC (k_mic_fft): H_hat taps = Bv hP; null when not eligible
     const double2* Bv;    // [var][snr][ntap][N][NP]
     const double2* Bs;    // [var][snr][QH blk][ntap][NP]: Bv summed over each block's FFT window
+    const int* pblk;      // QH blocks holding pilot rows (k_pilot_fft)
+    int npb;
 };
 
 // Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
@@ -145,6 +148,9 @@ struct PerfectDetectArgs {
 // MMSE IC iteration `stage` of an OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v
 // by FFT with the stage in its epilogue (after k_pilot_pre formed hp_new)
 bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b);
+// the pilot pre-pass of that path: y_ic of the stage at the pilot rows -> hp_new
+void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
+                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx);
 // stage 0 (one-tap + detection of both branches) of such a scheme when both IC
 // chains are index-based: k_ls + k_stage0_fft, decisions into qe / qp
 unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,

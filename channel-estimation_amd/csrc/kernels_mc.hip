@@ -1753,13 +1753,19 @@ struct MicArgs {
     double* mse_err;
     double* mse_pow;
     int var_prev, var_cur, nsnr, N, nblk, stage, nstage, last, scheme;
+    // PILOT mode (k_pilot_fft): the symbol blocks holding pilots, and this
+    // stage's LS pilot estimates y_ic(pilots) ./ xP / sqrt(kappa) out
+    const int* pblk;
+    int npb;
+    double2* hp_out;
 };
 
-template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM>
+template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM, bool PILOT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
+    band_block(ord, PILOT ? ma.npb : sk.QH.nblk, ug, blk);
+    if (PILOT) blk = ma.pblk[blk];
     const int tid = threadIdx.x, l = tid & 63, r = l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int U = o.U, R = o.R;
@@ -1855,8 +1861,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     if (!TAPM)
 #pragma unroll
         for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
+    if (!PILOT)
 #pragma unroll
-    for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
+        for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
     if (QIDX)
 #pragma unroll
@@ -1921,8 +1928,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             s = c_add(s, taps[m][q]);
         }
         double2 sq = make_double2(0.0, 0.0);
+        if (!PILOT)
 #pragma unroll
-        for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
+            for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
         s = c_add(s, dpp_c<QP_XOR1>(s));
         s = c_add(s, dpp_c<QP_XOR2>(s));
         sq = c_add(sq, dpp_c<QP_XOR1>(sq));
@@ -1971,6 +1979,24 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
     }
     dft6<-1>(x);
+    if constexpr (PILOT) {
+        // the next stage's LS pilot estimates (script:487-489) at the block's pilot rows
+        const double sqk = 1.0 / sk.inv_sqrt_kappa;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            const int pc = QIDX ? qr[a].pc : sk.row_pcol[row];
+            if (pc >= 0 && pc < NP) {
+                double2 ye = c_sub(yv[a], x[p6(a)]);
+                double2 hpv = sp0;
+                c_fma(hpv, wrow[4 * a + r], sp1);
+                c_fma(ye, hpv, u[a]);
+                const double2 q = c_div(ye, QIDX ? qr[a].xv : o.xp[(size_t)pc * R + rl]);
+                ma.hp_out[(size_t)pc * U + unit] = make_double2(q.x / sqk, q.y / sqk);
+            }
+        }
+        return;
+    }
     // ---- epilogue per row 4a + r: y_ic = y - acc + diag(D_hat_prev) u, one-tap
     // with diag(D_hat_new), slicer, counts, re-precoded decision into v
     int code[6], dp[6];
@@ -2338,13 +2364,13 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
 #define LAUNCH_MIC3(NTV, SHV, TM)                                                                                     \
     do {                                                                                                              \
         if (b.tr && qidx)                                                                                             \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true, TM>), grid, blk, 0, s, sk, om, ma, o);            \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true, TM, false>), grid, blk, 0, s, sk, om, ma, o);     \
         else if (b.tr)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false, TM>), grid, blk, 0, s, sk, om, ma, o);           \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false, TM, false>), grid, blk, 0, s, sk, om, ma, o);    \
         else if (qidx)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, TM>), grid, blk, 0, s, sk, om, ma, o);           \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, TM, false>), grid, blk, 0, s, sk, om, ma, o);    \
         else                                                                                                          \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, TM>), grid, blk, 0, s, sk, om, ma, o);          \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, TM, false>), grid, blk, 0, s, sk, om, ma, o);   \
     } while (0)
 #define LAUNCH_MIC(NTV, SHV)                                                                                          \
     do {                                                                                                              \
@@ -2358,6 +2384,41 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
 #undef LAUNCH_MIC
 #undef LAUNCH_MIC3
     return PATH_MIC_FFT;
+}
+
+// The pilot pre-pass of the structured MMSE IC (k_mic_fft in PILOT mode): y_ic of
+// IC iteration `stage` at the pilot rows only (script:482-489) -> hp_new, over
+// the symbol blocks that hold pilots (4 of 14 at C2); MFMA taps, no detection.
+void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
+                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx) {
+    PerfectDetectArgs pd{};
+    StorePerfectDetect o = chain_detect(sk, b, &pd, 0);
+    MicArgs ma{};
+    ma.bv = mm.Bv;
+    ma.bs = mm.Bs;
+    ma.hp_prev = hp_prev;
+    ma.hp_out = hp_new;
+    ma.v = b.v;
+    ma.var_prev = var_prev;
+    ma.nsnr = mm.nsnr;
+    ma.N = ch.N;
+    ma.nblk = sk.QH.nblk;
+    ma.pblk = mm.pblk;
+    ma.npb = mm.npb;
+    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
+    const dim3 grid((b.U / WAVE) * mm.npb), blk(256);
+#define LAUNCH_PIL(NTV, SHV)                                                                                          \
+    do {                                                                                                              \
+        if (qidx)                                                                                                     \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, true, true>), grid, blk, 0, s, sk, om, ma, o);   \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, true, true>), grid, blk, 0, s, sk, om, ma, o);  \
+    } while (0)
+    const int sh = pic_fft_shift(ch);
+    if (ch.ntap == 1) LAUNCH_PIL(1, 0);
+    else if (sh == 1) LAUNCH_PIL(2, 1);
+    else LAUNCH_PIL(2, 2);
+#undef LAUNCH_PIL
 }
 
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
