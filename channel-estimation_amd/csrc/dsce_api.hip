@@ -957,6 +957,10 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.e2 = dalloc<double2>(c, LK * U, L);
     b.qe = dalloc<uint16_t>(c, ND * U, L);
     b.qp = dalloc<uint16_t>(c, ND * U, L);
+    b.sidr = dalloc<uint16_t>(c, (LK + 32) * R, L);
+    b.qre = dalloc<uint16_t>(c, LK * U, L);
+    b.qrp = dalloc<uint16_t>(c, LK * U, L);
+    DSCE_HIP_CHECK(hipMemsetAsync(b.sidr, 0, (LK + 32) * R * sizeof(uint16_t), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.y + LK * U, 0, 32 * U * sizeof(double2), c->stream));

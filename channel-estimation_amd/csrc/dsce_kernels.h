@@ -87,6 +87,9 @@ struct McBuffers {
     double2* e2;      // [LK][U]   y_perf ./ h     (one-tap quotient, perfect CSI)
     uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
+    uint16_t* sidr;   // [LK][R]   transmitted symbol index per data row (row-indexed sidx)
+    uint16_t* qre;    // [LK][U]   QIDX chains: MMSE decisions per data row
+    uint16_t* qrp;    // [LK][U]   QIDX chains: perfect-CSI decisions per data row
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
     const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)

@@ -633,8 +633,10 @@ struct StorePerfectDetect {
     // k_pic_mfma's folded slicer (nearest_lin): f = z scale + offset, top = n - 1
     double scI, ofI, topI, scQ, ofQ, topQ;
     double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
-    uint16_t* qd;                      // QIDX chains: the branch's decisions [ND][U] (qe / qp)
-    const double2* xp;                 // pilots [NP][R] (QIDX: P xP rows of v / u)
+    uint16_t* qd;                      // QIDX chains: the branch's decisions, row-indexed [LK][U] (qre / qrp)
+    const double2* xp;                 // pilots [NP][R] (k_mic_fft PILOT mode: the LS division)
+    const double2* xs;                 // precoded symbols P [xP; xD] [LK][R] (QIDX: the pilot rows of v / u)
+    const uint16_t* sidr;              // transmitted symbol index per data row [LK][R]
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
     double2* sym;
@@ -773,7 +775,8 @@ struct StorePerfectDetect {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_tx_symbols(SchemeK sk, int bits_slot, int pilot_slot, uint64_t seed,
                                                    uint64_t rep0, int R, double2* __restrict__ xp,
-                                                   uint16_t* __restrict__ sidx, double2* __restrict__ xs) {
+                                                   uint16_t* __restrict__ sidx, double2* __restrict__ xs,
+                                                   uint16_t* __restrict__ sidr) {
     __shared__ double2 sym[256];
     for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
     __syncthreads();
@@ -792,7 +795,9 @@ __global__ void __launch_bounds__(64) k_tx_symbols(SchemeK sk, int bits_slot, in
         const uint4 w = stream_block(seed, rep, STREAM_BITS, bits_slot, q >> 7);
         const uint32_t wi = (q >> 5) & 3;
         const uint32_t word = wi == 0 ? w.x : wi == 1 ? w.y : wi == 2 ? w.z : w.w;
-        sidx[(size_t)i * R + rl] = (uint16_t)((word >> (q & 31)) & mmask);   // bi2de, LSB first
+        const uint16_t si = (uint16_t)((word >> (q & 31)) & mmask);   // bi2de, LSB first
+        sidx[(size_t)i * R + rl] = si;
+        sidr[(size_t)sk.data_pos[i] * R + rl] = si;                    // the same, row-indexed
     }
     // x = P [xP; xD]
     for (int r = 0; r < sk.LK; ++r) {
@@ -825,7 +830,7 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
                uint64_t rep0, McBuffers& b) {
     const int R = b.R;
     hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
-                       b.xp, b.sidx, b.xs);
+                       b.xp, b.sidx, b.xs, b.sidr);
     // s = G x (script:376-378)
     launch_band(s, sk.G, R, nullptr, LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
     hipLaunchKernelGGL(k_channel_apply, dim3(R / WAVE, (ch.N + 63) / 64), dim3(WAVE), 0, s, ch, R, b.ir, b.ss, b.r0);
@@ -1119,30 +1124,43 @@ __device__ __forceinline__ int nearest_lin(double x, double scale, double offset
     return (int)c;
 }
 
-// Index-based decisions (QIDX chains, StageArgs::qidx): row `row` of
-// v = P [xP; Q(x)] for a row-local precoder is row_pval * (xP[pcol] if pcol < NP,
-// else the decided symbol qd[pcol - NP]).  qidx_issue requests the operands
-// (clamped, unconditional: both candidates), qidx_value combines them once the
-// constellation is in LDS.
-struct QRow {
-    int pc;
-    double2 pv, xv;
-    unsigned q;
-};
-__device__ __forceinline__ QRow qidx_issue(const SchemeK& sk, int row, const uint16_t* __restrict__ qd,
-                                           const double2* __restrict__ xp, int NPV, int U, int R, int unit, int rl) {
-    QRow o;
-    o.pc = sk.row_pcol[row];
-    o.pv = sk.row_pval[row];
-    o.q = qd[(size_t)max(o.pc - NPV, 0) * U + unit];
-    o.xv = xp[(size_t)min(max(o.pc, 0), NPV - 1) * R + rl];
-    return o;
+// Index-based decisions (QIDX chains, StageArgs::qidx): the decisions live
+// row-indexed, qd[row][U] = symbol index of a data row, so a chain reads them
+// with no table lookup in front (row r of v = P [xP; Q(x)] is row_pval[r] *
+// symbols[qd[r]] for a data row of a row-local precoder); pilot rows are the
+// realisation's constant precoded pilots xs[row][R].  Transmitted indices come
+// row-indexed too (sidr, written by k_tx_symbols).
+__device__ __forceinline__ double2 qidx_value(bool data, unsigned q, double2 pv, const double2* sym,
+                                              const double2* __restrict__ xs, size_t xs_i) {
+    if (data) {
+        double2 v = make_double2(0.0, 0.0);
+        c_fma(v, pv, sym[q]);
+        return v;
+    }
+    return xs[xs_i];
 }
-__device__ __forceinline__ double2 qidx_value(const QRow& q, const double2* sym, int NPV) {
-    const double2 x = q.pc < NPV ? q.xv : sym[q.q];
-    double2 v = make_double2(0.0, 0.0);
-    c_fma(v, q.pv, x);
-    return q.pc < 0 ? make_double2(0.0, 0.0) : v;
+
+// Error counts of a 256-thread block, one atomic per counter per block: every
+// wave packs its totals (errors | no-edge errors << 16, per CSI branch) and
+// wave 0 sums the four waves' words from LDS.  `words` = 1 or 2 branches.
+__device__ __forceinline__ void block_counts(const int (&packed)[2], int words, int* lds /* [4][2] */,
+                                             unsigned long long* counters, size_t base, size_t stride_edge,
+                                             size_t stride_csi) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int t0 = wave_sum(packed[0]);
+    const int t1 = words > 1 ? wave_sum(packed[1]) : 0;
+    if (l == 0) {
+        lds[2 * w] = t0;
+        lds[2 * w + 1] = t1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * words) {
+        const int csi = threadIdx.x >> 1, edge = threadIdx.x & 1;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += (lds[2 * k + csi] >> (16 * edge)) & 0xffff;
+        if (v) atomicAdd(&counters[base + csi * stride_csi + edge * stride_edge], (unsigned long long)v);
+    }
 }
 
 // SH: bit q set when tap q reads the shifted sample (maxd - d_q = 1), so the
@@ -1578,12 +1596,13 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     }
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows
     double2 u[6], yh[6], hc[6];
-    QRow qr[QIDX ? 6 : 1];
+    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
-        if (QIDX) qr[a] = qidx_issue(sk, row, o.qd, o.xp, sk.NP, U, R, unit, rl);
+        if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
         else u[a] = o.u[(size_t)row * U + unit];
+        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
         const double2 yv = o.y[(size_t)row * U + unit];
         const double2 hh = o.h[(size_t)row * R + rl];
         const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
@@ -1591,19 +1610,19 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         yh[a] = c_mulf(yv, hc[a]);                               // y / h
     }
     __syncthreads();
-    if (QIDX)
-#pragma unroll
-        for (int a = 0; a < 6; ++a) u[a] = qidx_value(qr[a], sym, sk.NP);
-    // transmitted symbol indices (8 bits each) and data / no-edge masks
-    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+    // data / no-edge masks of the lane's rows
+    unsigned dmask = 0u, emask = 0u;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int dc = rdc[4 * a + r];
-        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
-        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
+    if (QIDX)
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+            u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
+                              (size_t)(row0 + 4 * a + r) * R + rl);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const __amdgpu_buffer_rsrc_t trs =
         buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo)) * R * sizeof(double2));
@@ -1707,10 +1726,14 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         cntl[w][it - 1] = wave_sum(ncnt);    // uniform: every lane writes the same word
         ncnt = 0;
     }
-    // counters of every iteration: lane 2 (it - 1) + edge of each wave
-    if (l < 2 * niter) {
-        const int it = (l >> 1) + 1, edge = l & 1;
-        const int v = (cntl[w][it - 1] >> (16 * edge)) & 0xffff;
+    // counters of every iteration, summed over the block's 4 waves: thread
+    // 2 (it - 1) + edge issues the block's one atomic per counter
+    __syncthreads();
+    if (tid < 2 * niter) {
+        const int it = (tid >> 1) + 1, edge = tid & 1;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += (cntl[k][it - 1] >> (16 * edge)) & 0xffff;
         const int snr = o.snr0 + (ug * WAVE) / R;
         const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
         if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
@@ -1836,7 +1859,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // the previous stage's pilots (all NP, shared by the quad) and a quarter of
     // this stage's (lane r: pilots 4r..4r+3 of the window sums)
     double2 u[6], yv[6], hq[TAPM ? 1 : NP], hn4[NP / 4];
-    QRow qr[QIDX ? 6 : 1];
+    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
     // TAPM: the taps as an MFMA GEMM, A = Bv rows (tap row R = q 24 + j, 16 per
     // tile), B = hP_prev (k = pilot, column = the wave's 16 units), 3M complex
     // products; lane (g = l >> 4, jc = l & 15) holds B[4 ks + g][unit jc]
@@ -1854,8 +1877,9 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
-        if (QIDX) qr[a] = qidx_issue(sk, row, o.qd, o.xp, NP, U, R, unit, rl);
+        if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
         else u[a] = ma.v[(size_t)row * U + unit];
+        if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
         yv[a] = o.y[(size_t)row * U + unit];
     }
     if (!TAPM)
@@ -1865,19 +1889,19 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
         for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
-    if (QIDX)
-#pragma unroll
-        for (int a = 0; a < 6; ++a) u[a] = qidx_value(qr[a], sym, NP);
-    // transmitted symbol indices (8 bits each) and data / no-edge masks
-    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+    // data / no-edge masks of the lane's rows
+    unsigned dmask = 0u, emask = 0u;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int dc = rdc[4 * a + r];
-        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
-        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
+    if (QIDX)
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+            u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
+                              (size_t)(row0 + 4 * a + r) * R + rl);
     // the estimated taps of the lane's samples 6 cq + m and the window sums S_q
     // of both stages.  TAPM: the MFMA GEMM's D tiles (row 16 t + g + 4 reg, unit
     // jc) go through the wave's own LDS slab into the quad layout; otherwise
@@ -1985,13 +2009,13 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const int row = row0 + 4 * a + r;
-            const int pc = QIDX ? qr[a].pc : sk.row_pcol[row];
+            const int pc = sk.row_pcol[row];
             if (pc >= 0 && pc < NP) {
                 double2 ye = c_sub(yv[a], x[p6(a)]);
                 double2 hpv = sp0;
                 c_fma(hpv, wrow[4 * a + r], sp1);
                 c_fma(ye, hpv, u[a]);
-                const double2 q = c_div(ye, QIDX ? qr[a].xv : o.xp[(size_t)pc * R + rl]);
+                const double2 q = c_div(ye, o.xp[(size_t)pc * R + rl]);
                 ma.hp_out[(size_t)pc * U + unit] = make_double2(q.x / sqk, q.y / sqk);
             }
         }
@@ -2052,7 +2076,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         if (TRACE && data && unit == o.tr->unit) o.tr->dec_e[(size_t)ma.stage * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
         if (!ma.last && data) {
             if (QIDX) {
-                o.qd[(size_t)(rdc[4 * a + r] >> 1) * U + unit] = (uint16_t)dp[a];
+                o.qd[(size_t)(row0 + 4 * a + r) * U + unit] = (uint16_t)dp[a];
             } else {
                 double2 nv = make_double2(0.0, 0.0);
                 c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
@@ -2060,11 +2084,11 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             }
         }
     }
-    const int tot = wave_sum(ncnt);
-    if (l < 2) {
-        const int v = (tot >> (16 * l)) & 0xffff;
-        const size_t i0 = o.cidx0 + (size_t)ma.stage + (size_t)snr * o.cstride_snr + (l ? (size_t)o.cstride_edge : 0);
-        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+    {
+        __shared__ int bcnt[8];
+        const int pk[2] = {ncnt, 0};
+        block_counts(pk, 1, bcnt, o.counters, o.cidx0 + (size_t)ma.stage + (size_t)snr * o.cstride_snr,
+                     (size_t)o.cstride_edge, 0);
     }
     if (ma.mse_err) flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage);
 }
@@ -2111,21 +2135,21 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
         }
     }
     double2 yv[6], hv[6], hn4[NP / 4];
+    unsigned txp[2] = {0u, 0u};
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
         yv[a] = o.y[(size_t)row * U + unit];
         hv[a] = o.h[(size_t)row * R + rl];
+        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
     }
 #pragma unroll
     for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
-    unsigned txp[2] = {0u, 0u}, dmask = 0u, emask = 0u;
+    unsigned dmask = 0u, emask = 0u;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int dc = rdc[4 * a + r];
-        const unsigned tv = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
-        txp[a >> 2] |= (tv & 0xffu) << (8 * (a & 3));
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
@@ -2195,11 +2219,17 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
             o.tr->dec_p[d] = dq[a];
         }
         if (!ma.last && data) {
-            o.qd[(size_t)d * U + unit] = (uint16_t)de[a];
-            qp[(size_t)d * U + unit] = (uint16_t)dq[a];
+            const size_t qi = (size_t)(row0 + 4 * a + r) * U + unit;
+            o.qd[qi] = (uint16_t)de[a];
+            qp[qi] = (uint16_t)dq[a];
         }
     }
-    flush_counts(cnt, counters, (((size_t)ma.scheme * 4) * ma.nsnr + snr) * ma.nstage, (size_t)ma.nsnr * ma.nstage, 2);
+    {
+        __shared__ int bcnt[8];
+        const int pk[2] = {cnt[0] | (cnt[1] << 16), cnt[2] | (cnt[3] << 16)};
+        block_counts(pk, 2, bcnt, counters, (((size_t)ma.scheme * 4) * ma.nsnr + snr) * ma.nstage,
+                     (size_t)ma.nsnr * ma.nstage, 2 * (size_t)ma.nsnr * ma.nstage);
+    }
     if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0);
 }
 
@@ -2319,8 +2349,10 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
-    o.qd = csi ? b.qp : b.qe;
+    o.qd = csi ? b.qrp : b.qre;
     o.xp = b.xp;
+    o.xs = b.xs;
+    o.sidr = b.sidr;
     o.scI = o.idd * o.sI;
     o.ofI = 0.5 - sk.lv0I * o.sI;
     o.topI = sk.nI - 1;
@@ -2986,7 +3018,7 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
                                                   const int* __restrict__ pil_c0, int var_prev, int nsnr, int snr0,
                                                   int R, int U, const double2* __restrict__ hp_prev,
                                                   const double2* __restrict__ v, const uint16_t* __restrict__ qd,
-                                                  const double2* __restrict__ y,
+                                                  const double2* __restrict__ xs, const double2* __restrict__ y,
                                                   const double2* __restrict__ xp, double2* __restrict__ hp_new) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int rl = unit % R;
@@ -3007,10 +3039,9 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
     auto vcol = [&](int c) -> double2 {
         if (!QIDX) return v[(size_t)c * U + unit];
         const int pc = sk.row_pcol[c];
-        if (pc < 0) return make_double2(0.0, 0.0);
-        const double2 x = pc < NP ? xp[(size_t)pc * R + rl] : sym[qd[(size_t)(pc - NP) * U + unit]];
+        if (pc < NP) return xs[(size_t)c * R + rl];          // pilot (or empty) row: P xP
         double2 r = make_double2(0.0, 0.0);
-        c_fma(r, sk.row_pval[c], x);
+        c_fma(r, sk.row_pval[c], sym[qd[(size_t)c * U + unit]]);
         return r;
     };
     double2 hq[NP];
@@ -3058,10 +3089,10 @@ void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var
                       const double2* hp_prev, double2* hp_new, bool qidx) {
     if (qidx)
         hipLaunchKernelGGL((k_pilot_pre<16, true>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev,
-                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qe, b.y, b.xp, hp_new);
+                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qre, b.xs, b.y, b.xp, hp_new);
     else
         hipLaunchKernelGGL((k_pilot_pre<16, false>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0,
-                           var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qe, b.y, b.xp, hp_new);
+                           var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qre, b.xs, b.y, b.xp, hp_new);
 }
 
 unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
@@ -3470,8 +3501,10 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                         v[ix] = av;
                         if (PERF) u[ix] = au;
                     } else {
-                        qe[(size_t)i * U + unit] = (uint16_t)de;
-                        qp[(size_t)i * U + unit] = (uint16_t)dp;
+                        // qidx: row-indexed decisions for the index-based chains
+                        const size_t qi = (size_t)(st.qidx ? row : i) * U + unit;
+                        qe[qi] = (uint16_t)de;
+                        qp[qi] = (uint16_t)dp;
                     }
                 }
             } else if (!st.last && sk.p_diag && st.stage == 0 && !st.qidx) {   // pilot / empty row: constant P xP
@@ -3491,23 +3524,25 @@ template <int NPT>
 static void launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
                                   unsigned long long* counters, int rb) {
     const int ug = b.U / 64;
+    uint16_t* qe_ = st.qidx ? b.qre : b.qe;            // qidx: row-indexed decisions
+    uint16_t* qp_ = st.qidx ? b.qrp : b.qp;
 #define LAUNCH_SF(RBV)                                                                                          \
     {                                                                                                           \
         const int nrb = (sk.LK + 4 * (RBV) - 1) / (4 * (RBV));                                                  \
         if (st.mse_err) {                                                                                       \
             if (st.perfect)                                                                                     \
                 hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, true>), dim3(ug * nrb), dim3(256), 0, s, sk, st, \
-                                   nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters); \
+                                   nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, qe_, qp_, b.v, b.u, counters); \
             else                                                                                                \
                 hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, true>), dim3(ug * nrb), dim3(256), 0, s, sk,  \
-                                   st, nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u,       \
+                                   st, nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, qe_, qp_, b.v, b.u,       \
                                    counters);                                                                   \
         } else if (st.perfect)                                                                                  \
             hipLaunchKernelGGL((k_stage_fused<NPT, RBV, true, false>), dim3(ug * nrb), dim3(256), 0, s, sk, st,   \
-                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
+                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, qe_, qp_, b.v, b.u, counters);     \
         else                                                                                                    \
             hipLaunchKernelGGL((k_stage_fused<NPT, RBV, false, false>), dim3(ug * nrb), dim3(256), 0, s, sk, st,  \
-                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, b.qe, b.qp, b.v, b.u, counters);     \
+                               nrb, mm.Wd, b.xp, b.sidx, b.h, b.hp, b.hest, qe_, qp_, b.v, b.u, counters);     \
         return;                                                                                                 \
     }
     if (rb == 4) LAUNCH_SF(4)
@@ -3594,9 +3629,9 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
 #define LAUNCH_S0(NTV, SHV)                                                                                           \
     do {                                                                                                              \
         if (b.tr)                                                                                                     \
-            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o, b.qp, pd->counters); \
+            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o, b.qrp, pd->counters); \
         else                                                                                                          \
-            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o, b.qp,            \
+            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o, b.qrp,           \
                                pd->counters);                                                                         \
     } while (0)
     const int sh = pic_fft_shift(ch);
