@@ -143,6 +143,8 @@ struct dsce_ctx {
     std::vector<std::unique_ptr<Scheme>> schemes;
     int batch = 8192;
     Opts op{};                            // kernel selection (dsce_set_option)
+    JakesChunks jk{};                     // samples of the IR a batch needs (update_jakes_chunks)
+    size_t jk_nsch = (size_t)-1;          // scheme count jk was computed for
     McBuffers buf{};
     size_t buf_key[6] = {0, 0, 0, 0, 0, 0};
     std::vector<void*> buf_allocs;
@@ -938,6 +940,8 @@ void ensure_buffers(dsce_ctx* c, int R) {
     // k_pic_mfma reads whole 32-row tiles of y and h and up to 3 samples past N
     // of the taps through block-based buffer views: pad those allocations (zeroed)
     b.ir = dalloc<double2>(c, (size_t)c->ch.ntap * N * R + 4 * (size_t)R, L);
+    // samples k_jakes skips (JakesChunks) stay zero
+    DSCE_HIP_CHECK(hipMemsetAsync(b.ir, 0, ((size_t)c->ch.ntap * N * R + 4 * (size_t)R) * sizeof(double2), c->stream));
     b.xp = dalloc<double2>(c, NP * R, L);
     b.sidx = dalloc<uint16_t>(c, ND * R, L);
     b.r0 = dalloc<double2>(c, N * R, L);
@@ -966,6 +970,37 @@ void ensure_buffers(dsce_ctx* c, int R) {
     DSCE_HIP_CHECK(hipMemsetAsync(b.y + LK * U, 0, 32 * U * sizeof(double2), c->stream));
 }
 
+// JakesChunks of the context: the union of every scheme's Q^H sample ranges,
+// in chunks of JakesChunks::LEN aligned to each range; kept only if it skips at
+// least 10 % of the samples (FBMC's overlapping Q^H blocks cover them all).
+void update_jakes_chunks(dsce_ctx* c) {
+    if (c->jk.n0) free_alloc(c, const_cast<int*>(c->jk.n0));
+    c->jk = JakesChunks{};
+    c->jk_nsch = c->schemes.size();
+    const int N = c->ch.N;
+    if (N <= 0 || c->schemes.empty()) return;
+    std::vector<char> need(N, 0);
+    for (auto& sp : c->schemes)
+        for (size_t b = 0; b < sp->qband.row0.size(); ++b)
+            for (int n = sp->qband.klo[b]; n < sp->qband.khi[b] && n < N; ++n) need[n] = 1;
+    std::vector<int> n0;
+    int covered = 0;
+    for (int n = 0; n < N;) {
+        if (!need[n]) {
+            ++n;
+            continue;
+        }
+        int e = n;
+        while (e < N && need[e]) ++e;
+        for (int a = n; a < e; a += JakesChunks::LEN) n0.push_back(a);
+        covered += ((e - n + JakesChunks::LEN - 1) / JakesChunks::LEN) * JakesChunks::LEN;
+        n = e;
+    }
+    if (n0.empty() || covered > 0.9 * N) return;
+    c->jk.n0 = dupload(c, n0);
+    c->jk.n = (int)n0.size();
+}
+
 // One traced unit (dsce_trace_unit_ex): realisation lane `lane` of the batch at
 // SNR index `snr` of scheme `scheme`.  Quantities that sit in a per-unit buffer
 // anyway (y, h, hP, and y_est / y_perf of the unfused paths) are copied from
@@ -991,7 +1026,8 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
     b.tr = nullptr;
     {
         Timed t(c, "k_jakes");
-        launch_jakes(c->stream, op, c->ch, seed, rep0, R, b.ir);
+        if (c->jk_nsch != c->schemes.size()) update_jakes_chunks(c);
+        launch_jakes(c->stream, op, c->ch, seed, rep0, R, b.ir, &c->jk);
     }
     const int chunk = snr_chunk(c);
     for (size_t si = 0; si < c->schemes.size(); ++si) {
@@ -1820,7 +1856,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

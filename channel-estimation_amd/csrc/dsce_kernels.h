@@ -27,6 +27,7 @@ struct Opts {
     int stage0_fft = 1;       // with qidx: stage 0 as k_stage0_fft (symbol blocks, structured diag(D_hat))
     int mic_mfma = 1;         // k_mic_fft's estimated taps as an MFMA GEMM (3M) instead of VALU dot products
     int pilot_fft = 1;        // structured pilot pre-pass (k_mic_fft PILOT mode) instead of k_pilot_pre's W rows
+    int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -117,8 +118,17 @@ struct MmseK {
 };
 
 // Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
+// Chunks of the impulse response a batch needs: every sample some Q^H row of
+// some scheme reads (the channel taps are used at output samples only there:
+// r0 = H s, diag(D) and the perfect-CSI passes / chains all go through Q^H).
+struct JakesChunks {
+    static constexpr int LEN = 12;   // samples per chunk
+    const int* n0 = nullptr;         // device: first sample of each chunk
+    int n = 0;
+};
+// jc: form only those chunks (samples outside stay as they are: zero)
 void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
-                  double2* ir);
+                  double2* ir, const JakesChunks* jc = nullptr);
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
                uint64_t rep0, McBuffers& b);
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,

@@ -205,7 +205,7 @@ static constexpr int JCH_MAX = 16;
 // 17 samples instead of 9).
 template <int JCH, int RPW>
 __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
-                                               double2* __restrict__ ir) {
+                                               double2* __restrict__ ir, const int* __restrict__ chunk_n0, int nchunk) {
     extern __shared__ double sm[];
     constexpr int LPR = WAVE / RPW;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -233,7 +233,11 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
         wi[p] = sn;
     }
     __syncthreads();
-    const int n0 = (blockIdx.x * LPR + sl) * JCH;
+    // chunk_n0: the first samples of the chunks to form (the samples some Q^H
+    // row reads, JakesChunks); otherwise all N samples in consecutive chunks
+    const int ck = blockIdx.x * LPR + sl;
+    if (chunk_n0 && ck >= nchunk) return;
+    const int n0 = chunk_n0 ? chunk_n0[ck] : ck * JCH;
     if (n0 >= ch.N) return;
     const double t0 = (double)n0 * ch.dt;
     double2 acc[JCH];
@@ -295,12 +299,13 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
 }
 
 template <int JCH, int RPW = 1>
-static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir) {
+static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir,
+                           const int* chunk_n0 = nullptr, int nck = 0) {
     constexpr int LPR = WAVE / RPW;
-    const int nchunk = (ch.N + JCH - 1) / JCH;
+    const int nchunk = chunk_n0 ? nck : (ch.N + JCH - 1) / JCH;
     dim3 grid((nchunk + LPR - 1) / LPR, R / (4 * RPW), ch.ntap);
     hipLaunchKernelGGL((k_jakes<JCH, RPW>), grid, dim3(256), (size_t)4 * RPW * 4 * ch.paths * sizeof(double), s, ch,
-                       seed, rep0, R, ir);
+                       seed, rep0, R, ir, chunk_n0, nchunk);
 }
 
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
@@ -379,7 +384,7 @@ __global__ void __launch_bounds__(64) k_discrete(ChannelK ch, uint64_t seed, uin
 }
 
 void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
-                  double2* ir) {
+                  double2* ir, const JakesChunks* jc) {
     if (ch.fD == 0.0) {
         hipLaunchKernelGGL(k_static, dim3(R / WAVE, (ch.N + 63) / 64, ch.ntap), dim3(WAVE), 0, s, ch, seed, rep0, R, ir);
         return;
@@ -387,6 +392,12 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
     if (ch.model >= 2) {
         hipLaunchKernelGGL(k_discrete, dim3(R / WAVE, (ch.N + DCH - 1) / DCH, ch.ntap), dim3(WAVE), 0, s, ch, seed,
                            rep0, R, ir);
+        return;
+    }
+    // only the samples some Q^H row reads (OFDM: the FFT windows): chunks of 12
+    // aligned to them, two realisations per wave
+    if (jc && jc->n0 && op.jakes_win && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024) {
+        launch_jakes_t<JakesChunks::LEN, 2>(s, ch, seed, rep0, R, ir, jc->n0, jc->n);
         return;
     }
     // two realisations per wave (32 lanes each) when that gives chunks of 9-20

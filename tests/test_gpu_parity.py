@@ -267,7 +267,8 @@ def test_stage_variants_agree(name):
     the W contraction instead of the structured MMSE IC (k_mic_fft), decisions
     passed between the stages as v / u instead of symbol indices, k_mic_fft's
     taps on the VALU instead of the matrix cores, the pilot pre-pass from W's
-    pilot rows (k_pilot_pre) instead of the structured chain."""
+    pilot rows (k_pilot_pre) instead of the structured chain, the Jakes taps at
+    every sample instead of only where a Q^H row reads them."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -282,7 +283,7 @@ def test_stage_variants_agree(name):
                 {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
-                {"pilot_fft": 0})
+                {"pilot_fft": 0}, {"jakes_win": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
