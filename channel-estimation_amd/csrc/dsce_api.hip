@@ -1089,7 +1089,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
             const bool mic = pfuse && mmse_fft_ok(op, s.k, mm, c->ch, b);
             // both IC chains index-based (k_mic_fft + k_pic_fft): the stage and the
             // chains pass decisions as symbol indices (qe / qp), not as v / u
-            const bool qidx = mic && chain && !two && s.k.M <= 65536 && op.qidx &&
+            const bool qidx = mic && chain && s.k.M <= 65536 && op.qidx &&
                               perfect_chain_fft(op, s.k, c->ch, b, c->niter);
             double2* hp_prev = b.hp;
             double2* hp_cur = b.hp2;
