@@ -328,9 +328,11 @@ def main():
         "data": "synthetic (Philox4x32-10 streams, include/dsce.h)",
         "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
                    "parallelism": "dp%d" % world, "options": options},
-        "roofline": {"bound": "valu" if mic_l else "mfma",
-                     "kernel": ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v, H_hat = Bv hP, "
-                                "DFT-24 chain + one-tap + detection (FP64 VALU)") if mic_l else
+        "roofline": {"bound": "mfma",
+                     "kernel": ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v; H_hat = Bv hP "
+                                "on the matrix cores (3M), DFT-24 chain + one-tap + detection on the VALU; FP64 "
+                                "roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both peaks "
+                                "78.6 TF)") if mic_l else
                                ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
                                 "diag(D_hat) + detection in its epilogue)"),
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -343,7 +345,7 @@ def main():
                      "flops_per_launch": flops / launches if launches else None,
                      "work_model": ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
                                     "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
-                                    "at 5 n log2 n flops; peak = FP64 vector spec (= FP64 matrix spec)") if mic_l else
+                                    "at 5 n log2 n flops; peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
                                     "fused diag(D_hat)), 8 real flops per CMAC; mfma_busy = executed matrix-core "
                                     "flops (6 of 8 in the 3M form) / measured peak"),

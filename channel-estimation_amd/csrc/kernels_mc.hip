@@ -808,7 +808,9 @@ __global__ void __launch_bounds__(64) k_tx_symbols(SchemeK sk, int bits_slot, in
         const uint32_t word = wi == 0 ? w.x : wi == 1 ? w.y : wi == 2 ? w.z : w.w;
         const uint16_t si = (uint16_t)((word >> (q & 31)) & mmask);   // bi2de, LSB first
         sidx[(size_t)i * R + rl] = si;
-        sidr[(size_t)sk.data_pos[i] * R + rl] = si;                    // the same, row-indexed
+        // the same, row-indexed (select mode only: data_pos holds one dummy entry
+        // for a data-spreading scheme, whose data symbols have no rows)
+        if (!sk.despread) sidr[(size_t)sk.data_pos[i] * R + rl] = si;
     }
     // x = P [xP; xD]
     for (int r = 0; r < sk.LK; ++r) {
