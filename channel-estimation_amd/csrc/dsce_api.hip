@@ -442,6 +442,8 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
         }
         s.k.pf_ok = fok ? 1 : 0;
         s.k.pf_scale = make_double2(qsc.x * gsc.x - qsc.y * gsc.y, qsc.x * gsc.y + qsc.y * gsc.x);
+        s.k.pf_gs = gsc;
+        s.k.pf_qs = qsc;
     }
     // W band: rows r, k = (c, p); c overlaps where Q-support(r) meets (H G)-support(c)
     int maxd = 0;
@@ -1052,7 +1054,9 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
         mm.npb = s.npb;
         {
             Timed t(c, "tx");
-            launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b);
+            b.U = R * std::min(chunk, c->nsnr);
+            launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b,
+                      txrx_fft_ok(op, s.k, c->ch, b));
         }
         const bool pfuse = perfect_fusable(op, s.k);
         for (int s0 = 0; s0 < c->nsnr; s0 += chunk) {
@@ -1856,7 +1860,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

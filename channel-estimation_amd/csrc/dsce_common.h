@@ -174,6 +174,7 @@ struct SchemeK {
     // max tap delay (checked entry by entry at pack time); pf_scale = qs gs
     int pf_ok;
     double2 pf_scale;
+    double2 pf_gs, pf_qs;         // the two factors: G block = gs w^(l m), Q^H block = qs w^(-l m)
 };
 
 struct ChannelK {

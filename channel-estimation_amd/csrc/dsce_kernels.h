@@ -28,6 +28,7 @@ struct Opts {
     int mic_mfma = 1;         // k_mic_fft's estimated taps as an MFMA GEMM (3M) instead of VALU dot products
     int pilot_fft = 1;        // structured pilot pre-pass (k_mic_fft PILOT mode) instead of k_pilot_pre's W rows
     int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
+    int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -45,6 +46,7 @@ enum : unsigned {
     PATH_NOISE_FUSED = 1u << 9,    // noise drawn inside the Q^H pass
     PATH_PIC_FFT = 1u << 10,       // k_pic_fft (perfect-CSI chain by FFT, OFDM)
     PATH_MIC_FFT = 1u << 11,       // k_pilot_pre + k_mic_fft (MMSE IC as Q' H_hat G by FFT, OFDM)
+    PATH_TXRX_FFT = 1u << 12,      // k_txrx_fft (TX + channel + noisy receiver front by FFT, OFDM)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -129,8 +131,11 @@ struct JakesChunks {
 // jc: form only those chunks (samples outside stay as they are: zero)
 void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
                   double2* ir, const JakesChunks* jc = nullptr);
+// txrx (txrx_fft_ok): only the symbols; k_txrx_fft forms s, r0 and diag(D) in
+// launch_rx_front
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
-               uint64_t rep0, McBuffers& b);
+               uint64_t rep0, McBuffers& b, bool txrx = false);
+bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
                          uint64_t seed, uint64_t rep0, McBuffers& b);
 // qidx: a row-local (p_diag) scheme's decisions leave the stage as symbol

@@ -840,10 +840,11 @@ __global__ void __launch_bounds__(64) k_channel_apply(ChannelK ch, int R, const 
 }
 
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
-               uint64_t rep0, McBuffers& b) {
+               uint64_t rep0, McBuffers& b, bool txrx) {
     const int R = b.R;
     hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
                        b.xp, b.sidx, b.xs, b.sidr);
+    if (txrx) return;      // s, r0 and diag(D) come from k_txrx_fft with the receiver front
     // s = G x (script:376-378)
     launch_band(s, sk.G, R, nullptr, LoadSoA{b.xs, R}, StoreSoA{b.ss, R});
     hipLaunchKernelGGL(k_channel_apply, dim3(R / WAVE, (ch.N + 63) / 64), dim3(WAVE), 0, s, ch, R, b.ir, b.ss, b.r0);
@@ -892,8 +893,12 @@ struct LoadNoisy {
     __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
 };
 
+static unsigned launch_txrx(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
+                            uint64_t seed, uint64_t rep0, McBuffers& b);
+
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
                          uint64_t seed, uint64_t rep0, McBuffers& b) {
+    if (txrx_fft_ok(op, sk, ch, b)) return launch_txrx(s, op, sk, ch, pn, seed, rep0, b);
     if (sk.qh_disjoint && op.noise_fuse) {
         launch_band(s, sk.QH, b.U, nullptr, LoadNoisy{b.r0, pn, seed, rep0, b.R, b.snr0, sk.noise_slot},
                     StoreSoA{b.y, b.U});
@@ -2246,6 +2251,141 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
     if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0);
 }
 
+// ---------------------------------------------------------------------------
+// TX, channel and receiver front of an FFT-form OFDM scheme in one pass
+// (k_txrx_fft, rows a7, a8, a12; script:371-409): per realisation and symbol
+// s = gs IDFT24(x) (G with its cyclic prefix), r0[n] = sum_q IR_q[n] s[n - d_q]
+// (GetConvolutionMatrix, FastFading.m:284), and for every SNR point of the
+// chunk y = qs DFT24(r0 + sqrt(Pn/2) z) with z the noise stream of LoadNoisy
+// (identical draws); the perfect-CSI diag(D) = qs gs sum_q w^(-l d_q) S_q(IR)
+// (S_q = the window sum of tap q).  Replaces the G band, k_channel_apply, the
+// diag(D) band and the noisy Q^H band: s and r0 never reach memory.  Lane quad
+// = realisation (k_pic_fft's layout), block = 64 realisations x one symbol.
+// ---------------------------------------------------------------------------
+struct TxrxArgs {
+    const double2* __restrict__ xs;   // [LK][R] precoded symbols P [xP; xD]
+    const double2* __restrict__ ir;   // [ntap][N][R]
+    const double* __restrict__ pn;    // [nsnr]
+    double2* y;                       // [LK][U]
+    double2* h;                       // [LK][R]
+    uint64_t seed, rep0;
+    int N, R, U, snr0, nchunk, slot;
+};
+
+template <int NT, int SH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
+    // block: 64 realisations x one symbol, XCD-aware (symbol fastest)
+    int L = blockIdx.x;
+    if (xcd) L = xcd_remap(L, gridDim.x);
+    const int blk = L % sk.QH.nblk, rg = L / sk.QH.nblk;
+    const int tid = threadIdx.x, l = tid & 63, r = l & 3, w = tid >> 6;
+    const int rl = rg * WAVE + w * 16 + (l >> 2);
+    const int R = ta.R;
+    const int cq = (r >> 1) + 2 * (r & 1);
+    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    __shared__ double2 twa[2][4][6];
+    __shared__ double2 twb[2][4];
+    __shared__ double2 wrow[24];
+    const double2 gs = sk.pf_gs, qs = sk.pf_qs, ps = sk.pf_scale;
+    {
+        const int e = ((tid / 6) % 4) * (tid % 6);
+        const double2 tw = kW24[e % 12];
+        if (tid < 48) {
+            const int dir = tid / 24;
+            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
+        } else if (tid < 56) {
+            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
+            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
+        } else if (tid >= 64 && tid < 88) {
+            const int lr = tid - 64;
+            const double2 t0 = kW24[lr % 12];
+            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            wrow[lr] = c_mul(ps, make_double2(wl.x, -wl.y));
+        }
+    }
+    double2 x[6], taps[6][NT];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) x[a] = ta.xs[(size_t)(row0 + 4 * a + r) * R + rl];
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+#pragma unroll
+        for (int q = 0; q < NT; ++q) taps[m][q] = ta.ir[((size_t)q * ta.N + klo + 6 * cq + m) * R + rl];
+    __syncthreads();
+    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
+    // perfect-CSI diag(D) of the symbol's rows from the window sums of the taps
+    {
+        double2 s0 = make_double2(0.0, 0.0), s1 = s0;
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int m = 0; m < 6; ++m) sq = c_add(sq, taps[m][q]);
+            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            if ((SH >> q) & 1) s1 = c_add(s1, sq);
+            else s0 = c_add(s0, sq);
+        }
+        s0 = c_mul(ps, s0);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            double2 hv = s0;
+            c_fma(hv, wrow[4 * a + r], s1);
+            if (ta.snr0 == 0) ta.h[(size_t)(row0 + 4 * a + r) * R + rl] = hv;
+        }
+    }
+    // s = gs IDFT24(x): lane r ends with the time samples 6 cq + m
+    dft6<1>(x);
+    double2 t[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
+        const double2 pv = dpp_c<QP_XOR2>(p);
+        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+        e = c_mulf(e, twb[0][r]);
+        const double2 qv = dpp_c<QP_XOR1>(e);
+        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+    }
+    // r0 = H s over the window (the delayed tap reads the cyclic prefix for m = 0
+    // of quarter 0: sample 5 of quarter 3)
+    double2 r0[6];
+    {
+        const double2 tprev = dpp_c<QP_PREV>(t[5]);
+#pragma unroll
+        for (int m = 5; m >= 0; --m) {
+            const double2 tp = m ? t[m - 1] : tprev;
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
+            r0[m] = acc;
+        }
+    }
+    // per SNR point: r = r0 + noise (LoadNoisy's draws), y = qs DFT24(r)
+    for (int k = 0; k < ta.nchunk; ++k) {
+        const int snr = ta.snr0 + k;
+        const double sc = sqrt(ta.pn[snr] / 2.0);
+        double2 f[6];
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const double2 z = normal_pair(stream_block(ta.seed, ta.rep0 + (uint64_t)rl, STREAM_NOISE,
+                                                       (uint32_t)(snr + 256 * ta.slot), (uint32_t)(klo + 6 * cq + m)));
+            const double2 rv = make_double2(r0[m].x + sc * z.x, r0[m].y + sc * z.y);
+            const double2 pv = dpp_c<QP_XOR1>(rv);
+            double2 g = make_double2(fma(sg2, rv.x, pv.x), fma(sg2, rv.y, pv.y));
+            g = c_mulf(g, twb[1][r]);
+            const double2 qv = dpp_c<QP_XOR2>(g);
+            f[m] = c_mulf(make_double2(fma(sg1, g.x, qv.x), fma(sg1, g.y, qv.y)), twa[1][r][m]);
+        }
+        dft6<-1>(f);
+        const size_t u0 = (size_t)k * R + rl;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) ta.y[(size_t)(row0 + 4 * a + r) * ta.U + u0] = f[p6(a)];
+    }
+}
+
+bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
+
 template <int NT, class Out>
 static void launch_pass2(hipStream_t s, const SchemeK& sk, const ChannelK& ch, McBuffers& b, const BandOrder& ord,
                          const Out& o, size_t lds) {
@@ -2314,6 +2454,36 @@ static int pic_fft_shift(const ChannelK& ch) {
         sh |= ch.tap_delay[q] << q;
     }
     return (ch.ntap == 1 && sh == 0) || (ch.ntap == 2 && (sh == 1 || sh == 2)) ? sh : -1;
+}
+
+// k_txrx_fft applies: FFT-form OFDM blocks, at most two taps with delays <= 1,
+// every sample of the scheme's frame read by exactly one Q^H block
+bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    return op.txrx_fft && op.noise_fuse && sk.pf_ok && sk.qh_disjoint && pic_fft_shift(ch) >= 0 &&
+           (b.R % WAVE) == 0 && (long long)ch.ntap * ch.N * b.R < (1ll << 40);
+}
+
+static unsigned launch_txrx(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
+                            uint64_t seed, uint64_t rep0, McBuffers& b) {
+    TxrxArgs ta{};
+    ta.xs = b.xs;
+    ta.ir = b.ir;
+    ta.pn = pn;
+    ta.y = b.y;
+    ta.h = b.h;
+    ta.seed = seed;
+    ta.rep0 = rep0;
+    ta.N = ch.N;
+    ta.R = b.R;
+    ta.U = b.U;
+    ta.snr0 = b.snr0;
+    ta.nchunk = b.U / b.R;
+    ta.slot = sk.noise_slot;
+    const dim3 grid((b.R / WAVE) * sk.QH.nblk), blk(256);
+    if (ch.ntap == 1) hipLaunchKernelGGL((k_txrx_fft<1, 0>), grid, blk, 0, s, sk, ta, op.xcd);
+    else if (pic_fft_shift(ch) == 1) hipLaunchKernelGGL((k_txrx_fft<2, 1>), grid, blk, 0, s, sk, ta, op.xcd);
+    else hipLaunchKernelGGL((k_txrx_fft<2, 2>), grid, blk, 0, s, sk, ta, op.xcd);
+    return PATH_NOISE_FUSED | PATH_TXRX_FFT;
 }
 
 static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {

@@ -194,6 +194,7 @@ typedef struct {
 #define DSCE_PATH_NOISE_FUSED     (1u << 9)   /* AWGN drawn inside the Q^H pass                            */
 #define DSCE_PATH_PIC_FFT         (1u << 10)  /* k_pic_fft: perfect-CSI IC chain by FFT (OFDM, VALU)       */
 #define DSCE_PATH_MIC_FFT         (1u << 11)  /* k_pilot_pre + k_mic_fft: MMSE IC as Q' H_hat G by FFT (OFDM) */
+#define DSCE_PATH_TXRX_FFT        (1u << 12)  /* k_txrx_fft: TX + channel + noisy receiver front by FFT (OFDM) */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);

@@ -73,7 +73,7 @@ def test_mmse_estimator_matches_oracle(ofdm):
 # for the perfect-CSI IC chain, k_stage_fused for the one-tap stage); the W
 # contraction (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"mic_fft", "pic_fft", "stage_fused", "noise_fused"}
+BENCH_PATH = {"mic_fft", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
 W_PATH = BENCH_PATH - {"mic_fft"} | {"wpair3_fused"}
 
 
@@ -268,7 +268,8 @@ def test_stage_variants_agree(name):
     passed between the stages as v / u instead of symbol indices, k_mic_fft's
     taps on the VALU instead of the matrix cores, the pilot pre-pass from W's
     pilot rows (k_pilot_pre) instead of the structured chain, the Jakes taps at
-    every sample instead of only where a Q^H row reads them."""
+    every sample instead of only where a Q^H row reads them, TX / channel /
+    noisy Q^H as banded passes instead of k_txrx_fft."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -283,7 +284,7 @@ def test_stage_variants_agree(name):
                 {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
-                {"pilot_fft": 0}, {"jakes_win": 0})
+                {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
