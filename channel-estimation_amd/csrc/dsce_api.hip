@@ -106,6 +106,7 @@ struct Scheme {
     double2* Bv = nullptr;          // structured MMSE IC operator (k_mic_fft; null: not eligible)
     double2* Bs = nullptr;
     int* pblk = nullptr;            // QH blocks with pilot rows (k_pilot_fft)
+    int* pmask = nullptr;           // [QH blk] 1 = holds pilot rows
     int npb = 0;
     long long wp_elems = 0, wp_exec = 0;
     long long w_diag = 0;           // (r, r) pairs inside the band (stored as zeros: diag(D_hat) comes from Wd)
@@ -763,14 +764,18 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
         s.Bv = s.Bs = nullptr;
         return;
     }
-    std::vector<int> pb;
+    std::vector<int> pb, pm(nblk, 0);
     for (int b = 0; b < nblk; ++b) {
         bool has = false;
         for (int p : s.pilot_pos) has |= p >= s.qband.row0[b] && p < s.qband.row0[b] + s.qband.nrows[b];
         if (has) pb.push_back(b);
+        pm[b] = has ? 1 : 0;
     }
     s.npb = (int)pb.size();
-    if (s.npb) s.pblk = dupload(c, pb);
+    if (s.npb) {
+        s.pblk = dupload(c, pb);
+        s.pmask = dupload(c, pm);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -795,8 +800,9 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         if (s.Bv) free_alloc(c, s.Bv);
         if (s.Bs) free_alloc(c, s.Bs);
         if (s.pblk) free_alloc(c, s.pblk);
+        if (s.pmask) free_alloc(c, s.pmask);
         s.Bv = s.Bs = nullptr;
-        s.pblk = nullptr;
+        s.pblk = s.pmask = nullptr;
         s.npb = 0;
         s.W = s.Wd = s.Wp = nullptr;
         s.Wp3 = nullptr;
@@ -1051,6 +1057,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
         mm.Bv = s.Bv;
         mm.Bs = s.Bs;
         mm.pblk = s.pblk;
+        mm.pmask = s.pmask;
         mm.npb = s.npb;
         {
             Timed t(c, "tx");
@@ -1091,6 +1098,8 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
             const bool mfuse = pfuse && mmse_fused_ok(op, s.k, mm, b);
             // OFDM: the MMSE IC as Q' H_hat G by FFT (k_pilot_pre + k_mic_fft)
             const bool mic = pfuse && mmse_fft_ok(op, s.k, mm, c->ch, b);
+            // the pilot pass hands y_ic of the pilot symbols to k_mic_fft
+            const bool yic = mic && op.pilot_fft && op.mic_yic && mm.npb > 0;
             // both IC chains index-based (k_mic_fft + k_pic_fft): the stage and the
             // chains pass decisions as symbol indices (qe / qp), not as v / u
             const bool qidx = mic && chain && s.k.M <= 65536 && op.qidx &&
@@ -1123,7 +1132,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                         Timed t(c, "k_pilot_pre");
                         if (op.pilot_fft && mm.npb > 0)
                             launch_pilot_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter), b, hp_prev,
-                                             hp_cur, op.xcd, qidx);
+                                             hp_cur, op.xcd, qidx, yic);
                         else
                             launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur,
                                              qidx);
@@ -1135,7 +1144,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                                              s.k.slI, s.k.slQ};
                         s.path |= launch_mmse_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter),
                                                   var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
-                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0);
+                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0, yic);
                     }
                     std::swap(hp_prev, hp_cur);
                     if (!two && !chain) {
@@ -1860,7 +1869,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

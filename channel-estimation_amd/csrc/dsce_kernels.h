@@ -29,6 +29,7 @@ struct Opts {
     int pilot_fft = 1;        // structured pilot pre-pass (k_mic_fft PILOT mode) instead of k_pilot_pre's W rows
     int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
     int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
+    int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -117,6 +118,7 @@ struct MmseK {
     const double2* Bs;    // [var][snr][QH blk][ntap][NP]: Bv summed over each block's FFT window
     const int* pblk;      // QH blocks holding pilot rows (k_pilot_fft)
     int npb;
+    const int* pmask;     // [QH blk]: 1 = holds pilot rows
 };
 
 // Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
@@ -167,8 +169,9 @@ struct PerfectDetectArgs {
 // by FFT with the stage in its epilogue (after k_pilot_pre formed hp_new)
 bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b);
 // the pilot pre-pass of that path: y_ic of the stage at the pilot rows -> hp_new
+// yic: also store y_ic of the pilot symbols (for k_mic_fft's pilot-symbol blocks)
 void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx);
+                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx, bool yic = false);
 // stage 0 (one-tap + detection of both branches) of such a scheme when both IC
 // chains are index-based: k_ls + k_stage0_fft, decisions into qe / qp
 unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
@@ -176,7 +179,7 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                          const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,
-                         bool tapm = true);
+                         bool tapm = true, bool yic = false);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in

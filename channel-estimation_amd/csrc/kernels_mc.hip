@@ -1799,6 +1799,12 @@ struct MicArgs {
     const int* pblk;
     int npb;
     double2* hp_out;
+    // y_ic of the pilot symbols handed from the pilot pass to k_mic_fft (yic):
+    // the pass stores it, the main pass's pilot-symbol blocks load it instead
+    // of forming it again (same taps, same decisions, same chain)
+    double2* yest;                        // [LK][U]
+    const int* pmask;                     // [nblk]: 1 = the block holds pilot rows
+    int yic;
 };
 
 template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM, bool PILOT>
@@ -1807,6 +1813,8 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     int ug, blk;
     band_block(ord, PILOT ? ma.npb : sk.QH.nblk, ug, blk);
     if (PILOT) blk = ma.pblk[blk];
+    // block-uniform: this pilot-symbol block's y_ic comes from the pilot pass
+    const bool yic = !PILOT && ma.yic && ma.pmask[blk];
     const int tid = threadIdx.x, l = tid & 63, r = l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int U = o.U, R = o.R;
@@ -1839,11 +1847,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
         const double2* __restrict__ bvb = ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo) * NP;
         double2 bvr[PER];
+        if (!yic)
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
-            bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
-        }
+            for (int k = 0; k < PER; ++k) {
+                const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
+                bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
+            }
         const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
         const int e = ((tid / 6) % 4) * (tid % 6);
         const double2 tw = kW24[e % 12];
@@ -1853,11 +1862,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             rpv[tid] = pv;
             rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
         }
+        if (!yic)
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = tid + 256 * k;
-            if (i < NBV) sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
-        }
+            for (int k = 0; k < PER; ++k) {
+                const int i = tid + 256 * k;
+                if (i < NBV) sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
+            }
         if (tid < NT * NP) sbs[tid / NP][tid % NP] = bsv;
         if (tid < 48) {
             const int dir = tid / 24;
@@ -1883,7 +1893,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // products; lane (g = l >> 4, jc = l & 15) holds B[4 ks + g][unit jc]
     constexpr int NTILE = (NT * 24 + 15) / 16, NKS = NP / 4;
     double br[TAPM ? NKS : 1], bi[TAPM ? NKS : 1], bsm[TAPM ? NKS : 1];
-    if (TAPM) {
+    if (TAPM && !yic) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             const double2 hv = ma.hp_prev[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
@@ -1895,12 +1905,14 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
-        if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
-        else u[a] = ma.v[(size_t)row * U + unit];
+        if (!yic) {
+            if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
+            else u[a] = ma.v[(size_t)row * U + unit];
+        }
         if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        yv[a] = o.y[(size_t)row * U + unit];
+        yv[a] = (yic ? ma.yest : o.y)[(size_t)row * U + unit];   // yic: y_ic itself
     }
-    if (!TAPM)
+    if (!TAPM && !yic)
 #pragma unroll
         for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
     if (!PILOT)
@@ -1915,7 +1927,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    if (QIDX)
+    if (QIDX && !yic)
 #pragma unroll
         for (int a = 0; a < 6; ++a)
             u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
@@ -1925,7 +1937,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // jc) go through the wave's own LDS slab into the quad layout; otherwise
     // each lane forms its 12 taps on the VALU (Bv rows broadcast from LDS)
     __shared__ double2 hhs[TAPM ? 4 : 1][TAPM ? NTILE * 16 : 1][17];
-    if (TAPM) {
+    if (TAPM && !yic) {
         const int g = l >> 4, jc = l & 15;
         const int R = jc;                                   // A row of this lane within a tile
 #pragma unroll
@@ -1988,51 +2000,56 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     sp0 = c_mul(scale, sp0);
     sn0 = c_mul(scale, sn0);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
-    // ---- phase B: acc = Q' H_hat G u for the symbol (k_pic_fft's chain)
+    // ---- phase B: acc = Q' H_hat G u for the symbol (k_pic_fft's chain); a yic
+    // block has y_ic already
     double2 x[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) x[a] = u[a];
-    dft6<1>(x);
-    double2 t[6];
-#pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
-        const double2 pv = dpp_c<QP_XOR2>(p);
-        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-        e = c_mulf(e, twb[0][r]);
-        const double2 qv = dpp_c<QP_XOR1>(e);
-        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+    if (!yic) {
+    #pragma unroll
+        for (int a = 0; a < 6; ++a) x[a] = u[a];
+        dft6<1>(x);
+        double2 t[6];
+    #pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
+            const double2 pv = dpp_c<QP_XOR2>(p);
+            double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+            e = c_mulf(e, twb[0][r]);
+            const double2 qv = dpp_c<QP_XOR1>(e);
+            t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+        }
+        const double2 tprev = dpp_c<QP_PREV>(t[5]);
+    #pragma unroll
+        for (int m = 5; m >= 0; --m) {
+            const double2 tp = m ? t[m - 1] : tprev;
+            double2 acc = make_double2(0.0, 0.0);
+    #pragma unroll
+            for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
+            t[m] = acc;
+        }
+    #pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            const double2 pv = dpp_c<QP_XOR1>(t[m]);
+            double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+            f = c_mulf(f, twb[1][r]);
+            const double2 qv = dpp_c<QP_XOR2>(f);
+            x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+        }
+        dft6<-1>(x);
     }
-    const double2 tprev = dpp_c<QP_PREV>(t[5]);
-#pragma unroll
-    for (int m = 5; m >= 0; --m) {
-        const double2 tp = m ? t[m - 1] : tprev;
-        double2 acc = make_double2(0.0, 0.0);
-#pragma unroll
-        for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
-        t[m] = acc;
-    }
-#pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const double2 pv = dpp_c<QP_XOR1>(t[m]);
-        double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-        f = c_mulf(f, twb[1][r]);
-        const double2 qv = dpp_c<QP_XOR2>(f);
-        x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
-    }
-    dft6<-1>(x);
     if constexpr (PILOT) {
         // the next stage's LS pilot estimates (script:487-489) at the block's pilot rows
+        // (and, for k_mic_fft's yic blocks, y_ic of every row of the symbol)
         const double sqk = 1.0 / sk.inv_sqrt_kappa;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const int row = row0 + 4 * a + r;
             const int pc = sk.row_pcol[row];
+            double2 ye = c_sub(yv[a], x[p6(a)]);
+            double2 hpv = sp0;
+            c_fma(hpv, wrow[4 * a + r], sp1);
+            c_fma(ye, hpv, u[a]);
+            if (ma.yic) ma.yest[(size_t)row * U + unit] = ye;
             if (pc >= 0 && pc < NP) {
-                double2 ye = c_sub(yv[a], x[p6(a)]);
-                double2 hpv = sp0;
-                c_fma(hpv, wrow[4 * a + r], sp1);
-                c_fma(ye, hpv, u[a]);
                 const double2 q = c_div(ye, o.xp[(size_t)pc * R + rl]);
                 ma.hp_out[(size_t)pc * U + unit] = make_double2(q.x / sqk, q.y / sqk);
             }
@@ -2053,8 +2070,11 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         c_fma(hpv, wl, sp1);
         c_fma(hnv, wl, sn1);
         hn[a] = hnv;
-        double2 ye = c_sub(yv[a], x[p6(a)]);
-        c_fma(ye, hpv, u[a]);
+        double2 ye = yv[a];
+        if (!yic) {
+            ye = c_sub(yv[a], x[p6(a)]);
+            c_fma(ye, hpv, u[a]);
+        }
         const double2 z = c_div1(ye, hnv);
         int tI, tQ;
         const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
@@ -2555,7 +2575,8 @@ bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Chann
 
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx, bool tapm) {
+                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx, bool tapm,
+                         bool yic) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     MicArgs ma{};
     ma.bv = mm.Bv;
@@ -2574,6 +2595,9 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     ma.nstage = n_iter + 1;
     ma.last = last ? 1 : 0;
     ma.scheme = pd->scheme;
+    ma.yest = b.yest;
+    ma.pmask = mm.pmask;
+    ma.yic = yic && mm.pmask ? 1 : 0;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
 #define LAUNCH_MIC3(NTV, SHV, TM)                                                                                     \
@@ -2605,7 +2629,7 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
 // IC iteration `stage` at the pilot rows only (script:482-489) -> hp_new, over
 // the symbol blocks that hold pilots (4 of 14 at C2); MFMA taps, no detection.
 void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx) {
+                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx, bool yic) {
     PerfectDetectArgs pd{};
     StorePerfectDetect o = chain_detect(sk, b, &pd, 0);
     MicArgs ma{};
@@ -2620,6 +2644,8 @@ void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const C
     ma.nblk = sk.QH.nblk;
     ma.pblk = mm.pblk;
     ma.npb = mm.npb;
+    ma.yest = b.yest;
+    ma.yic = yic ? 1 : 0;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
     const dim3 grid((b.U / WAVE) * mm.npb), blk(256);
 #define LAUNCH_PIL(NTV, SHV)                                                                                          \

@@ -269,7 +269,8 @@ def test_stage_variants_agree(name):
     taps on the VALU instead of the matrix cores, the pilot pre-pass from W's
     pilot rows (k_pilot_pre) instead of the structured chain, the Jakes taps at
     every sample instead of only where a Q^H row reads them, TX / channel /
-    noisy Q^H as banded passes instead of k_txrx_fft."""
+    noisy Q^H as banded passes instead of k_txrx_fft, the pilot symbols' y_ic
+    formed again in k_mic_fft instead of handed over by the pilot pass."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -284,7 +285,8 @@ def test_stage_variants_agree(name):
                 {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
-                {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0})
+                {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
+                {"mic_yic": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
