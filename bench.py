@@ -347,8 +347,9 @@ def main():
                                     "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
                                     "at 5 n log2 n flops; peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
-                                    "fused diag(D_hat)), 8 real flops per CMAC; mfma_busy = executed matrix-core "
-                                    "flops (6 of 8 in the 3M form) / measured peak"),
+                                    "fused diag(D_hat)), 8 real flops per CMAC; the 3M form executes 6 of the 8 counted "
+                                    "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "
+                                    "peak"),
                      "paths": paths},
         "cpu_baseline": cpu,
         "setup_s": setup_s,

@@ -10,7 +10,7 @@ namespace dsce {
 struct Opts {
     int xcd = 1;              // XCD-aware work order (each XCD walks a contiguous range)
     int fuse_stage = 1;       // MMSE stage of the IC iterations fused into the contraction
-    int wpair_3m = -1;        // 3M complex products in k_wpair3: -1 auto, 0 off (4 MFMAs), 1 on
+    int wpair_3m = -1;        // 3M complex products in k_wpair3: -1 / 1 on (default), 0 off (4 MFMAs)
     int wda_3m = 1;           // fused epilogue's diag(D_hat) in 3M form
     int pic_chain = 3;        // perfect-CSI IC: 0 per-iteration passes, 1 VALU chain, 2 MFMA chain, 3 FFT chain
     int pfuse = 1;            // perfect-CSI detection fused into the second banded pass

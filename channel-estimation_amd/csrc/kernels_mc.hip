@@ -3285,8 +3285,9 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
 }
 
 static bool wpair_3m(const Opts& op, const MmseK& mm) {
-    // 3M by default where its extra registers still leave 3 waves/SIMD (NP <= 16)
-    return mm.Wp3 && (op.wpair_3m < 0 ? mm.Pb.nks <= 4 : op.wpair_3m != 0);
+    // 3M by default (NP = 32 too: its extra registers cost occupancy, but the
+    // contraction still drops 286 -> 225 ms per launch at C5, r02)
+    return mm.Wp3 && op.wpair_3m != 0;
 }
 
 bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b) {
