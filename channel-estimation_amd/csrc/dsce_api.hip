@@ -1869,7 +1869,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(snr_base)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN
@@ -1885,6 +1885,7 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     if (n == "jakes_rpw" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "jakes_rpw: 1 | 2");
     if (n == "pic_chain" && (value < 0 || value > 3)) throw ApiError(DSCE_EINVAL, "pic_chain: 0 | 1 | 2 | 3");
     if (n == "streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "streams: 1 | 2");
+    if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;
     API_END

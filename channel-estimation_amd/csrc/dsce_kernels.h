@@ -30,6 +30,7 @@ struct Opts {
     int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
     int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
+    int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through

@@ -854,10 +854,12 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 
 // ---------------------------------------------------------------------------
 // a12: r = r0 + noise (script:397-403), lane = unit; grid (U/64, ceil(N/64)).
-// Noise sub-stream snr + 256 * slot (slot: schemes drawing separate noise, e.g.
-// n_FBMC / n_OFDM of SimpleVersion_DoublyFlat.m:125-126).
+// Noise sub-stream k + 256 * slot with k = base + snr the SNR point's index in
+// the full sweep (Opts::snr_base: a rank serving SNR points [base, ...) of a
+// sweep draws the one-rank run's noise) and slot the noise slot (schemes drawing
+// separate noise, e.g. n_FBMC / n_OFDM of SimpleVersion_DoublyFlat.m:125-126).
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int slot, const double* __restrict__ pn, uint64_t seed,
+__global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int slot, int base, const double* __restrict__ pn, uint64_t seed,
                                               uint64_t rep0, const double2* __restrict__ r0,
                                               double2* __restrict__ rbuf) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
@@ -866,7 +868,7 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int
     const double sc = sqrt(pn[snr] / 2.0);
     const int n0 = blockIdx.y * 64;
     for (int n = n0; n < n0 + 64 && n < N; ++n) {
-        const double2 z = normal_pair(stream_block(seed, rep, STREAM_NOISE, (uint32_t)(snr + 256 * slot), (uint32_t)n));
+        const double2 z = normal_pair(stream_block(seed, rep, STREAM_NOISE, (uint32_t)(base + snr + 256 * slot), (uint32_t)n));
         const double2 r = r0[(size_t)n * R + rl];
         rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * z.x, r.y + sc * z.y);
     }
@@ -880,13 +882,13 @@ struct LoadNoisy {
     const double2* __restrict__ r0;    // [N][R]
     const double* __restrict__ pn;
     uint64_t seed, rep0;
-    int R, snr0, slot;
+    int R, snr0, slot, base;
     typedef double2 Regs;
     __device__ __forceinline__ Regs load(int n, int lane) const {
         const int snr = snr0 + lane / R, rl = lane % R;
         const double sc = sqrt(pn[snr] / 2.0);
         const double2 z = normal_pair(stream_block(seed, rep0 + (uint64_t)rl, STREAM_NOISE,
-                                                   (uint32_t)(snr + 256 * slot), (uint32_t)n));
+                                                   (uint32_t)(base + snr + 256 * slot), (uint32_t)n));
         const double2 r = r0[(size_t)n * R + rl];
         return make_double2(r.x + sc * z.x, r.y + sc * z.y);
     }
@@ -900,11 +902,12 @@ unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const
                          uint64_t seed, uint64_t rep0, McBuffers& b) {
     if (txrx_fft_ok(op, sk, ch, b)) return launch_txrx(s, op, sk, ch, pn, seed, rep0, b);
     if (sk.qh_disjoint && op.noise_fuse) {
-        launch_band(s, sk.QH, b.U, nullptr, LoadNoisy{b.r0, pn, seed, rep0, b.R, b.snr0, sk.noise_slot},
+        launch_band(s, sk.QH, b.U, nullptr, LoadNoisy{b.r0, pn, seed, rep0, b.R, b.snr0, sk.noise_slot, op.snr_base},
                     StoreSoA{b.y, b.U});
         return PATH_NOISE_FUSED;
     }
-    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, sk.noise_slot, pn, seed, rep0,
+    hipLaunchKernelGGL(k_noise, dim3(b.U / WAVE, (sk.N + 63) / 64), dim3(WAVE), 0, s, sk.N, b.R, b.U, b.snr0, sk.noise_slot,
+                       op.snr_base, pn, seed, rep0,
                        b.r0, b.t);
     // y = Q' r (script:406-409)
     launch_band(s, sk.QH, b.U, nullptr, LoadSoA{b.t, b.U}, StoreSoA{b.y, b.U});
@@ -2289,7 +2292,7 @@ struct TxrxArgs {
     double2* y;                       // [LK][U]
     double2* h;                       // [LK][R]
     uint64_t seed, rep0;
-    int N, R, U, snr0, nchunk, slot;
+    int N, R, U, snr0, nchunk, slot, base;
 };
 
 template <int NT, int SH>
@@ -2389,7 +2392,8 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
             const double2 z = normal_pair(stream_block(ta.seed, ta.rep0 + (uint64_t)rl, STREAM_NOISE,
-                                                       (uint32_t)(snr + 256 * ta.slot), (uint32_t)(klo + 6 * cq + m)));
+                                                       (uint32_t)(ta.base + snr + 256 * ta.slot),
+                                                       (uint32_t)(klo + 6 * cq + m)));
             const double2 rv = make_double2(r0[m].x + sc * z.x, r0[m].y + sc * z.y);
             const double2 pv = dpp_c<QP_XOR1>(rv);
             double2 g = make_double2(fma(sg2, rv.x, pv.x), fma(sg2, rv.y, pv.y));
@@ -2499,6 +2503,7 @@ static unsigned launch_txrx(hipStream_t s, const Opts& op, const SchemeK& sk, co
     ta.snr0 = b.snr0;
     ta.nchunk = b.U / b.R;
     ta.slot = sk.noise_slot;
+    ta.base = op.snr_base;
     const dim3 grid((b.R / WAVE) * sk.QH.nblk), blk(256);
     if (ch.ntap == 1) hipLaunchKernelGGL((k_txrx_fft<1, 0>), grid, blk, 0, s, sk, ta, op.xcd);
     else if (pic_fft_shift(ch) == 1) hipLaunchKernelGGL((k_txrx_fft<2, 1>), grid, blk, 0, s, sk, ta, op.xcd);

@@ -1,8 +1,11 @@
 """Command-line Monte-Carlo run: the reference script's loop and plots
 (DoublySelectiveChannelEstimation.m:350-631) on one MI355X, or sharded over the
-GPUs of a node (one process per GPU, realisations split contiguously, one
-all-reduce of the counters and MSE sums — SURVEY §8e; bit-identical counts for
-any number of ranks):
+GPUs of a node (one process per GPU, one all-reduce of the counters and MSE
+sums — SURVEY §8e; bit-identical counts for any number of ranks).  Two shard
+axes: realisations (contiguous slices, the default) or SNR points (--shard snr:
+each rank builds the estimator for its own SNR points only, so the setup is
+split too; the noise keeps the sweep's SNR index through the engine's snr_base
+option):
 
     python -m dsce.simulate --config default --reps 4096 --out run.json --figures figs/
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -32,6 +35,8 @@ def main(argv=None):
     ap.add_argument("--npz", action="store_true")
     ap.add_argument("--figures", default=None, help="directory for Figure2-5.png")
     ap.add_argument("--mse", action="store_true", help="also accumulate the channel-estimation NMSE per stage")
+    ap.add_argument("--shard", choices=("reps", "snr"), default="reps",
+                    help="multi-rank split: realisation slices (default) or SNR points")
     a = ap.parse_args(argv)
 
     from dsce import results
@@ -56,33 +61,60 @@ def main(argv=None):
     names = tuple(a.schemes.split(","))
     S = build_setup(a.config, schemes=names)
     reps = a.reps if a.reps is not None else S.n_repetitions
-    reps = max(64 * world, (reps + 64 * world - 1) // (64 * world) * (64 * world))
-    first, mine = shard_range(0, reps, world, rank)
-    t0 = time.perf_counter()
-    eng = build_engine(S, device=device, batch=min(a.batch, mine))
-    setup_s = time.perf_counter() - t0
-    counts = np.zeros(eng.counter_shape(), dtype=np.int64)
-    if a.mse:
-        eng.enable_mse()
-    done, t0 = 0, time.perf_counter()
-    step = min(a.batch, mine)
-    while done < mine:
-        n = min(step, mine - done)
-        eng.run(a.seed, first + done, n, counts)
-        done += n
-        el = time.perf_counter() - t0
-        if rank == 0:
-            print("%d%% Completed! Time Left: %.1f s" % (100 * done // mine, el / done * (mine - done)), flush=True)
-    bits = np.array([eng.bits_per_rep(i) for i in range(len(names))])
-    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world}
-    if a.mse:
-        err, pw = eng.mse()
+    reps = max(64, (reps + 63) // 64 * 64)          # one wavefront of realisations per step
+    nsnr = len(S.snr_db)
+    if a.shard == "snr":
+        # SNR points [s0, s0 + ns) on this rank, every realisation
+        s0, ns = shard_range(0, nsnr, world, rank, align=1)
+        first, mine = 0, (reps if ns else 0)
+        Sr = _snr_subset(S, s0, ns) if ns else None
+        options = {"snr_base": s0}
+    else:
+        s0, ns = 0, nsnr
+        first, mine = shard_range(0, reps, world, rank)
+        Sr, options = S, {}
+    nst = S.n_iter + 1
+    counts = np.zeros((len(names), 2, 2, nsnr, nst), dtype=np.int64)
+    err = np.zeros((len(names), nsnr, nst))
+    pw = np.zeros((len(names), nsnr))
+    bits = None
+    setup_s, t0 = 0.0, time.perf_counter()
+    if mine:                                         # a rank with an empty shard contributes zeros
+        eng = build_engine(Sr, device=device, batch=min(a.batch, mine), options=options)
+        setup_s = time.perf_counter() - t0
+        sub = np.zeros(eng.counter_shape(), dtype=np.int64)
+        if a.mse:
+            eng.enable_mse()
+        done, t0 = 0, time.perf_counter()
+        step = min(a.batch, mine)
+        while done < mine:
+            n = min(step, mine - done)
+            eng.run(a.seed, first + done, n, sub)
+            done += n
+            el = time.perf_counter() - t0
+            if rank == 0:
+                print("%d%% Completed! Time Left: %.1f s" % (100 * done // mine, el / done * (mine - done)), flush=True)
+        counts[:, :, :, s0:s0 + ns, :] = sub
+        bits = np.array([eng.bits_per_rep(i) for i in range(len(names))])
+        if a.mse:
+            e_, p_ = eng.mse()
+            err[:, s0:s0 + ns, :] = e_
+            pw[:, s0:s0 + ns] = p_
+        eng.close()
+    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world, "shard": a.shard}
     if world > 1:
         dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else None
         counts = allreduce_counts(counts, dev)                    # the one exchange
         if a.mse:
             err = allreduce_counts(err, dev)
             pw = allreduce_counts(pw, dev)
+        # bits per realisation are a property of the schemes: every rank with work
+        # has them (collective on every rank, so a rank with an empty shard too)
+        have = np.array([0 if bits is None else 1], dtype=np.int64)
+        b = np.zeros((len(names), 2), dtype=np.int64) if bits is None else np.asarray(bits, dtype=np.int64)
+        b = allreduce_counts(b, dev)
+        have = allreduce_counts(have, dev)
+        bits = b // max(1, int(have[0]))
         import torch
         import torch.distributed as dist
         t = torch.tensor([extra["seconds"]], dtype=torch.float64)
@@ -95,7 +127,6 @@ def main(argv=None):
     extra["realisations_per_s"] = reps / extra["seconds"]
     res = results.make(S, names, counts, bits, reps, a.seed, extra=extra)
     if rank != 0:
-        eng.close()
         if world > 1:
             dist.destroy_process_group()
         return 0
@@ -110,10 +141,18 @@ def main(argv=None):
                    "ber_ic_mmse": float(res["ber"][s]["mmse"]["all"][k][-1]),
                    "ber_onetap_mmse": float(res["ber"][s]["mmse"]["all"][k][0])} for s in names}
     print(json.dumps(summary))
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _snr_subset(S, s0, ns):
+    """The setup namespace with SNR points [s0, s0 + ns) only (pn_time, snr_db)."""
+    import copy
+    T = copy.copy(S)
+    T.pn_time = np.asarray(S.pn_time)[s0:s0 + ns]
+    T.snr_db = np.asarray(S.snr_db)[s0:s0 + ns]
+    return T
 
 
 def _doubly_flat(a):

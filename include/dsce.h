@@ -290,8 +290,11 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  * dsce_build_mmse), wcontract_valu, mmse_ic (1: the MMSE IC iterations of an FFT-form
  * OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}
  * (k_mic_fft; equal to the W contraction of script:482-511 to rounding, checked
- * at dsce_build_mmse), 0: the W contraction everywhere).  Unknown names return
- * DSCE_EINVAL. */
+ * at dsce_build_mmse), 0: the W contraction everywhere), qidx, stage0_fft,
+ * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic (the OFDM fast-path pieces,
+ * 1 = on), snr_base (0..255: the noise of SNR index k is sub-stream
+ * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
+ * one-rank run's noise).  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);
 int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 

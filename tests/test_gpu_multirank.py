@@ -42,6 +42,30 @@ def test_simulate_two_ranks_equals_one(tmp_path):
         np.testing.assert_allclose(np.array(a["nmse"][s]), np.array(b["nmse"][s]), rtol=1e-12)
 
 
+def test_simulate_snr_shards_equal_one_rank(tmp_path):
+    """--shard snr: 2 ranks take 2 + 1 of 3 SNR points each with only its own
+    estimator (snr_base keys the noise by the sweep's SNR index); counters and
+    MSE sums equal the one-rank run exactly.  An odd realisation count
+    (64 x 5) is not padded to a multiple of 64 x world."""
+    args = ["--config", "default", "--schemes", "ofdm,fbmc_aux", "--reps", "320", "--batch", "128", "--mse"]
+    env = dict(os.environ, DSCE_DIST_BACKEND="gloo", PYTHONPATH=harness.PKG)
+    one, two, three = tmp_path / "one.json", tmp_path / "two.json", tmp_path / "three.json"
+    subprocess.run([sys.executable, "-m", "dsce.simulate", *args, "--out", str(one)], cwd=harness.PKG, env=env,
+                   check=True, timeout=240, capture_output=True)
+    for nproc, out, shard in ((2, two, "snr"), (3, three, "reps")):
+        subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "dsce.simulate", *args,
+                        "--shard", shard, "--out", str(out)], cwd=harness.PKG, env=env, check=True, timeout=300,
+                       capture_output=True)
+    a = json.load(open(one))
+    for f in (two, three):
+        b = json.load(open(f))
+        assert b["n_repetitions"] == a["n_repetitions"] == 320
+        assert np.array_equal(np.array(a["counts"]), np.array(b["counts"]))
+        for s in ("ofdm", "fbmc_aux"):
+            np.testing.assert_allclose(np.array(a["nmse"][s]), np.array(b["nmse"][s]), rtol=1e-12)
+
+
 def test_bench_gpus_flag_launches_ranks():
     """bench.py --gpus 2 without a launcher starts torch.distributed.run itself
     (one rank per GPU; here both ranks share the one GPU over gloo) and forwards
