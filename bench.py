@@ -234,7 +234,8 @@ def main():
     for kv in args.option:
         k, v = kv.split("=")
         options[k.strip()] = int(v)
-    S = build_setup(setup_name, schemes=schemes)
+    from dsce.engine import gpu_tx
+    S = build_setup(setup_name, schemes=schemes, tx=gpu_tx(device))       # G / Q produced on the GPU (row f1)
     t_setup = time.perf_counter()
     eng = build_engine(S, device=device, batch=batch, options=options)
     setup_s = time.perf_counter() - t_setup

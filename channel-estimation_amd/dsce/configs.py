@@ -95,8 +95,18 @@ ALIASES = {"ofdm24x14": "default", "c2": "default", "c3": "default", "c4": "defa
            "default": "default"}
 
 
-def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db=None, n_iter=4):
+def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db=None, n_iter=4, tx=None):
+    """The script's setup (script:16-205).  ``tx``: optional producer of
+    (G, Q = GetRXMatrix') for a modulation object, e.g. dsce.engine.gpu_tx
+    (dsce_tx_matrices, row f1: G and Q in closed form on the GPU instead of
+    L K Modulation() calls); default: the host mirror's GetTXMatrix /
+    GetRXMatrix."""
     cfg = _CONFIGS[ALIASES[name]]
+
+    def txrx(mod):
+        if tx is not None:
+            return tx(mod)
+        return mod.GetTXMatrix(), mod.GetRXMatrix().conj().T
     L = cfg["L"]
     F = 15e3
     SR = F * cfg["SRmul"]
@@ -153,9 +163,8 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
     out = {}
     need_fbmc = any(s.startswith("fbmc") for s in schemes)
     if need_fbmc:
+        G_fbmc, Q_fbmc = txrx(fbmc)                            # script:191-192
         Dfbmc = fbmc.GetFBMCMatrix()
-        G_fbmc = fbmc.GetTXMatrix()
-        Q_fbmc = fbmc.GetRXMatrix().conj().T                   # script:192
     if "fbmc_aux" in schemes:
         aux = IIC("Auxiliary", aux_pm, Dfbmc, 28, p2d_aux)     # script:116-122
         kappa = aux.PilotToDataPowerOffset * aux.DataPowerReduction
@@ -187,8 +196,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
             kappa=float(kappa), dpr=cod.DataPowerReduction, const=pam, considered_symbols=cm,
             n_pilots=NP, n_data=nd, bits_slot=1, pilot_slot=0, extras=dict(iic=cod, pilot_matrix=pm_fbmc, modulation=fbmc))
     if "ofdm" in schemes:
-        G_ofdm = ofdm.GetTXMatrix()
-        Q_ofdm = ofdm.GetRXMatrix().conj().T                   # script:195
+        G_ofdm, Q_ofdm = txrx(ofdm)                            # script:194-195
         pmv = _col(pm_ofdm)
         PMap = np.zeros((LK_ofdm, LK_ofdm))                    # script:134-137
         PMap[np.ix_(pmv == 1, np.arange(NP))] = np.sqrt(p2d) * np.eye(NP)

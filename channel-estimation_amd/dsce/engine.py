@@ -392,6 +392,18 @@ class Engine:
         return cm.value, wb.value
 
 
+def gpu_tx(device=0):
+    """Producer of (G, Q) for build_setup(tx=...): dsce_tx_matrices on `device`
+    (row f1, OFDM.m:184-218 / FBMC.m:318-354 in closed form per element)."""
+    def produce(mod):
+        eng = Engine(device)
+        try:
+            return eng.tx_matrices(mod)
+        finally:
+            eng.close()
+    return produce
+
+
 def build_engine(setup, schemes=None, device=0, zero_threshold=None, batch=None, options=None):
     """Engine configured like the script: channel, SNR list, schemes, MMSE setup.
     ``options``: dsce_set_option name -> value, applied before the MMSE build."""

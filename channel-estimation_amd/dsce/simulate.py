@@ -59,7 +59,8 @@ def main(argv=None):
         torch.cuda.set_device(device)
         dist.init_process_group(os.environ.get("DSCE_DIST_BACKEND", "nccl"))
     names = tuple(a.schemes.split(","))
-    S = build_setup(a.config, schemes=names)
+    from dsce.engine import gpu_tx
+    S = build_setup(a.config, schemes=names, tx=gpu_tx(device))      # G / Q on the GPU (row f1)
     reps = a.reps if a.reps is not None else S.n_repetitions
     reps = max(64, (reps + 63) // 64 * 64)          # one wavefront of realisations per step
     nsnr = len(S.snr_db)

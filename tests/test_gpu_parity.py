@@ -327,3 +327,21 @@ def test_tx_matrices_on_gpu_match_host_mirror(name):
         if key == "ofdm":
             np.testing.assert_allclose(G, O.schemes["ofdm"]["G"], rtol=0, atol=1e-13 * scale)
     eng.close()
+
+
+def test_setup_with_gpu_tx_matrices_gives_the_same_counts():
+    """Row f1 wired into the setup: build_setup(tx=gpu_tx()) takes G and Q from
+    dsce_tx_matrices; the engine built from it counts exactly like the one
+    built from the host mirror's G / Q (C2 OFDM and FBMC auxiliary, 256
+    realisations, 2 SNR points)."""
+    from dsce.configs import build_setup
+    from dsce.engine import build_engine, gpu_tx
+    for sc in ("ofdm", "fbmc_aux"):
+        a = build_setup("default", schemes=(sc,), snr_db=[15.0, 35.0])
+        b = build_setup("default", schemes=(sc,), snr_db=[15.0, 35.0], tx=gpu_tx())
+        np.testing.assert_allclose(b.schemes[sc].G, a.schemes[sc].G, rtol=0, atol=1e-13 * np.abs(a.schemes[sc].G).max())
+        ea, eb = build_engine(a, batch=256), build_engine(b, batch=256)
+        np.testing.assert_array_equal(ea.run(SEED, 0, 256), eb.run(SEED, 0, 256))
+        ea.close()
+        eb.close()
+
