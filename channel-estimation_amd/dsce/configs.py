@@ -226,7 +226,7 @@ def build_setup(name="default", schemes=("fbmc_aux", "fbmc_cod", "ofdm"), snr_db
 # SimpleVersion_DoublyFlat.m (BASELINE config 1): doubly-flat channel, pilot
 # interpolation instead of the MMSE estimator, no interference cancellation.
 # ---------------------------------------------------------------------------
-def build_doubly_flat_setup(qam_order=16, snr_db=None, n_repetitions=1000):
+def build_doubly_flat_setup(qam_order=16, snr_db=None, n_repetitions=1000, interpolation="linear", block=None):
     """Setup of ``SimpleVersion_DoublyFlat.m`` (:12-82).
 
     Schemes 'fbmc_aux', 'fbmc_cod', 'ofdm' with their interpolation weights
@@ -237,6 +237,11 @@ def build_doubly_flat_setup(qam_order=16, snr_db=None, n_repetitions=1000):
     h = sqrt(1/2) (randn + j randn) (:123).  The script draws everything —
     bits, pilots, h, noise — inside its SNR loop (:90-126); the engine runs one
     SNR point per call with the key ``snr_seed(seed, k)`` (dsce.doubly_flat).
+    ``interpolation`` selects the PSACE method (the script uses 'linear';
+    'nearest', 'natural', 'FullAverage' and 'MovingBlockAverage' with ``block``
+    = [BlockLengthFrequency, BlockLengthTime] are the class's other methods,
+    PSACE.m:73-99): all are linear in the LS estimates, so each crosses the ABI
+    as one weight matrix.
     """
     from .estimation import PilotSymbolAidedChannelEstimation as PSACE
     L = 12
@@ -250,8 +255,8 @@ def build_doubly_flat_setup(qam_order=16, snr_db=None, n_repetitions=1000):
         raise ValueError("Total number of samples must be the same for OFDM and FBMC.")
     pam = SignalConstellation(int(np.sqrt(qam_order)), "PAM")                       # :43-44
     qam = SignalConstellation(qam_order, "QAM")
-    ce_ofdm = PSACE("Diamond", [[ofdm.Nr.Subcarriers, 6], [ofdm.Nr.MCSymbols, 4]], "linear")   # :47-56
-    ce_fbmc = PSACE("Diamond", [[fbmc.Nr.Subcarriers, 6], [fbmc.Nr.MCSymbols, 8]], "linear")   # :57-66
+    ce_ofdm = PSACE("Diamond", [[ofdm.Nr.Subcarriers, 6], [ofdm.Nr.MCSymbols, 4]], interpolation, block)   # :47-56
+    ce_fbmc = PSACE("Diamond", [[fbmc.Nr.Subcarriers, 6], [fbmc.Nr.MCSymbols, 8]], interpolation, block)   # :57-66
     Dfbmc = fbmc.GetFBMCMatrix()
     aux_pm = ce_fbmc.GetAuxiliaryMatrix(1)
     aux = IIC("Auxiliary", aux_pm, Dfbmc, 16, 2)                                      # :69-75

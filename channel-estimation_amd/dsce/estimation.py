@@ -193,6 +193,78 @@ class ImaginaryInterferenceCancellationAtPilotPosition:
         self.ConsideredInterferenceMatrix = ci
 
 
+def _clip_halfplane(poly, a, b):
+    """Sutherland-Hodgman: the part of the convex polygon ``poly`` (k x 2) with
+    a . p <= b."""
+    out = []
+    n = len(poly)
+    for k in range(n):
+        p, q = poly[k], poly[(k + 1) % n]
+        fp, fq = a @ p - b, a @ q - b
+        if fp <= 0.0:
+            out.append(p)
+        if fp * fq < 0.0:
+            out.append(p + (q - p) * (fp / (fp - fq)))
+    return np.array(out) if out else np.zeros((0, 2))
+
+
+def _area(poly):
+    if len(poly) < 3:
+        return 0.0
+    x, y = poly[:, 0], poly[:, 1]
+    return 0.5 * abs(np.dot(x, np.roll(y, -1)) - np.dot(y, np.roll(x, -1)))
+
+
+def _sibson(pts, x):
+    """Sibson natural-neighbour coordinates of the point ``x`` w.r.t. the sites
+    ``pts`` (scatteredInterpolant 'natural', PSACE.m:74-76, :118-121): the area
+    x's Voronoi cell would take from each site's cell if x were inserted, over
+    the cell's area.  x's cell is the polygon of the circumcentres of the
+    Delaunay triangles incident to x; the part taken from site i is that
+    polygon clipped to the half-planes closer to s_i than to every other
+    natural neighbour s_j (the second-nearest site of any point of x's cell is
+    a natural neighbour of x).  Returns None when x coincides with a site or
+    its cell is unbounded (x on the hull boundary): the caller uses the linear
+    weights there, which are Sibson's limit."""
+    from scipy.spatial import Delaunay
+    NP = pts.shape[0]
+    d2 = np.sum((pts - x) ** 2, axis=1)
+    if d2.min() < 1e-20:
+        w = np.zeros(NP)
+        w[int(np.argmin(d2))] = 1.0
+        return w
+    tri = Delaunay(np.vstack([pts, x[None, :]]))
+    inc = [s for s in tri.simplices if NP in s]
+    nbr = sorted({int(v) for s in inc for v in s if v != NP})
+    # x's cell is bounded only if x is interior: every incident triangle's edge
+    # opposite... equivalently x is not on the convex hull of the new point set
+    if NP in set(tri.convex_hull.ravel().tolist()):
+        return None
+    cc = []
+    for s in inc:
+        A = np.vstack([pts[v] if v < NP else x for v in s])
+        # circumcentre: solve 2 (b - a) . c = |b|^2 - |a|^2 for the two edges
+        M = 2.0 * (A[1:] - A[0])
+        rhs = np.sum(A[1:] ** 2, axis=1) - np.sum(A[0] ** 2)
+        cc.append(np.linalg.solve(M, rhs))
+    cc = np.array(cc)
+    ang = np.arctan2(cc[:, 1] - x[1], cc[:, 0] - x[0])
+    cell = cc[np.argsort(ang)]
+    w = np.zeros(NP)
+    for i in nbr:
+        poly = cell
+        for j in nbr:
+            if j == i or len(poly) == 0:
+                continue
+            # |p - s_i|^2 <= |p - s_j|^2  <=>  2 (s_j - s_i) . p <= |s_j|^2 - |s_i|^2
+            poly = _clip_halfplane(poly, 2.0 * (pts[j] - pts[i]), pts[j] @ pts[j] - pts[i] @ pts[i])
+        w[i] = _area(poly)
+    tot = w.sum()
+    if not tot > 0.0:
+        return None
+    return w / tot
+
+
 class PilotSymbolAidedChannelEstimation:
     """``(PilotPattern, Parameters, InterpolationMethod[, Block])`` (PSACE.m:33-112).
 
@@ -288,10 +360,8 @@ class PilotSymbolAidedChannelEstimation:
             return np.ones(self.PilotMatrix.shape) * np.mean(LS)
         if m == "MovingBlockAverage":
             return (self.InterpolationMatrix @ LS).reshape(self.PilotMatrix.shape, order="F")
-        if m in ("linear", "nearest"):
+        if m in ("linear", "nearest", "natural"):
             return (self._scattered_weights(m) @ LS).reshape(self.PilotMatrix.shape, order="F")
-        if m == "natural":
-            raise NotImplementedError("natural-neighbour interpolation is not provided")
         if m == "MMSE":
             if self._mmse is None:
                 raise RuntimeError("MMSE interpolation needs an engine: call set_mmse_engine()")
@@ -304,7 +374,11 @@ class PilotSymbolAidedChannelEstimation:
         the Delaunay triangulation of the pilot positions; outside the convex
         hull the affine function of the boundary triangle nearest to the query
         point (MATLAB's default linear extrapolation; exact for affine fields).
-        'nearest': the closest pilot (its default extrapolation too)."""
+        'nearest': the closest pilot (its default extrapolation too).
+        'natural': Sibson natural-neighbour coordinates inside the convex hull
+        (``_sibson``), the 'linear' weights on the hull boundary (the limit of
+        Sibson's coordinates there) and outside it (scatteredInterpolant's
+        default ExtrapolationMethod for 'natural' is 'linear')."""
         key = "_w_" + method
         if getattr(self, key, None) is not None:
             return getattr(self, key)
@@ -333,6 +407,11 @@ class PilotSymbolAidedChannelEstimation:
                         hull_edges.append((e[0], e[1], si))
             for i, xy in enumerate(q):
                 si = simp[i]
+                if method == "natural" and si >= 0:
+                    w = _sibson(pts, xy)
+                    if w is not None:
+                        Wt[i] = w
+                        continue
                 if si < 0:
                     best, bd = None, np.inf
                     for a, b, s_ in hull_edges:
@@ -364,7 +443,7 @@ class PilotSymbolAidedChannelEstimation:
             return np.full((LK, NP), 1.0 / NP)
         if m == "MovingBlockAverage":
             return self.InterpolationMatrix.copy()
-        if m in ("linear", "nearest"):
+        if m in ("linear", "nearest", "natural"):
             return self._scattered_weights(m).copy()
         raise ValueError("no fixed interpolation weights for method %r" % m)
 

@@ -35,6 +35,9 @@ def main(argv=None):
     ap.add_argument("--npz", action="store_true")
     ap.add_argument("--figures", default=None, help="directory for Figure2-5.png")
     ap.add_argument("--mse", action="store_true", help="also accumulate the channel-estimation NMSE per stage")
+    ap.add_argument("--interpolation", default="linear",
+                    choices=("linear", "nearest", "natural", "FullAverage"),
+                    help="doubly_flat: PSACE interpolation method (the script uses 'linear')")
     ap.add_argument("--shard", choices=("reps", "snr"), default="reps",
                     help="multi-rank split: realisation slices (default) or SNR points")
     a = ap.parse_args(argv)
@@ -161,8 +164,9 @@ def _doubly_flat(a):
     from dsce import results
     from dsce.doubly_flat import DoublyFlatSim
 
+    from dsce.configs import build_doubly_flat_setup
     t0 = time.perf_counter()
-    sim = DoublyFlatSim(batch=a.batch)
+    sim = DoublyFlatSim(build_doubly_flat_setup(interpolation=a.interpolation), batch=a.batch)
     setup_s = time.perf_counter() - t0
     S = sim.setup
     reps = a.reps if a.reps is not None else S.n_repetitions

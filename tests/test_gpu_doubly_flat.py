@@ -107,6 +107,28 @@ def test_doubly_flat_counts_match_oracle(flat):
     assert got.sum() > 1000
 
 
+@pytest.mark.parametrize("method", ["natural", "nearest"])
+def test_doubly_flat_other_interpolations_match_oracle(method):
+    """PSACE's other scatteredInterpolant methods (PSACE.m:74-76) on the same
+    kernels: counts identical to the oracle with the same weights, 64
+    realisations x 7 SNR points, all three schemes."""
+    from dsce.configs import build_doubly_flat_setup
+    from dsce.doubly_flat import DoublyFlatSim
+    sim = DoublyFlatSim(build_doubly_flat_setup(interpolation=method), batch=64)
+    try:
+        S = sim.setup
+        got = sim.run(SEED, 0, 64)
+        ref = refsim.simulate_doubly_flat(SEED, 0, 64, S.N, _oracle_schemes(S), S.pn_time)
+        diff = np.abs(got - ref["err"]).sum(axis=(1, 2))
+        assert np.all(diff <= 8 * ref["borderline"]), (got, ref["err"])
+        ls = np.random.default_rng(2).standard_normal(S.schemes["ofdm"].n_pilots) + 0j
+        g = sim.engine.mmse_onetap(sim.sid["ofdm"], 0, ls)
+        np.testing.assert_allclose(g, S.schemes["ofdm"].extras["psace"].ChannelInterpolation(ls).reshape(-1, order="F"),
+                                   rtol=0, atol=1e-13)
+    finally:
+        sim.close()
+
+
 def test_doubly_flat_interpolation_onetap_matches_psace(flat):
     """dsce_mmse_onetap on an interpolation scheme = PSACE.ChannelInterpolation."""
     S = flat.setup

@@ -138,6 +138,52 @@ def test_psace_linear_weights_match_scipy_inside_hull():
     assert np.allclose(got.reshape(-1, order="F"), W @ v)
 
 
+def test_psace_natural_neighbour_weights():
+    """PSACE 'natural' (PSACE.m:74-76, :118-121; scatteredInterpolant 'natural'
+    = Sibson coordinates, 'linear' extrapolation).  Checked by properties that
+    do not depend on the construction: rows sum to one, non-negative inside the
+    hull, affine fields reproduced everywhere (Sibson's linear precision), LS
+    values reproduced at the pilots, smooth weights that differ from 'linear';
+    and at interior points against a brute-force raster of the definition (the
+    share of x's Voronoi cell that each pilot's cell would lose)."""
+    from dsce.estimation import PilotSymbolAidedChannelEstimation as PSACE
+    from dsce.estimation import _sibson
+    parity = "parity unpinned: MATLAB's scatteredInterpolant is absent; property + definition checks"
+    for pattern, params in (("Diamond", [[12, 4], [15, 4]]), ("Rectangular", [[24, 6], [14, 7]]),
+                            ("Diamond", [[12, 6], [30, 8]])):
+        ce = PSACE(pattern, params, "natural")
+        W = ce.GetInterpolationWeights()
+        PM = ce.PilotMatrix
+        nL, nK = PM.shape
+        assert W.shape == (nL * nK, ce.NrPilotSymbols)
+        np.testing.assert_allclose(W.sum(axis=1), 1.0, rtol=0, atol=1e-12, err_msg=parity)
+        f, t = np.meshgrid(np.arange(1, nL + 1), np.arange(1, nK + 1), indexing="ij")
+        H = (0.3 - 0.2j) + (0.05 + 0.01j) * f - (0.02 - 0.03j) * t
+        ls = H.reshape(-1, order="F")[PM.reshape(-1, order="F") == 1]
+        np.testing.assert_allclose(ce.ChannelInterpolation(ls), H, rtol=0, atol=1e-12)
+        lin = PSACE(pattern, params, "linear").GetInterpolationWeights()
+        assert np.abs(W - lin).max() > 1e-3            # not the linear weights
+        piv = PM.reshape(-1, order="F") == 1
+        np.testing.assert_allclose(W[piv], np.eye(ce.NrPilotSymbols), atol=1e-12)
+    # the definition, by raster, at interior points off the lattice symmetry
+    ce = PSACE("Diamond", [[12, 6], [30, 8]], "natural")
+    rows, cols = np.nonzero(ce.PilotMatrix.T)
+    pts = np.stack([cols + 1.0, rows + 1.0], axis=1)
+    h = 0.01
+    for x in (np.array([6.3, 14.7]), np.array([5.0, 17.0]), np.array([8.2, 11.1])):
+        w = _sibson(pts, x)
+        assert w is not None and (w >= -1e-15).all()
+        g = np.arange(-7.0, 7.0, h) + h / 2
+        px, py = np.meshgrid(x[0] + g, x[1] + g, indexing="ij")
+        P = np.stack([px.ravel(), py.ravel()], axis=1)
+        d = ((P[:, None, :] - pts[None, :, :]) ** 2).sum(-1)
+        near = d.argmin(axis=1)
+        mine = ((P - x) ** 2).sum(-1) < d.min(axis=1)
+        est = np.bincount(near[mine], minlength=pts.shape[0]) / mine.sum()
+        assert np.abs(est - w).max() < 0.01, (x, np.abs(est - w).max())
+        np.testing.assert_allclose(w @ pts, x, atol=1e-12)
+
+
 def test_doubly_flat_setup_matches_script():
     """SimpleVersion_DoublyFlat.m:16-82: sizes, pilots, kappa, noise slots."""
     from dsce.configs import build_doubly_flat_setup
