@@ -1589,48 +1589,65 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
     __shared__ double2 twb[2][4];                               // quad-network twiddle of lane r
     __shared__ int cntl[4][PM_MAXIT];
+    // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
+    // and the channel taps of the lane's samples (registers for all iterations)
+    double2 u[6], yh[6], hc[6];
+    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
+    double2 taps[6][NT];
+    const __amdgpu_buffer_rsrc_t trs =
+        buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo)) * R * sizeof(double2));
+    const unsigned tv0 = (unsigned)(6 * cq * R + rl) * 16u;
     {
-        // every global load of the prologue before the first LDS write (clamped)
+        // table loads, then the per-unit loads (raw y and h into yh / hc), then
+        // the LDS writes: the writes wait only for the tables (vmcnt retires in
+        // order), the per-unit data arrives during the barrier
         const double2 a = o.symbols[min(tid, o.M - 1)];
         const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
         const int rt = min(tid, 23);
         const double2 pv = o.row_pval[row0 + rt];
         const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
-        const int e = ((tid / 6) % 4) * (tid % 6);              // twa: w24^(r m')
+        const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);   // twa: w24^(r m')
         const double2 tw = kW24[e % 12];
         const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+#pragma unroll
+        for (int b = 0; b < 6; ++b) {
+            const int row = row0 + 4 * b + r;
+            if (QIDX) qv[b] = o.qd[(size_t)row * U + unit];
+            else u[b] = o.u[(size_t)row * U + unit];
+            txp[b >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (b & 3));
+            yh[b] = o.y[(size_t)row * U + unit];
+            hc[b] = o.h[(size_t)row * R + rl];
+        }
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+#pragma unroll
+            for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
         sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
         sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
-        if (tid < 24) {
-            rpv[tid] = pv;
-            rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;  // data index << 1 | no-edge, or -1
-        }
-        if (tid < 48) {
+        // unconditional (clamped) table writes: a write under `if (tid < 24)`
+        // lets the compiler sink the table loads into the branch, behind a
+        // vmcnt(0) that also waits for every per-unit load
+        rpv[rt] = pv;
+        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;     // data index << 1 | no-edge, or -1
+        {
             // IFFT w24^(r m'); FFT qs gs w24^-(r m') (the output scale of Q' H G)
-            const int dir = tid / 24;
+            const int tc = min(tid, 47), dir = tc / 24;
             const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        } else if (tid < 56) {
+            twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+        }
+        if (tid >= 48 && tid < 56) {
             const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
             twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
         }
     }
-    // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows
-    double2 u[6], yh[6], hc[6];
-    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
+    __syncthreads();
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-        const int row = row0 + 4 * a + r;
-        if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
-        else u[a] = o.u[(size_t)row * U + unit];
-        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        const double2 yv = o.y[(size_t)row * U + unit];
-        const double2 hh = o.h[(size_t)row * R + rl];
+        const double2 hh = hc[a], yv = yh[a];
         const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
         hc[a] = make_double2(hh.x * id, -hh.y * id);            // 1 / h
         yh[a] = c_mulf(yv, hc[a]);                               // y / h
     }
-    __syncthreads();
     // data / no-edge masks of the lane's rows
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
@@ -1645,15 +1662,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
                               (size_t)(row0 + 4 * a + r) * R + rl);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
-    const __amdgpu_buffer_rsrc_t trs =
-        buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo)) * R * sizeof(double2));
-    const unsigned tv0 = (unsigned)(6 * cq * R + rl) * 16u;
-    // the channel taps of the lane's samples, iteration-invariant: registers
-    double2 taps[6][NT];
-#pragma unroll
-    for (int m = 0; m < 6; ++m)
-#pragma unroll
-        for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
     int ncnt = 0;
     for (int it = 1; it <= niter; ++it) {
         // an opaque zero keeps the per-iteration LDS twiddle reads inside the loop
@@ -1837,58 +1845,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     __shared__ double2 wrow[24];                                // qs gs w^(-l): diag(D_hat) weight of a delayed tap
     __shared__ double2 twa[2][4][6];
     __shared__ double2 twb[2][4];
-    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    {
-        // every global load of the prologue before the first LDS write (clamped)
-        const double2 a = o.symbols[min(tid, o.M - 1)];
-        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
-        const int rt = min(tid, 23);
-        const double2 pv = o.row_pval[row0 + rt];
-        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
-        // the operator slices: Bv rows klo..klo+23 of every tap (NT x 24 x NP,
-        // contiguous per tap) and Bs of the block
-        constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
-        const double2* __restrict__ bvb = ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo) * NP;
-        double2 bvr[PER];
-        if (!yic)
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
-                bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
-            }
-        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
-        const int e = ((tid / 6) % 4) * (tid % 6);
-        const double2 tw = kW24[e % 12];
-        sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
-        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
-        if (tid < 24) {
-            rpv[tid] = pv;
-            rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
-        }
-        if (!yic)
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int i = tid + 256 * k;
-                if (i < NBV) sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
-            }
-        if (tid < NT * NP) sbs[tid / NP][tid % NP] = bsv;
-        if (tid < 48) {
-            const int dir = tid / 24;
-            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        } else if (tid < 56) {
-            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
-            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
-        } else if (tid >= 64 && tid < 88) {
-            const int lr = tid - 64;
-            const double2 t0 = kW24[lr % 12];
-            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            wrow[lr] = c_mul(scale, make_double2(wl.x, -wl.y));
-        }
-    }
-    // per-unit operands, all requested before the barrier: the rows' v and y,
-    // the previous stage's pilots (all NP, shared by the quad) and a quarter of
-    // this stage's (lane r: pilots 4r..4r+3 of the window sums)
+    // per-unit operands (the rows' v and y, the previous stage's pilots, all NP,
+    // shared by the quad, and a quarter of this stage's: lane r holds pilots
+    // 4r..4r+3 of the window sums), requested after the table / operator loads
+    // and before the first LDS write: the LDS writes then wait only for the
+    // tables (vmcnt retires in order; the flat pointers keep the compiler from
+    // moving these loads above the LDS stores itself)
     double2 u[6], yv[6], hq[TAPM ? 1 : NP], hn4[NP / 4];
     unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
     // TAPM: the taps as an MFMA GEMM, A = Bv rows (tap row R = q 24 + j, 16 per
@@ -1896,31 +1858,78 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // products; lane (g = l >> 4, jc = l & 15) holds B[4 ks + g][unit jc]
     constexpr int NTILE = (NT * 24 + 15) / 16, NKS = NP / 4;
     double br[TAPM ? NKS : 1], bi[TAPM ? NKS : 1], bsm[TAPM ? NKS : 1];
-    if (TAPM && !yic) {
+    double2 hb[TAPM ? NKS : 1];
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    {
+        // every global load of the prologue before the first LDS write (clamped)
+        const double2 sa = o.symbols[min(tid, o.M - 1)];
+        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int rt = min(tid, 23);
+        const double2 pv = o.row_pval[row0 + rt];
+        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        // twiddles (a lane-varying index into the constant table is a vector
+        // load: issued here, with the tables, not behind the per-unit loads)
+        const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);
+        const double2 tw = kW24[e % 12];
+        const int lr0 = min(max(tid - 64, 0), 23);
+        const double2 t0 = kW24[lr0 % 12];
+        // the operator slices: Bv rows klo..klo+23 of every tap (NT x 24 x NP,
+        // contiguous per tap) and Bs of the block (loaded unconditionally: a
+        // branch around the array loads sent it through scratch)
+        constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
+        const double2* __restrict__ bvb = ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo) * NP;
+        double2 bvr[PER];
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const double2 hv = ma.hp_prev[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
-            br[ks] = hv.x;
-            bi[ks] = hv.y;
-            bsm[ks] = hv.x + hv.y;
+            for (int k = 0; k < PER; ++k) {
+                const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
+                bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
+            }
+        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
+        if (TAPM && !yic) {
+    #pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+                hb[ks] = ma.hp_prev[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
+            }
+        }
+    #pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            if (!yic) {
+                if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
+                else u[a] = ma.v[(size_t)row * U + unit];
+            }
+        }
+        if (!TAPM && !yic)
+    #pragma unroll
+            for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
+        if (!PILOT)
+    #pragma unroll
+            for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
+        sym[tid] = make_double2(tid < o.M ? sa.x : 0.0, tid < o.M ? sa.y : 0.0);
+        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
+        rpv[rt] = pv;                                           // unconditional, clamped (see k_pic_fft)
+        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+        // unconditional (yic blocks do not read sbv): under `if (!yic)` the
+        // compiler sinks the bvr loads next to these writes, behind a vmcnt(0)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = min(tid + 256 * k, NBV - 1);
+            sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
+        }
+        {
+            const int ib = min(tid, NT * NP - 1);
+            sbs[ib / NP][ib % NP] = bsv;
+            const int tc = min(tid, 47), dir = tc / 24;
+            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+            twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+            const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            wrow[lr0] = c_mul(scale, make_double2(wl.x, -wl.y));
+        }
+        if (tid >= 48 && tid < 56) {
+            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
+            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
         }
     }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int row = row0 + 4 * a + r;
-        if (!yic) {
-            if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
-            else u[a] = ma.v[(size_t)row * U + unit];
-        }
-        if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        yv[a] = (yic ? ma.yest : o.y)[(size_t)row * U + unit];   // yic: y_ic itself
-    }
-    if (!TAPM && !yic)
-#pragma unroll
-        for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
-    if (!PILOT)
-#pragma unroll
-        for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
     // data / no-edge masks of the lane's rows
     unsigned dmask = 0u, emask = 0u;
@@ -1941,6 +1950,12 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // each lane forms its 12 taps on the VALU (Bv rows broadcast from LDS)
     __shared__ double2 hhs[TAPM ? 4 : 1][TAPM ? NTILE * 16 : 1][17];
     if (TAPM && !yic) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            br[ks] = hb[ks].x;
+            bi[ks] = hb[ks].y;
+            bsm[ks] = hb[ks].x + hb[ks].y;
+        }
         const int g = l >> 4, jc = l & 15;
         const int R = jc;                                   // A row of this lane within a tile
 #pragma unroll
@@ -1961,7 +1976,19 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             for (int reg = 0; reg < 4; ++reg)
                 hhs[w][16 * t + g + 4 * reg][jc] = make_double2(p1[reg] - p2[reg], p3[reg] - p1[reg] - p2[reg]);
         }
-        __syncthreads();
+        // the slab is the wave's own: a wave-level fence, no block barrier
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    // y (or y_ic) and the transmitted indices are first needed in the epilogue:
+    // requested here, their latency runs under the tap assembly and the DFT
+    // chain (in the prologue they held 26 more registers at its peak)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int row = row0 + 4 * a + r;
+        if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
+        yv[a] = (yic ? ma.yest : o.y)[(size_t)row * U + unit];   // yic: y_ic itself
     }
     double2 taps[6][NT];
     double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
@@ -2160,32 +2187,35 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
     __shared__ int rdc[24];
     __shared__ double2 wrow[24];
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    double2 yv[6], hv[6], hn4[NP / 4];
+    unsigned txp[2] = {0u, 0u};
     {
+        // table loads, then the per-unit loads, then the LDS writes: the writes
+        // wait only for the tables (vmcnt retires in order)
         const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
         const int rt = min(tid, 23);
         const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
         const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
+        const int lr0 = min(max(tid - 64, 0), 23);
+        const double2 t0 = kW24[lr0 % 12];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            yv[a] = o.y[(size_t)row * U + unit];
+            hv[a] = o.h[(size_t)row * R + rl];
+            txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
+        }
+#pragma unroll
+        for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
         sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
-        if (tid < 24) rdc[tid] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
-        if (tid < NT * NP) sbs[tid / NP][tid % NP] = bsv;
-        if (tid >= 64 && tid < 88) {
-            const int lr = tid - 64;
-            const double2 t0 = kW24[lr % 12];
-            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            wrow[lr] = c_mul(scale, make_double2(wl.x, -wl.y));
+        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;     // unconditional, clamped (see k_pic_fft)
+        {
+            const int ib = min(tid, NT * NP - 1);
+            sbs[ib / NP][ib % NP] = bsv;
+            const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            wrow[lr0] = c_mul(scale, make_double2(wl.x, -wl.y));
         }
     }
-    double2 yv[6], hv[6], hn4[NP / 4];
-    unsigned txp[2] = {0u, 0u};
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int row = row0 + 4 * a + r;
-        yv[a] = o.y[(size_t)row * U + unit];
-        hv[a] = o.h[(size_t)row * R + rl];
-        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-    }
-#pragma unroll
-    for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
     __syncthreads();
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
