@@ -1859,6 +1859,11 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     constexpr int NTILE = (NT * 24 + 15) / 16, NKS = NP / 4;
     double br[TAPM ? NKS : 1], bi[TAPM ? NKS : 1], bsm[TAPM ? NKS : 1];
     double2 hb[TAPM ? NKS : 1];
+    // PILOT: pilot column of the lane's rows (prologue) and the transmitted
+    // pilot of each (requested with y, clamped, unconditional): the LS
+    // division in the epilogue then waits on no dependent load
+    int pcv[PILOT ? 6 : 1];
+    double2 xpv[PILOT ? 6 : 1];
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
     {
         // every global load of the prologue before the first LDS write (clamped)
@@ -1898,6 +1903,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
                 if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
                 else u[a] = ma.v[(size_t)row * U + unit];
             }
+            if (PILOT) pcv[a] = sk.row_pcol[row];
         }
         if (!TAPM && !yic)
     #pragma unroll
@@ -1989,6 +1995,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         const int row = row0 + 4 * a + r;
         if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
         yv[a] = (yic ? ma.yest : o.y)[(size_t)row * U + unit];   // yic: y_ic itself
+        if (PILOT) xpv[a] = o.xp[(size_t)min(max(pcv[a], 0), NP - 1) * R + rl];
     }
     double2 taps[6][NT];
     double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
@@ -2073,14 +2080,14 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const int row = row0 + 4 * a + r;
-            const int pc = sk.row_pcol[row];
+            const int pc = pcv[a];
             double2 ye = c_sub(yv[a], x[p6(a)]);
             double2 hpv = sp0;
             c_fma(hpv, wrow[4 * a + r], sp1);
             c_fma(ye, hpv, u[a]);
             if (ma.yic) ma.yest[(size_t)row * U + unit] = ye;
             if (pc >= 0 && pc < NP) {
-                const double2 q = c_div(ye, o.xp[(size_t)pc * R + rl]);
+                const double2 q = c_div(ye, xpv[a]);
                 ma.hp_out[(size_t)pc * U + unit] = make_double2(q.x / sqk, q.y / sqk);
             }
         }
@@ -2315,6 +2322,8 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
 // diag(D) band and the noisy Q^H band: s and r0 never reach memory.  Lane quad
 // = realisation (k_pic_fft's layout), block = 64 realisations x one symbol.
 // ---------------------------------------------------------------------------
+constexpr int TXRX_MAXSNR = 64;      // SNR points per k_txrx_fft launch (the launcher checks)
+
 struct TxrxArgs {
     const double2* __restrict__ xs;   // [LK][R] precoded symbols P [xP; xD]
     const double2* __restrict__ ir;   // [ntap][N][R]
@@ -2340,31 +2349,37 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     __shared__ double2 twa[2][4][6];
     __shared__ double2 twb[2][4];
     __shared__ double2 wrow[24];
+    __shared__ double ssc[TXRX_MAXSNR];                        // sqrt(Pn / 2) of the chunk's SNR points
     const double2 gs = sk.pf_gs, qs = sk.pf_qs, ps = sk.pf_scale;
-    {
-        const int e = ((tid / 6) % 4) * (tid % 6);
-        const double2 tw = kW24[e % 12];
-        if (tid < 48) {
-            const int dir = tid / 24;
-            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-            twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
-        } else if (tid < 56) {
-            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
-            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
-        } else if (tid >= 64 && tid < 88) {
-            const int lr = tid - 64;
-            const double2 t0 = kW24[lr % 12];
-            const double2 wl = lr >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            wrow[lr] = c_mul(ps, make_double2(wl.x, -wl.y));
-        }
-    }
     double2 x[6], taps[6][NT];
+    {
+        // table loads (twiddles, noise powers), then the per-unit loads, then
+        // the LDS writes (unconditional, clamped: a write under a branch lets
+        // the compiler sink its load there, behind a vmcnt(0))
+        const int tc = min(tid, 47);
+        const int e = ((tc / 6) % 4) * (tc % 6);
+        const double2 tw = kW24[e % 12];
+        const int lr0 = min(max(tid - 64, 0), 23);
+        const double2 t0 = kW24[lr0 % 12];
+        const int kc = min(tid, ta.nchunk - 1);
+        const double pnv = ta.pn[ta.snr0 + kc];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) x[a] = ta.xs[(size_t)(row0 + 4 * a + r) * R + rl];
+        for (int a = 0; a < 6; ++a) x[a] = ta.xs[(size_t)(row0 + 4 * a + r) * R + rl];
 #pragma unroll
-    for (int m = 0; m < 6; ++m)
+        for (int m = 0; m < 6; ++m)
 #pragma unroll
-        for (int q = 0; q < NT; ++q) taps[m][q] = ta.ir[((size_t)q * ta.N + klo + 6 * cq + m) * R + rl];
+            for (int q = 0; q < NT; ++q) taps[m][q] = ta.ir[((size_t)q * ta.N + klo + 6 * cq + m) * R + rl];
+        const int dir = tc / 24;
+        const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+        twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
+        if (tid >= 48 && tid < 56) {
+            const int dr = (tid - 48) / 4, rr = (tid - 48) % 4;
+            twb[dr][rr] = rr == 3 ? make_double2(0.0, dr ? -1.0 : 1.0) : make_double2(1.0, 0.0);
+        }
+        const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+        wrow[lr0] = c_mul(ps, make_double2(wl.x, -wl.y));
+        ssc[kc] = sqrt(pnv / 2.0);
+    }
     __syncthreads();
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     // perfect-CSI diag(D) of the symbol's rows from the window sums of the taps
@@ -2417,7 +2432,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     // per SNR point: r = r0 + noise (LoadNoisy's draws), y = qs DFT24(r)
     for (int k = 0; k < ta.nchunk; ++k) {
         const int snr = ta.snr0 + k;
-        const double sc = sqrt(ta.pn[snr] / 2.0);
+        const double sc = ssc[k];
         double2 f[6];
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
@@ -2514,7 +2529,7 @@ static int pic_fft_shift(const ChannelK& ch) {
 // every sample of the scheme's frame read by exactly one Q^H block
 bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
     return op.txrx_fft && op.noise_fuse && sk.pf_ok && sk.qh_disjoint && pic_fft_shift(ch) >= 0 &&
-           (b.R % WAVE) == 0 && (long long)ch.ntap * ch.N * b.R < (1ll << 40);
+           (b.R % WAVE) == 0 && b.U / b.R <= TXRX_MAXSNR && (long long)ch.ntap * ch.N * b.R < (1ll << 40);
 }
 
 static unsigned launch_txrx(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
