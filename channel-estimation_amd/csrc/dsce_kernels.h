@@ -127,7 +127,7 @@ struct MmseK {
 // some scheme reads (the channel taps are used at output samples only there:
 // r0 = H s, diag(D) and the perfect-CSI passes / chains all go through Q^H).
 struct JakesChunks {
-    static constexpr int LEN = 12;   // samples per chunk
+    static constexpr int LEN = 24;   // samples per chunk
     const int* n0 = nullptr;         // device: first sample of each chunk
     int n = 0;
 };

@@ -203,7 +203,9 @@ static constexpr int JCH_MAX = 16;
 // realisations of 32 chunks of 17 samples keep every lane busy with twice the
 // chunk length of one realisation per wave (the per-chunk cis is amortised over
 // 17 samples instead of 9).
-template <int JCH, int RPW>
+// PS lanes per chunk split the paths (PS = 2: lane pair, sums joined by a lane
+// exchange): long chunks amortise the per-chunk cis without idling lanes.
+template <int JCH, int RPW, int PS = 1>
 __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
                                                double2* __restrict__ ir, const int* __restrict__ chunk_n0, int nchunk) {
     extern __shared__ double sm[];
@@ -235,7 +237,7 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
     __syncthreads();
     // chunk_n0: the first samples of the chunks to form (the samples some Q^H
     // row reads, JakesChunks); otherwise all N samples in consecutive chunks
-    const int ck = blockIdx.x * LPR + sl;
+    const int ck = blockIdx.x * (LPR / PS) + sl / PS, par = sl % PS;
     if (chunk_n0 && ck >= nchunk) return;
     const int n0 = chunk_n0 ? chunk_n0[ck] : ck * JCH;
     if (n0 >= ch.N) return;
@@ -246,32 +248,41 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
     // Per path and chunk: one exact cis at the chunk start, one rotation for the
     // second sample, then the three-term recurrence z[i+1] = 2 cos(theta) z[i] -
     // z[i-1] (two FMAs per sample instead of a complex rotation's four; its
-    // rounding error grows at most like i^2 eps, ~1e-14 at 16 samples).  Two
-    // paths per step: independent chains interleave (ILP).
-    int p = 0;
-    for (; p + 1 < P; p += 2) {
-        double2 a0 = cis_turns(ph[p] + ds[p] * t0);
-        double2 a1 = cis_turns(ph[p + 1] + ds[p + 1] * t0);
-        const double2 w0 = make_double2(wr[p], wi[p]), w1 = make_double2(wr[p + 1], wi[p + 1]);
-        const double c0 = 2.0 * wr[p], c1 = 2.0 * wr[p + 1];
-        double2 b0 = c_mul_fma(a0, w0), b1 = c_mul_fma(a1, w1);
-        acc[0].x += a0.x + a1.x;
-        acc[0].y += a0.y + a1.y;
+    // rounding error grows at most like i^2 eps, ~1e-14 at 16 samples).  Four
+    // paths per step: four independent recurrences interleave (two left the
+    // wave waiting on FMA latency half its cycles, SQ_WAIT_INST_ANY 0.53), and
+    // the accumulation costs 1.5 adds per path and sample instead of 2.  With
+    // 24-sample chunks (PS = 2) two paths per step keep the kernel at 3
+    // waves / SIMD (4 need 204 VGPRs).
+    constexpr int PU = PS == 2 ? 2 : 4;
+    const int pend = (par + 1) * P / PS;
+    int p = par * P / PS;
+    for (; p + PU - 1 < pend; p += PU) {
+        double2 a[PU], b[PU];
+        double c[PU];
+#pragma unroll
+        for (int j = 0; j < PU; ++j) {
+            a[j] = cis_turns(ph[p + j] + ds[p + j] * t0);
+            c[j] = 2.0 * wr[p + j];
+            b[j] = c_mul_fma(a[j], make_double2(wr[p + j], wi[p + j]));
+        }
+        acc[0].x += PU == 4 ? (a[0].x + a[1].x) + (a[2 % PU].x + a[3 % PU].x) : a[0].x + a[1].x;
+        acc[0].y += PU == 4 ? (a[0].y + a[1].y) + (a[2 % PU].y + a[3 % PU].y) : a[0].y + a[1].y;
 #pragma unroll
         for (int i = 1; i < JCH; ++i) {
-            acc[i].x += b0.x + b1.x;
-            acc[i].y += b0.y + b1.y;
+            acc[i].x += PU == 4 ? (b[0].x + b[1].x) + (b[2 % PU].x + b[3 % PU].x) : b[0].x + b[1].x;
+            acc[i].y += PU == 4 ? (b[0].y + b[1].y) + (b[2 % PU].y + b[3 % PU].y) : b[0].y + b[1].y;
             if (i + 1 < JCH) {
-                const double2 n0 = make_double2(fma(c0, b0.x, -a0.x), fma(c0, b0.y, -a0.y));
-                const double2 n1 = make_double2(fma(c1, b1.x, -a1.x), fma(c1, b1.y, -a1.y));
-                a0 = b0;
-                a1 = b1;
-                b0 = n0;
-                b1 = n1;
+#pragma unroll
+                for (int j = 0; j < PU; ++j) {
+                    const double2 n = make_double2(fma(c[j], b[j].x, -a[j].x), fma(c[j], b[j].y, -a[j].y));
+                    a[j] = b[j];
+                    b[j] = n;
+                }
             }
         }
     }
-    for (; p < P; ++p) {
+    for (; p < pend; ++p) {
         double2 a = cis_turns(ph[p] + ds[p] * t0);
         const double2 w = make_double2(wr[p], wi[p]);
         const double c = 2.0 * wr[p];
@@ -289,22 +300,29 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
             }
         }
     }
+    if (PS == 2)
+#pragma unroll
+        for (int i = 0; i < JCH; ++i) {
+            acc[i].x += __shfl_xor(acc[i].x, 1);
+            acc[i].y += __shfl_xor(acc[i].y, 1);
+        }
     const double sp = sqrt((double)P);
     const double g = ch.sqrt_pdp[tap];
 #pragma unroll
     for (int i = 0; i < JCH; ++i) {
         const int n = n0 + i;
-        if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
+        if (n < ch.N && (i * PS) / JCH == par)
+            ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
     }
 }
 
-template <int JCH, int RPW = 1>
+template <int JCH, int RPW = 1, int PS = 1>
 static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R, double2* ir,
                            const int* chunk_n0 = nullptr, int nck = 0) {
-    constexpr int LPR = WAVE / RPW;
+    constexpr int CPW = WAVE / RPW / PS;          // chunks per realisation and wave
     const int nchunk = chunk_n0 ? nck : (ch.N + JCH - 1) / JCH;
-    dim3 grid((nchunk + LPR - 1) / LPR, R / (4 * RPW), ch.ntap);
-    hipLaunchKernelGGL((k_jakes<JCH, RPW>), grid, dim3(256), (size_t)4 * RPW * 4 * ch.paths * sizeof(double), s, ch,
+    dim3 grid((nchunk + CPW - 1) / CPW, R / (4 * RPW), ch.ntap);
+    hipLaunchKernelGGL((k_jakes<JCH, RPW, PS>), grid, dim3(256), (size_t)4 * RPW * 4 * ch.paths * sizeof(double), s, ch,
                        seed, rep0, R, ir, chunk_n0, nchunk);
 }
 
@@ -394,10 +412,12 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
                            rep0, R, ir);
         return;
     }
-    // only the samples some Q^H row reads (OFDM: the FFT windows): chunks of 12
-    // aligned to them, two realisations per wave
+    // only the samples some Q^H row reads (OFDM: the FFT windows): chunks of 24
+    // aligned to them, two realisations per wave, a lane pair per chunk
+    // splitting the paths (12-sample chunks, one lane each: 2.37 ms per
+    // 65536 realisations at C2, the per-chunk cis ~45 % of the instructions)
     if (jc && jc->n0 && op.jakes_win && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024) {
-        launch_jakes_t<JakesChunks::LEN, 2>(s, ch, seed, rep0, R, ir, jc->n0, jc->n);
+        launch_jakes_t<JakesChunks::LEN, 2, 2>(s, ch, seed, rep0, R, ir, jc->n0, jc->n);
         return;
     }
     // two realisations per wave (32 lanes each) when that gives chunks of 9-20
