@@ -1661,13 +1661,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         }
     }
     __syncthreads();
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const double2 hh = hc[a], yv = yh[a];
-        const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
-        hc[a] = make_double2(hh.x * id, -hh.y * id);            // 1 / h
-        yh[a] = c_mulf(yv, hc[a]);                               // y / h
-    }
     // data / no-edge masks of the lane's rows
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
@@ -1729,6 +1722,16 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][ro][m]);
         }
         dft6<-1>(x);
+        // y / h and 1 / h at the first epilogue (not before the loop): the
+        // first chain runs while y and h are still in flight
+        if (it == 1)
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double2 hh = hc[a], yv = yh[a];
+                const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+                hc[a] = make_double2(hh.x * id, -hh.y * id);        // 1 / h
+                yh[a] = c_mulf(yv, hc[a]);                           // y / h
+            }
         // epilogue per row 4a + r: z = y / h - acc / h + u, slicer, counts,
         // re-precoded decision into u
         int code[6], dp[6];
