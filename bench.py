@@ -346,7 +346,8 @@ def main():
                      "flops_per_launch": flops / launches if launches else None,
                      "work_model": ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
                                     "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
-                                    "at 5 n log2 n flops; peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else
+                                    "at 5 n log2 n flops; with pilot_fuse (iterations 1..niter-1) also the next iteration's pilot-symbol "
+                                    "chains (taps, channel, diag(D_hat) u, two DFT-24); peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
                                     "fused diag(D_hat)), 8 real flops per CMAC; the 3M form executes 6 of the 8 counted "
                                     "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "

@@ -961,6 +961,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.yperf = dalloc<double2>(c, LK * U, L);
     b.hp = dalloc<double2>(c, NP * U, L);
     b.hp2 = dalloc<double2>(c, NP * U, L);
+    b.hp3 = dalloc<double2>(c, NP * U, L);
     b.hest = dalloc<double2>(c, LK * U, L);
     b.v = dalloc<double2>(c, LK * U, L);
     b.u = dalloc<double2>(c, LK * U, L);
@@ -1106,6 +1107,11 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                               perfect_chain_fft(op, s.k, c->ch, b, c->niter);
             double2* hp_prev = b.hp;
             double2* hp_cur = b.hp2;
+            double2* hp_next = b.hp3;
+            // pilot_fuse: iteration it's k_mic_fft also runs iteration it + 1's
+            // pilot pass in its pilot-symbol blocks (hP of it + 1 into hp_next)
+            const bool pfz = yic && op.pilot_fuse && op.mic_mfma;
+            bool have_next = false;
             for (int it = 0; it <= c->niter; ++it) {
                 if (it == 1 && (two || chain)) {
                     hipStream_t ps = two ? c->stream2 : c->stream;
@@ -1128,7 +1134,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                     if (two) DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
                 }
                 if (it > 0 && mic) {
-                    {
+                    if (!have_next) {
                         Timed t(c, "k_pilot_pre");
                         if (op.pilot_fft && mm.npb > 0)
                             launch_pilot_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter), b, hp_prev,
@@ -1144,9 +1150,18 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
                                              s.k.slI, s.k.slQ};
                         s.path |= launch_mmse_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter),
                                                   var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
-                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0, yic);
+                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0, yic,
+                                                  pfz ? hp_next : nullptr);
                     }
-                    std::swap(hp_prev, hp_cur);
+                    have_next = pfz && it < c->niter;
+                    if (have_next) {
+                        double2* const t = hp_prev;
+                        hp_prev = hp_cur;
+                        hp_cur = hp_next;
+                        hp_next = t;
+                    } else {
+                        std::swap(hp_prev, hp_cur);
+                    }
                     if (!two && !chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
@@ -1833,6 +1848,12 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
         const double nt = ctx->ch.ntap, NP = s.d.n_pilots;
         const double blk = nt * 24 * NP + nt * NP + nt * 24 + 2 * 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
         *cmac = blk * s.k.QH.nblk * ctx->nsnr * ctx->niter;
+        // pilot_fuse: iterations 1..niter-1 also form the next iteration's y_ic of
+        // the pilot symbols (taps, channel, diag(D_hat) u, two DFT-24)
+        if (s.path & PATH_PILOT_FUSED) {
+            const double pil = nt * 24 * NP + nt * 24 + 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
+            *cmac += pil * s.npb * ctx->nsnr * (ctx->niter - 1);
+        }
     }
     if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
     API_END
@@ -1869,7 +1890,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(snr_base)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

@@ -30,6 +30,7 @@ struct Opts {
     int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
     int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
+    int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
 };
 
@@ -49,6 +50,7 @@ enum : unsigned {
     PATH_PIC_FFT = 1u << 10,       // k_pic_fft (perfect-CSI chain by FFT, OFDM)
     PATH_MIC_FFT = 1u << 11,       // k_pilot_pre + k_mic_fft (MMSE IC as Q' H_hat G by FFT, OFDM)
     PATH_TXRX_FFT = 1u << 12,      // k_txrx_fft (TX + channel + noisy receiver front by FFT, OFDM)
+    PATH_PILOT_FUSED = 1u << 13,   // k_mic_fft also runs the next iteration's pilot pass (pilot_fuse)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -84,6 +86,7 @@ struct McBuffers {
     double2* yperf;   // [LK][U]
     double2* hp;      // [NP][U]   LS pilot estimates of the current stage
     double2* hp2;     // [NP][U]   second buffer (fused MMSE stage: previous / current stage)
+    double2* hp3;     // [NP][U]   third buffer (k_mic_fft with the next iteration's pilot pass)
     double2* hest;    // [LK][U]   diag(D_hat) of the current stage
     double2* v;       // [LK][U]   P [xP; Q(x_est)]
     double2* u;       // [LK][U]   P [xP; Q(x_perfect)]
@@ -180,7 +183,7 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                          const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,
-                         bool tapm = true, bool yic = false);
+                         bool tapm = true, bool yic = false, double2* hp_next = nullptr);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in

@@ -1839,6 +1839,13 @@ struct MicArgs {
     double2* yest;                        // [LK][U]
     const int* pmask;                     // [nblk]: 1 = the block holds pilot rows
     int yic;
+    // the next iteration's pilot pass fused into the main pass (fuse, yic blocks
+    // only): once a pilot-symbol block has its decisions, it forms the next
+    // iteration's y_ic of the symbol with the taps Bv(var_cur) hp_new, stores it
+    // over yest and the LS pilots into hp_next (a third buffer: other blocks of
+    // this launch still read hp_prev)
+    double2* hp_next;                     // [NP][U]
+    int fuse;
 };
 
 template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM, bool PILOT>
@@ -1849,6 +1856,10 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     if (PILOT) blk = ma.pblk[blk];
     // block-uniform: this pilot-symbol block's y_ic comes from the pilot pass
     const bool yic = !PILOT && ma.yic && ma.pmask[blk];
+    // block-uniform: this pilot-symbol block also runs the next iteration's
+    // pilot pass (its sbv / hhs then hold Bv(var_cur) and the taps of hp_new:
+    // the y_ic epilogue of this iteration reads neither)
+    const bool fz = TAPM && !PILOT && yic && ma.fuse;
     const int tid = threadIdx.x, l = tid & 63, r = l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int U = o.U, R = o.R;
@@ -1861,6 +1872,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     constexpr int BVS = NP + 1;                                 // padded sample stride: the quad's 4 rows in distinct banks
     __shared__ double2 sbv[NT][24][BVS];                        // Bv of the symbol's window samples (previous stage's var)
     __shared__ double2 sbs[NT][NP];                             // Bs of the symbol (this stage's var)
+    __shared__ int rpc[PILOT ? 1 : 24];                         // pilot column of the block's rows (fz)
     __shared__ double2 sym[256];
     __shared__ int sgrid[256];
     __shared__ double2 rpv[24];
@@ -1895,6 +1907,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         const int rt = min(tid, 23);
         const double2 pv = o.row_pval[row0 + rt];
         const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        const int pcr = PILOT ? 0 : sk.row_pcol[row0 + rt];
         // twiddles (a lane-varying index into the constant table is a vector
         // load: issued here, with the tables, not behind the per-unit loads)
         const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);
@@ -1905,7 +1918,8 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         // contiguous per tap) and Bs of the block (loaded unconditionally: a
         // branch around the array loads sent it through scratch)
         constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
-        const double2* __restrict__ bvb = ma.bv + ((size_t)(ma.var_prev * ma.nsnr + snr) * NT * ma.N + klo) * NP;
+        const double2* __restrict__ bvb =
+            ma.bv + ((size_t)((fz ? ma.var_cur : ma.var_prev) * ma.nsnr + snr) * NT * ma.N + klo) * NP;
         double2 bvr[PER];
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
@@ -1913,10 +1927,11 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
                 bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
             }
         const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
-        if (TAPM && !yic) {
+        if (TAPM && (!yic || fz)) {
+            const double2* __restrict__ hpb = fz ? ma.hp_new : ma.hp_prev;
     #pragma unroll
             for (int ks = 0; ks < NKS; ++ks) {
-                hb[ks] = ma.hp_prev[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
+                hb[ks] = hpb[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
             }
         }
     #pragma unroll
@@ -1938,6 +1953,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
         rpv[rt] = pv;                                           // unconditional, clamped (see k_pic_fft)
         rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+        if (!PILOT) rpc[rt] = pcr;
         // unconditional (yic blocks do not read sbv): under `if (!yic)` the
         // compiler sinks the bvr loads next to these writes, behind a vmcnt(0)
 #pragma unroll
@@ -1978,7 +1994,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     // jc) go through the wave's own LDS slab into the quad layout; otherwise
     // each lane forms its 12 taps on the VALU (Bv rows broadcast from LDS)
     __shared__ double2 hhs[TAPM ? 4 : 1][TAPM ? NTILE * 16 : 1][17];
-    if (TAPM && !yic) {
+    if (TAPM && (!yic || fz)) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             br[ks] = hb[ks].x;
@@ -2062,15 +2078,13 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     // ---- phase B: acc = Q' H_hat G u for the symbol (k_pic_fft's chain); a yic
     // block has y_ic already
-    double2 x[6];
-    if (!yic) {
-    #pragma unroll
-        for (int a = 0; a < 6; ++a) x[a] = u[a];
-        dft6<1>(x);
+    // x <- Q' (H_hat (G x)) of the symbol for the taps tp (k_pic_fft's chain)
+    auto chain = [&](double2 (&xx)[6], const double2 (&tp)[6][NT]) {
+        dft6<1>(xx);
         double2 t[6];
     #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
+            const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
             const double2 pv = dpp_c<QP_XOR2>(p);
             double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
             e = c_mulf(e, twb[0][r]);
@@ -2080,10 +2094,10 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         const double2 tprev = dpp_c<QP_PREV>(t[5]);
     #pragma unroll
         for (int m = 5; m >= 0; --m) {
-            const double2 tp = m ? t[m - 1] : tprev;
+            const double2 tq = m ? t[m - 1] : tprev;
             double2 acc = make_double2(0.0, 0.0);
     #pragma unroll
-            for (int q = 0; q < NT; ++q) c_fma(acc, taps[m][q], ((SH >> q) & 1) ? tp : t[m]);
+            for (int q = 0; q < NT; ++q) c_fma(acc, tp[m][q], ((SH >> q) & 1) ? tq : t[m]);
             t[m] = acc;
         }
     #pragma unroll
@@ -2092,9 +2106,15 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
             f = c_mulf(f, twb[1][r]);
             const double2 qv = dpp_c<QP_XOR2>(f);
-            x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+            xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
         }
-        dft6<-1>(x);
+        dft6<-1>(xx);
+    };
+    double2 x[6];
+    if (!yic) {
+    #pragma unroll
+        for (int a = 0; a < 6; ++a) x[a] = u[a];
+        chain(x, taps);
     }
     if constexpr (PILOT) {
         // the next stage's LS pilot estimates (script:487-489) at the block's pilot rows
@@ -2148,6 +2168,20 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             o.tr->hest[(size_t)ma.stage * o.tr->LK + row] = hnv;
         }
     }
+    // fz: y as received and the transmitted pilots of the next iteration's
+    // pilot pass, requested as soon as y_ic is consumed (their latency runs
+    // under the tie handling, the counts and the decision stores)
+    double2 xq[6];
+    int pc[6];
+    if (fz) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            pc[a] = rpc[4 * a + r];
+            yv[a] = o.y[(size_t)row * U + unit];
+            xq[a] = o.xp[(size_t)min(max(pc[a], 0), NP - 1) * R + rl];
+        }
+    }
     if (ma.mse_err) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -2189,6 +2223,37 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
                      (size_t)o.cstride_edge, 0);
     }
     if (ma.mse_err) flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage);
+    if (fz) {
+        // the next iteration's pilot pass (PILOT mode above) on this symbol:
+        // u = this iteration's decisions, taps Bv(var_cur) hp_new from the
+        // wave's slab, sp0 / sp1 their window sums (formed above), y as received
+        const double sqk = 1.0 / sk.inv_sqrt_kappa;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            u[a] = qidx_value((dmask >> a) & 1, (unsigned)dp[a], rpv[4 * a + r], sym, o.xs, (size_t)row * R + rl);
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q)
+#pragma unroll
+            for (int m = 0; m < 6; ++m) taps[m][q] = hhs[w][q * 24 + 6 * cq + m][l >> 2];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) x[a] = u[a];
+        chain(x, taps);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int row = row0 + 4 * a + r;
+            double2 ye = c_sub(yv[a], x[p6(a)]);
+            double2 hpv = sp0;
+            c_fma(hpv, wrow[4 * a + r], sp1);
+            c_fma(ye, hpv, u[a]);
+            ma.yest[(size_t)row * U + unit] = ye;
+            if (pc[a] >= 0 && pc[a] < NP) {
+                const double2 qq = c_div(ye, xq[a]);
+                ma.hp_next[(size_t)pc[a] * U + unit] = make_double2(qq.x / sqk, qq.y / sqk);
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2649,7 +2714,7 @@ bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Chann
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                          const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx, bool tapm,
-                         bool yic) {
+                         bool yic, double2* hp_next) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     MicArgs ma{};
     ma.bv = mm.Bv;
@@ -2671,6 +2736,9 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     ma.yest = b.yest;
     ma.pmask = mm.pmask;
     ma.yic = yic && mm.pmask ? 1 : 0;
+    ma.hp_next = hp_next;
+    ma.fuse = hp_next && ma.yic && tapm && !last ? 1 : 0;
+    const unsigned pf = ma.fuse ? PATH_PILOT_FUSED : 0u;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
 #define LAUNCH_MIC3(NTV, SHV, TM)                                                                                     \
@@ -2695,7 +2763,7 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     else LAUNCH_MIC(2, 2);
 #undef LAUNCH_MIC
 #undef LAUNCH_MIC3
-    return PATH_MIC_FFT;
+    return PATH_MIC_FFT | pf;
 }
 
 // The pilot pre-pass of the structured MMSE IC (k_mic_fft in PILOT mode): y_ic of

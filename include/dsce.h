@@ -195,6 +195,7 @@ typedef struct {
 #define DSCE_PATH_PIC_FFT         (1u << 10)  /* k_pic_fft: perfect-CSI IC chain by FFT (OFDM, VALU)       */
 #define DSCE_PATH_MIC_FFT         (1u << 11)  /* k_pilot_pre + k_mic_fft: MMSE IC as Q' H_hat G by FFT (OFDM) */
 #define DSCE_PATH_TXRX_FFT        (1u << 12)  /* k_txrx_fft: TX + channel + noisy receiver front by FFT (OFDM) */
+#define DSCE_PATH_PILOT_FUSED     (1u << 13)  /* k_mic_fft also runs the next IC iteration's pilot pass       */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -291,7 +292,7 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  * OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}
  * (k_mic_fft; equal to the W contraction of script:482-511 to rounding, checked
  * at dsce_build_mmse), 0: the W contraction everywhere), qidx, stage0_fft,
- * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic (the OFDM fast-path pieces,
+ * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic, pilot_fuse (the OFDM fast-path pieces,
  * 1 = on), snr_base (0..255: the noise of SNR index k is sub-stream
  * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
  * one-rank run's noise).  Unknown names return DSCE_EINVAL. */

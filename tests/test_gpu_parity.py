@@ -73,8 +73,8 @@ def test_mmse_estimator_matches_oracle(ofdm):
 # for the perfect-CSI IC chain, k_stage_fused for the one-tap stage); the W
 # contraction (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"mic_fft", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
-W_PATH = BENCH_PATH - {"mic_fft"} | {"wpair3_fused"}
+BENCH_PATH = {"mic_fft", "pilot_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
+W_PATH = BENCH_PATH - {"mic_fft", "pilot_fused"} | {"wpair3_fused"}
 
 
 def _check_trace(g, u, name, tol=1e-9):
@@ -270,7 +270,9 @@ def test_stage_variants_agree(name):
     pilot rows (k_pilot_pre) instead of the structured chain, the Jakes taps at
     every sample instead of only where a Q^H row reads them, TX / channel /
     noisy Q^H as banded passes instead of k_txrx_fft, the pilot symbols' y_ic
-    formed again in k_mic_fft instead of handed over by the pilot pass."""
+    formed again in k_mic_fft instead of handed over by the pilot pass, the
+    pilot pass as its own launch instead of riding in the previous iteration's
+    k_mic_fft."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -286,7 +288,7 @@ def test_stage_variants_agree(name):
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
                 {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
-                {"mic_yic": 0})
+                {"mic_yic": 0}, {"pilot_fuse": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
