@@ -146,6 +146,28 @@ def test_error_counts_match_oracle(ofdm):
     assert b[0] == sc["n_data"] * sc["bits_per_symbol"] and b[1] == sc["considered"].sum() * sc["bits_per_symbol"]
 
 
+@pytest.mark.parametrize("n_iter", [1, 2, 3, 6])
+def test_ic_iteration_counts_match_oracle(n_iter):
+    """Other IC iteration counts (script:479 `NrIterations`): the estimator
+    variant switch (W0 up to niter / 2, script:497-501) and the fused pilot pass
+    (iteration i's k_mic_fft forms iteration i + 1's pilots; none for niter 1)
+    against the oracle, counts of every stage, and one unit traced per element."""
+    S = harness.setup("default", schemes=("ofdm",), snr_db=[15.0, 35.0], n_iter=n_iter)
+    eng = harness.engine(S, batch=64)
+    cg = eng.run(SEED, 0, 64)
+    path = eng.path_info(0)
+    assert BENCH_PATH - {"pilot_fused"} <= path, path
+    assert ("pilot_fused" in path) == (n_iter >= 2), path
+    res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
+    assert cg.shape == res["err"].shape
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
+    tr = {}
+    harness.simulate(S, SEED, 3, 1, ["ofdm"], trace=tr)
+    for k in range(2):
+        assert _check_trace(eng.trace_unit(0, SEED, 3, k), tr["units"][k], "niter %d snr %d" % (n_iter, k)) == n_iter + 1
+    eng.close()
+
+
 # ---------------------------------------------------------------------------
 # C3 / C4: FBMC-OQAM with auxiliary-symbol and data-spreading precoders
 # (two SNR points keep the literal oracle's run time in check)
