@@ -206,8 +206,9 @@ static constexpr int JCH_MAX = 16;
 // PS lanes per chunk split the paths (PS = 2: lane pair, sums joined by a lane
 // exchange): long chunks amortise the per-chunk cis without idling lanes.
 template <int JCH, int RPW, int PS = 1>
-__global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
-                                               double2* __restrict__ ir, const int* __restrict__ chunk_n0, int nchunk) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_jakes(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restrict__ ir, const int* __restrict__ chunk_n0,
+        int nchunk) {
     extern __shared__ double sm[];
     constexpr int LPR = WAVE / RPW;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -252,8 +253,10 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
     // paths per step: four independent recurrences interleave (two left the
     // wave waiting on FMA latency half its cycles, SQ_WAIT_INST_ANY 0.53), and
     // the accumulation costs 1.5 adds per path and sample instead of 2.  With
-    // 24-sample chunks (PS = 2) two paths per step keep the kernel at 3
-    // waves / SIMD (4 need 204 VGPRs).
+    // 24-sample chunks (PS = 2) two paths per step (4 need 204 VGPRs); pinned
+    // to 3 waves / SIMD (154 VGPRs, no spill since the lane pair exchanges
+    // half-chunks below; unpinned the compiler took 204 and 2 waves: 2.04 ->
+    // 1.90 ms per step at C2; 4 waves spill inside the path loop: 1.97 ms).
     constexpr int PU = PS == 2 ? 2 : 4;
     const int pend = (par + 1) * P / PS;
     int p = par * P / PS;
@@ -300,19 +303,27 @@ __global__ void __launch_bounds__(256) k_jakes(ChannelK ch, uint64_t seed, uint6
             }
         }
     }
-    if (PS == 2)
-#pragma unroll
-        for (int i = 0; i < JCH; ++i) {
-            acc[i].x += __shfl_xor(acc[i].x, 1);
-            acc[i].y += __shfl_xor(acc[i].y, 1);
-        }
     const double sp = sqrt((double)P);
     const double g = ch.sqrt_pdp[tap];
+    if constexpr (PS == 2) {
+        // the lane pair's path sums: each lane keeps the half of the chunk it
+        // stores and receives the partner's partial sums of that half (one
+        // exchange per sample instead of two; a + b == b + a, same sums)
+        constexpr int H = JCH / 2;
 #pragma unroll
-    for (int i = 0; i < JCH; ++i) {
-        const int n = n0 + i;
-        if (n < ch.N && (i * PS) / JCH == par)
-            ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
+        for (int k = 0; k < H; ++k) {
+            const double sx = par ? acc[k].x : acc[k + H].x, sy = par ? acc[k].y : acc[k + H].y;
+            const double ox = par ? acc[k + H].x : acc[k].x, oy = par ? acc[k + H].y : acc[k].y;
+            const double vx = ox + __shfl_xor(sx, 1), vy = oy + __shfl_xor(sy, 1);
+            const int n = n0 + k + H * par;
+            if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (vx / sp), g * (vy / sp));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < JCH; ++i) {
+            const int n = n0 + i;
+            if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(g * (acc[i].x / sp), g * (acc[i].y / sp));
+        }
     }
 }
 
