@@ -352,7 +352,10 @@ def main():
                                     "fused diag(D_hat)), 8 real flops per CMAC; the 3M form executes 6 of the 8 counted "
                                     "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "
                                     "peak"),
-                     "paths": paths},
+                     "paths": paths,
+                     "limiter": ("neither roof: issue-latency-bound at 2 waves/SIMD (240 VGPRs, 72.8 KB LDS; VALU "
+                                 "issue ~45 %, HBM ~0.30 of 8 TB/s, profiles/r02r_pmc_table.txt, DESIGN.md section 4)")
+                                if mic_l else "matrix cores (mfma_busy)"},
         "cpu_baseline": cpu,
         "setup_s": setup_s,
         "kernels_ms": kernels,
