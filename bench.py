@@ -77,7 +77,7 @@ def source_hash():
 # CPU baseline: the oracle (literal NumPy restatement of the reference's dense
 # formulation) on the GPU box's host cores, bounded sample, median of 3
 # ---------------------------------------------------------------------------
-def cpu_baseline_leg(seconds, workload):
+def cpu_baseline_leg(seconds, workload, index=0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import harness
     from oracle import refsim
@@ -86,14 +86,15 @@ def cpu_baseline_leg(seconds, workload):
     mm = [harness.oracle_mmse(S, s) for s in schemes]              # setup, untimed
     chan = S.chan
     osc = [S.schemes[s] for s in schemes]
-    refsim.simulate(SEED, 20_000_000, 1, chan, osc, S.pn_time, S.n_iter, mm)   # warm-up
+    base = 10_000_000 + 1_000_000 * index            # disjoint realisations per pool process
+    refsim.simulate(SEED, base + 900_000, 1, chan, osc, S.pn_time, S.n_iter, mm)   # warm-up
     rates = []
     n_total = 0
     for k in range(3):
         n = 0
         t0 = time.perf_counter()
         while True:
-            refsim.simulate(SEED, 10_000_000 + n_total, 1, chan, osc, S.pn_time, S.n_iter, mm)
+            refsim.simulate(SEED, base + n_total, 1, chan, osc, S.pn_time, S.n_iter, mm)
             n += 1
             n_total += 1
             el = time.perf_counter() - t0
@@ -120,39 +121,60 @@ def host_info():
     return info
 
 
+def _leg_env(threads=1):
+    env = dict(os.environ)
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "BLIS_NUM_THREADS"):
+        env[k] = str(threads)
+    env["HIP_VISIBLE_DEVICES"] = ""
+    return env
+
+
 def run_cpu_baseline(seconds, workload):
+    """Two legs of the oracle on the host, each about seconds / 2: one process
+    with single-threaded BLAS, and a pool of P such processes running at once
+    on disjoint realisations (P = the host share: OMP_NUM_THREADS on the GPU box
+    (16), else the CPUs this process may use).  Per-realisation NumPy work is
+    too small for BLAS threading (r02: 16 BLAS threads ran slower than one), so
+    the all-core baseline is the process pool: its value is the sum of the
+    processes' rates."""
     host = host_info()
-    nt = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or host.get("affinity") or host["nproc"]
-    legs = {}
-    for threads in (1, nt):
-        env = dict(os.environ)
-        for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS", "BLIS_NUM_THREADS"):
-            env[k] = str(threads)
-        env["HIP_VISIBLE_DEVICES"] = ""
-        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds",
-                              str(seconds / 2), "--config", workload], env=env, capture_output=True, text=True,
-                             timeout=900)
-        if out.returncode != 0:
+    pool = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or host.get("affinity") or host["nproc"]
+    pool = max(1, min(pool, host.get("affinity") or pool))
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds", str(seconds / 2),
+           "--config", workload]
+    one = subprocess.run(cmd, env=_leg_env(), capture_output=True, text=True, timeout=900)
+    if one.returncode != 0:
+        return None
+    leg1 = json.loads(one.stdout.strip().splitlines()[-1])
+    procs = [subprocess.Popen(cmd + ["--leg-index", str(i + 1)], env=_leg_env(), stdout=subprocess.PIPE,
+                              stderr=subprocess.DEVNULL, text=True) for i in range(pool)]
+    legs = []
+    for pr in procs:
+        out, _ = pr.communicate(timeout=900)
+        if pr.returncode != 0:
             return None
-        legs[threads] = json.loads(out.stdout.strip().splitlines()[-1])
-    med = {t: statistics.median(r["rates"]) for t, r in legs.items()}
-    best = max(med, key=med.get)          # the baseline is the faster of the two thread counts
-    return {"value": med[best], "unit": "realisations/s", "cores": best, "kind": "port",
-            "value_1t": med[1], "value_nt": med[nt], "samples_1t": legs[1]["rates"], "samples_nt": legs[nt]["rates"],
+        legs.append(json.loads(out.strip().splitlines()[-1]))
+    v1 = statistics.median(leg1["rates"])
+    vp = sum(statistics.median(l["rates"]) for l in legs)
+    return {"value": max(v1, vp), "unit": "realisations/s", "cores": pool if vp >= v1 else 1, "kind": "port",
+            "value_1t": v1, "value_pool": vp, "pool_processes": pool, "samples_1t": leg1["rates"],
+            "samples_pool": [l["rates"] for l in legs],
             "label": "CPU restatement of reference algorithm, not MATLAB",
             "sample": "oracle/refsim.simulate (dense Q'HG zgemm, full(W) reshape-and-sum contraction, brute-force "
-                      "nearest-neighbour detection, NumPy/OpenBLAS fp64) on %s; median of 3 samples of ~%.0f s per "
-                      "thread count (%d and %d threads), %d + %d realisations"
-                      % (workload.upper(), seconds / 6, 1, nt, legs[1]["reps"], legs[nt]["reps"]),
+                      "nearest-neighbour detection, NumPy/OpenBLAS fp64, 1 BLAS thread per process) on %s: one "
+                      "process, then %d concurrent processes on disjoint realisations; 3 samples of ~%.0f s per "
+                      "process, median; %d + %d realisations"
+                      % (workload.upper(), pool, seconds / 6, leg1["reps"], sum(l["reps"] for l in legs)),
             "host": host}
 
 
-def stored_traffic(kernel_tag, workload):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC
-    summary (profiles/*_pmc_*.json, tools/prof_summary.py), used only when it
-    was measured on a build of these exact sources, this workload and kernel."""
+def stored_pmc(kernel_tag, workload):
+    """The committed rocprofv3 PMC summary of the dominant kernel
+    (profiles/*_pmc_*.json, tools/prof_summary.py: HBM bytes per launch and the
+    SQ counters per launch), used only when it was measured on a build of these
+    exact sources, this workload and kernel.  Returns (summary or None, source)."""
     src = source_hash()
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json")), key=os.path.getmtime)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json")))
     for f in reversed(cands):
         try:
             d = json.load(open(f))
@@ -160,8 +182,51 @@ def stored_traffic(kernel_tag, workload):
             continue
         if d.get("source_hash") == src and d.get("workload", "c2") == workload and \
                 d.get("kernel", "k_wcontract") == kernel_tag:
-            return d.get("hbm_bytes_per_launch"), "profiles/" + os.path.basename(f)
+            return d, "profiles/" + os.path.basename(f)
     return None, "no PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
+
+
+SIMDS = 1024                   # 256 CUs x 4 SIMDs (MI355X)
+
+
+def derive_limiter(pmc, achieved_tf, avg_ms):
+    """What bounds the kernel, from the stamped PMC summary of THIS build (None
+    without one).  Kernel cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs,
+    MI355X_MICROARCH.md, DVFS note); per SIMD and cycle:
+      valu_issue   = SQ_INSTS_VALU x 4 / (SIMDS x cycles)   (a 64-lane FP64 VALU op
+                     occupies a 16-lane SIMD 4 cycles)
+      mfma_busy    = SQ_VALU_MFMA_BUSY_CYCLES / (SIMDS x cycles)
+      waves/SIMD   = SQ_WAVE_CYCLES x 4 / (SIMDS x cycles)  (quad-cycles)
+      wait         = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES      (share of wave time stalled on a dependency)
+      hbm          = HBM bytes per launch / launch time / 8 TB/s
+      fp64         = achieved / 78.6 TF (VALU and MFMA FP64 share that peak)
+    The limiter is the largest utilisation when it reaches 0.7, else issue
+    latency."""
+    if not pmc:
+        return None
+    sq = pmc.get("sq_per_launch") or {}
+    need = ("GRBM_GUI_ACTIVE", "SQ_INSTS_VALU", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY")
+    if any(sq.get(k) is None for k in need) or not sq["GRBM_GUI_ACTIVE"]:
+        return None
+    cyc = sq["GRBM_GUI_ACTIVE"] / 8.0
+    d = {"valu_issue": sq["SQ_INSTS_VALU"] * 4.0 / (SIMDS * cyc),
+         "mfma_busy": sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * cyc),
+         "waves_per_simd": sq["SQ_WAVE_CYCLES"] * 4.0 / (SIMDS * cyc),
+         "wait_frac": sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"] if sq["SQ_WAVE_CYCLES"] else None,
+         "valu_per_mfma": sq["SQ_INSTS_VALU"] / sq["SQ_INSTS_MFMA"] if sq.get("SQ_INSTS_MFMA") else None,
+         "eff_clock_ghz": cyc / (pmc["avg_duration_ns_rocprof"] * 1e-9) / 1e9 if pmc.get("avg_duration_ns_rocprof") else None,
+         "hbm": (pmc["hbm_bytes_per_launch"] / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9))
+         if pmc.get("hbm_bytes_per_launch") and avg_ms else None,
+         "fp64": achieved_tf / FP64_PEAK_TFLOPS if achieved_tf else None}
+    util = {k: d[k] for k in ("valu_issue", "mfma_busy", "hbm") if d[k] is not None}
+    top = max(util, key=util.get)
+    if util[top] >= 0.7:
+        d["limiter"] = {"valu_issue": "VALU issue", "mfma_busy": "matrix cores", "hbm": "HBM bandwidth"}[top]
+    else:
+        d["limiter"] = "issue latency (%.1f waves/SIMD, %.0f %% of wave cycles stalled on dependencies)" % (
+            d["waves_per_simd"], 100 * (d["wait_frac"] or 0))
+    d["source"] = "PMC counters of this build (derive_limiter in bench.py)"
+    return {k: (round(v, 4) if isinstance(v, float) else v) for k, v in d.items()}
 
 
 # ---------------------------------------------------------------------------
@@ -198,9 +263,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-leg", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--leg-index", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_leg:
-        cpu_baseline_leg(args.cpu_seconds, args.config)
+        cpu_baseline_leg(args.cpu_seconds, args.config, args.leg_index)
         return 0
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -289,7 +355,14 @@ def main():
     achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     peak_meas = eng.fp64_mfma_peak()
-    traffic, traffic_src = stored_traffic(kname, args.config)
+    pmc, traffic_src = stored_pmc(kname, args.config)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    avg_ms = wc_ms / launches if launches else None
+    lim = derive_limiter(pmc, achieved_tf, avg_ms)
+    # the roof the kernel sits closer to: FP64 compute (MFMA / VALU share the
+    # peak) or HBM (traffic from the stamped PMC pass)
+    hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
+    bound = "hbm" if hbm_frac is not None and achieved_tf and hbm_frac > achieved_tf / FP64_PEAK_TFLOPS else "mfma"
     kernels = {}
     for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_fft", "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
@@ -329,7 +402,7 @@ def main():
         "data": "synthetic (Philox4x32-10 streams, include/dsce.h)",
         "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
                    "parallelism": "dp%d" % world, "options": options},
-        "roofline": {"bound": "mfma",
+        "roofline": {"bound": bound,
                      "kernel": ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v; H_hat = Bv hP "
                                 "on the matrix cores (3M), DFT-24 chain + one-tap + detection on the VALU; FP64 "
                                 "roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both peaks "
@@ -338,9 +411,14 @@ def main():
                                 "diag(D_hat) + detection in its epilogue)"),
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
-                     "peak_measured": None if mic_l else peak_meas,
-                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas and not mic_l else None,
-                     "mfma_busy": (exec_tf / peak_meas) if exec_tf and peak_meas and not mic_l else None,
+                     "peak_measured": peak_meas,
+                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas else None,
+                     # executed matrix-core flops / measured peak from the work model (W contraction), or the
+                     # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (k_mic_fft: only its tap GEMM
+                     # runs on the matrix cores)
+                     "mfma_busy": (lim or {}).get("mfma_busy") if mic_l else
+                     ((exec_tf / peak_meas) if exec_tf and peak_meas else None),
+                     "hbm_frac": hbm_frac,
                      "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
                      "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
                      "flops_per_launch": flops / launches if launches else None,
@@ -353,9 +431,8 @@ def main():
                                     "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "
                                     "peak"),
                      "paths": paths,
-                     "limiter": ("neither roof: issue-latency-bound at 2 waves/SIMD (240 VGPRs, 72.8 KB LDS; VALU "
-                                 "issue ~45 %, HBM ~0.30 of 8 TB/s, profiles/r02r_pmc_table.txt, DESIGN.md section 4)")
-                                if mic_l else "matrix cores (mfma_busy)"},
+                     "limiter": lim["limiter"] if lim else None,
+                     "counters": lim},
         "cpu_baseline": cpu,
         "setup_s": setup_s,
         "kernels_ms": kernels,

@@ -105,9 +105,11 @@ struct Scheme {
     int* pil_c0 = nullptr;
     double2* Bv = nullptr;          // structured MMSE IC operator (k_mic_fft; null: not eligible)
     double2* Bs = nullptr;
-    int* pblk = nullptr;            // QH blocks with pilot rows (k_pilot_fft)
+    int* pblk = nullptr;            // QH blocks with pilot rows (k_pilot_fft, k_mic_pilot)
     int* pmask = nullptr;           // [QH blk] 1 = holds pilot rows
     int npb = 0;
+    int* dblk = nullptr;            // QH blocks without pilot rows (k_mic_data)
+    int ndb = 0;
     long long wp_elems = 0, wp_exec = 0;
     long long w_diag = 0;           // (r, r) pairs inside the band (stored as zeros: diag(D_hat) comes from Wd)
     unsigned path = 0;              // PATH_* bits of the last dsce_run / trace (dsce_path_info)
@@ -147,7 +149,7 @@ struct dsce_ctx {
     JakesChunks jk{};                     // samples of the IR a batch needs (update_jakes_chunks)
     size_t jk_nsch = (size_t)-1;          // scheme count jk was computed for
     McBuffers buf{};
-    size_t buf_key[6] = {0, 0, 0, 0, 0, 0};
+    size_t buf_key[7] = {0, 0, 0, 0, 0, 0, 0};
     std::vector<void*> buf_allocs;
     unsigned long long* d_counters = nullptr;
     size_t counters_n = 0;
@@ -346,70 +348,21 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
                 if (seen[n]++) disj = false;
         s.k.qh_disjoint = disj ? 1 : 0;
     }
-    // fused perfect-CSI IC tables (see SchemeK::pic_ok)
+    // block-local perfect-CSI IC (SchemeK::pic_ok): every Q^H block reads only
+    // samples whose G columns are the block's own rows
     {
         int md = 0;
         for (int q = 0; q < c->ch.ntap; ++q) md = std::max(md, c->ch.tap_delay[q]);
         const int nb = (int)s.qband.row0.size();
-        std::vector<int> s0v(nb);
-        std::vector<long long> goff(nb);
-        std::vector<double2> gtab;
         bool ok = true;
-        int prow = 0;
         for (int b = 0; b < nb && ok; ++b) {
             const int r0 = s.qband.row0[b], klo = s.qband.klo[b], khi = s.qband.khi[b];
             const int s0 = std::max(0, klo - md);
             for (int n = s0; n < khi && ok; ++n)
                 for (int col = 0; col < LK && ok; ++col)
                     if (nz(s.G[(size_t)col * N + n]) && (col < r0 || col >= r0 + DSCE_RB)) ok = false;
-            s0v[b] = s0;
-            prow = std::max(prow, (khi - s0) + (khi - klo));
-            goff[b] = (long long)gtab.size();
-            for (int n = s0; n < khi; ++n)
-                for (int cc = 0; cc < DSCE_RB; ++cc)
-                    gtab.push_back(r0 + cc < LK ? s.G[(size_t)(r0 + cc) * N + n] : make_double2(0, 0));
         }
-        s.k.pic_ok = ok && nb > 0 && prow * DSCE_RB * 16 <= 96 * 1024 ? 1 : 0;
-        s.k.pic_rows = prow;
-        if (s.k.pic_ok) {
-            s.k.pic_s0 = dupload(c, s0v);
-            s.k.pic_goff = dupload(c, goff);
-            s.k.pic_g = dupload(c, gtab);
-        }
-        // MFMA operand tables of k_pic_mfma (SchemeK::pm_ok)
-        int ksq = 0;
-        bool mok = s.k.pic_ok && md <= 1;
-        for (int b = 0; b < nb && mok; ++b) {
-            const int klo = s.qband.klo[b], khi = s.qband.khi[b];
-            if (khi - s0v[b] > 32 || khi - klo > 28 || s.qband.nrows[b] > DSCE_RB) mok = false;
-            ksq = std::max(ksq, (khi - klo + 3) / 4);
-        }
-        s.k.pm_ok = mok ? 1 : 0;
-        if (mok) {
-            const long long stride = (long long)(2 * 6 + 2 * ksq) * 64;
-            std::vector<double2> pa((size_t)stride * nb, make_double2(0, 0));
-            for (int b = 0; b < nb; ++b) {
-                const int r0 = s.qband.row0[b], nr = s.qband.nrows[b], klo = s.qband.klo[b], khi = s.qband.khi[b];
-                double2* g = pa.data() + (size_t)stride * b;
-                double2* q = g + 2 * 6 * 64;
-                for (int t = 0; t < 2; ++t)
-                    for (int l = 0; l < 64; ++l) {
-                        for (int k = 0; k < 6; ++k) {            // G[s0 + 16t + (l&15)][r0 + 4k + (l>>4)]
-                            const int n = s0v[b] + 16 * t + (l & 15), col = r0 + 4 * k + (l >> 4);
-                            if (n < khi && col < r0 + DSCE_RB && col < LK)
-                                g[((size_t)t * 6 + k) * 64 + l] = s.G[(size_t)col * N + n];
-                        }
-                        for (int k = 0; k < ksq; ++k) {          // Q^H[r0 + 16t + (l&15)][klo + 4k + (l>>4)]
-                            const int r = 16 * t + (l & 15), n = klo + 4 * k + (l >> 4);
-                            if (r < nr && n < khi)
-                                q[((size_t)t * ksq + k) * 64 + l] = s.qband.vals[s.qband.off[b] + (size_t)(n - klo) * DSCE_RB + r];
-                        }
-                    }
-            }
-            s.k.pm_ksq = ksq;
-            s.k.pm_stride = stride;
-            s.k.pm_a = dupload(c, pa);
-        }
+        s.k.pic_ok = ok && nb > 0 ? 1 : 0;
         // FFT form (SchemeK::pf_ok): 24-row blocks, 24-sample windows, G / Q^H
         // equal to gs w^(l m) / qs w^(-l m) (w = e^(2 pi i / 24), m = n - klo) to
         // 1e-12 relative, and the md samples before the window a cyclic prefix
@@ -717,12 +670,18 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 // Operator of the structured MMSE IC (k_mic_fft): D_hat = Q' H_hat G with the
 // estimated taps H_hat = Bv hP (setup_bv).  Eligible: FFT-form OFDM blocks
 // (SchemeK::pf_ok), the fused stage's pilot pre-pass (Wpil), NP = 16, at most two
-// taps with delays <= 1.  Kept only if diag(Q' H_hat G) reproduces the diagonal
-// of the thresholded W (Wd) of every (variant, SNR) slice to within the 1e-8
-// threshold plus 1e-9 relative: the check that the 1e-8 sparsification of
-// script:264-265 / :287-289 drops nothing the IC chain would see.
+// taps with delays <= 1.  Kept only if Q' H_hat G reproduces EVERY entry of the
+// thresholded W of every (variant, SNR) slice — the diagonal (Wd, the one-tap
+// channel of script:428/:515) and the off-diagonal entries the IC subtraction
+// uses (the packed band, script:482-484), zero across FFT blocks — to within the
+// threshold plus 1e-9 relative: the check that the sparsification of R_Dij,hP
+// and W (script:264-265, :287-289, :306-308) drops nothing the IC chain would see.
+//
+// In FFT form block b of Q' H_hat_p G is, with w = e^(2 pi i / 24), m = n - klo_b,
+//   D_p[lr, lc] = qs gs sum_q w^(-lc d_q) F_q[lc - lr],  F_q[k] = sum_m w^(k m) Bv[q][klo_b + m][p]
+// (Q^H row lr = qs w^(-lr m), G column lc = gs w^(lc m), cyclic over the prefix).
 void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, const double2* rinv) {
-    const int NP = s.d.n_pilots, LK = s.LK, nsl = 2 * c->nsnr, nt = c->ch.ntap;
+    const int NP = s.d.n_pilots, LK = s.LK, N = s.N, nsl = 2 * c->nsnr, nt = c->ch.ntap;
     const int nblk = s.k.QH.nblk;
     bool ok = s.k.pf_ok && s.Wpil && NP == 16 && nt >= 1 && nt <= 2;
     for (int q = 0; q < nt && ok; ++q) ok = c->ch.tap_delay[q] <= 1;
@@ -731,30 +690,93 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
     s.Bv = dalloc<double2>(c, (size_t)nsl * nt * s.N * NP);
     s.Bs = dalloc<double2>(c, (size_t)nsl * nblk * nt * NP);
     setup_bv(c->stream, a, nsl, m, rinv, s.Bv, nblk, s.k.QH.klo, 24, s.Bs);
-    std::vector<double2> bs((size_t)nsl * nblk * nt * NP), wd((size_t)nsl * LK * NP);
-    DSCE_HIP_CHECK(hipMemcpyAsync(bs.data(), s.Bs, bs.size() * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    std::vector<double2> bv((size_t)nsl * nt * N * NP), wd((size_t)nsl * LK * NP), wb((size_t)nsl * s.w_elems);
+    DSCE_HIP_CHECK(hipMemcpyAsync(bv.data(), s.Bv, bv.size() * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     DSCE_HIP_CHECK(hipMemcpyAsync(wd.data(), s.Wd, wd.size() * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
+    DSCE_HIP_CHECK(hipMemcpyAsync(wb.data(), s.W, wb.size() * sizeof(double2), hipMemcpyDeviceToHost, c->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(c->stream));
     const double2 ps = s.k.pf_scale;
+    // FFT block of each row (-1: none)
+    std::vector<int> fblk(LK, -1);
+    for (int b = 0; b < nblk; ++b)
+        for (int lr = 0; lr < 24; ++lr) fblk[s.qband.row0[b] + lr] = b;
+    std::vector<double2> wpow(24);
+    for (int e = 0; e < 24; ++e) wpow[e] = make_double2(std::cos(2.0 * M_PI * e / 24.0), std::sin(2.0 * M_PI * e / 24.0));
+    const HostBand& wbnd = s.wband;
+    // D[sl][b][p][lr][lc] of one slice at a time
+    std::vector<double2> F((size_t)nt * 24), Ds((size_t)nblk * NP * 576);
+    std::vector<char> seen((size_t)nblk * 576);
     double worst = 0.0;
     for (int sl = 0; sl < nsl; ++sl) {
         double mx = 0.0, md = 0.0;
-        for (int i = 0; i < LK * NP; ++i) mx = std::max(mx, std::hypot(wd[(size_t)sl * LK * NP + i].x, wd[(size_t)sl * LK * NP + i].y));
-        for (int b = 0; b < nblk; ++b)
-            for (int lr = 0; lr < 24; ++lr) {
-                const double ang = -2.0 * M_PI * lr / 24.0;
-                const double2 wl = make_double2(std::cos(ang), std::sin(ang));
-                for (int p = 0; p < NP; ++p) {
-                    double2 acc = make_double2(0, 0);
-                    for (int q = 0; q < nt; ++q) {
-                        const double2 v = bs[(((size_t)sl * nblk + b) * nt + q) * NP + p];
-                        acc = c_add(acc, c->ch.tap_delay[q] ? c_mul(wl, v) : v);
+        const double2* wds = wd.data() + (size_t)sl * LK * NP;
+        const double2* wbs = wb.data() + (size_t)sl * s.w_elems;
+        for (int i = 0; i < LK * NP; ++i) mx = std::max(mx, std::hypot(wds[i].x, wds[i].y));
+        for (long long i = 0; i < s.w_elems; ++i) mx = std::max(mx, std::hypot(wbs[i].x, wbs[i].y));
+        for (int b = 0; b < nblk; ++b) {
+            const int klo = s.qband.klo[b];
+            for (int p = 0; p < NP; ++p) {
+                for (int q = 0; q < nt; ++q)
+                    for (int k = 0; k < 24; ++k) {
+                        double2 acc = make_double2(0, 0);
+                        for (int mm = 0; mm < 24; ++mm)
+                            acc = c_add(acc, c_mul(wpow[(k * mm) % 24],
+                                                   bv[(((size_t)sl * nt + q) * N + klo + mm) * NP + p]));
+                        F[(size_t)q * 24 + k] = acc;
                     }
-                    acc = c_mul(ps, acc);
-                    const double2 ref = wd[(size_t)sl * LK * NP + (size_t)(s.qband.row0[b] + lr) * NP + p];
-                    md = std::max(md, std::hypot(acc.x - ref.x, acc.y - ref.y));
+                for (int lr = 0; lr < 24; ++lr)
+                    for (int lc = 0; lc < 24; ++lc) {
+                        double2 acc = make_double2(0, 0);
+                        for (int q = 0; q < nt; ++q)
+                            acc = c_add(acc, c_mul(wpow[(24 - (lc * c->ch.tap_delay[q]) % 24) % 24],
+                                                   F[(size_t)q * 24 + (lc - lr + 24) % 24]));
+                        Ds[((size_t)b * NP + p) * 576 + lr * 24 + lc] = c_mul(ps, acc);
+                    }
+            }
+        }
+        // diagonal: Wd
+        for (int r = 0; r < LK; ++r) {
+            const int b = fblk[r];
+            for (int p = 0; p < NP; ++p) {
+                const double2 ref = wds[(size_t)r * NP + p];
+                double2 st = make_double2(0, 0);
+                if (b >= 0) {
+                    const int lr = r - s.qband.row0[b];
+                    st = Ds[((size_t)b * NP + p) * 576 + lr * 24 + lr];
+                }
+                md = std::max(md, std::hypot(st.x - ref.x, st.y - ref.y));
+            }
+        }
+        // off-diagonal: every entry of the (trimmed) band, then the in-block
+        // pairs the band does not hold (W = 0 there)
+        std::fill(seen.begin(), seen.end(), 0);
+        for (size_t blk = 0; blk < wbnd.row0.size(); ++blk) {
+            const int clo = wbnd.klo[blk] / NP, chi = wbnd.khi[blk] / NP;
+            for (int rl = 0; rl < wbnd.nrows[blk]; ++rl) {
+                const int r = wbnd.row0[blk] + rl, b = fblk[r];
+                for (int cc = clo; cc < chi; ++cc) {
+                    if (cc == r) continue;
+                    const bool inb = b >= 0 && fblk[cc] == b;
+                    if (inb) seen[(size_t)b * 576 + (r - s.qband.row0[b]) * 24 + (cc - s.qband.row0[b])] = 1;
+                    for (int p = 0; p < NP; ++p) {
+                        const double2 w = wbs[wbnd.off[blk] + ((size_t)(cc - clo) * NP + p) * wbnd.rb + rl];
+                        double2 st = make_double2(0, 0);
+                        if (inb)
+                            st = Ds[((size_t)b * NP + p) * 576 + (r - s.qband.row0[b]) * 24 + (cc - s.qband.row0[b])];
+                        md = std::max(md, std::hypot(st.x - w.x, st.y - w.y));
+                    }
                 }
             }
+        }
+        for (int b = 0; b < nblk; ++b)
+            for (int lr = 0; lr < 24; ++lr)
+                for (int lc = 0; lc < 24; ++lc) {
+                    if (lr == lc || seen[(size_t)b * 576 + lr * 24 + lc]) continue;
+                    for (int p = 0; p < NP; ++p) {
+                        const double2 st = Ds[((size_t)b * NP + p) * 576 + lr * 24 + lc];
+                        md = std::max(md, std::hypot(st.x, st.y));
+                    }
+                }
         worst = std::max(worst, md / (a.thr + 1e-9 * mx));
     }
     s.mic_check = worst;
@@ -764,18 +786,20 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
         s.Bv = s.Bs = nullptr;
         return;
     }
-    std::vector<int> pb, pm(nblk, 0);
+    std::vector<int> pb, db, pm(nblk, 0);
     for (int b = 0; b < nblk; ++b) {
         bool has = false;
         for (int p : s.pilot_pos) has |= p >= s.qband.row0[b] && p < s.qband.row0[b] + s.qband.nrows[b];
-        if (has) pb.push_back(b);
+        (has ? pb : db).push_back(b);
         pm[b] = has ? 1 : 0;
     }
     s.npb = (int)pb.size();
+    s.ndb = (int)db.size();
     if (s.npb) {
         s.pblk = dupload(c, pb);
         s.pmask = dupload(c, pm);
     }
+    if (s.ndb) s.dblk = dupload(c, db);
 }
 
 // ---------------------------------------------------------------------------
@@ -801,9 +825,10 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         if (s.Bs) free_alloc(c, s.Bs);
         if (s.pblk) free_alloc(c, s.pblk);
         if (s.pmask) free_alloc(c, s.pmask);
+        if (s.dblk) free_alloc(c, s.dblk);
         s.Bv = s.Bs = nullptr;
-        s.pblk = s.pmask = nullptr;
-        s.npb = 0;
+        s.pblk = s.pmask = s.dblk = nullptr;
+        s.npb = s.ndb = 0;
         s.W = s.Wd = s.Wp = nullptr;
         s.Wp3 = nullptr;
         s.Wpil = s.WdA = nullptr;
@@ -934,7 +959,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
         NP = std::max<size_t>(NP, s->d.n_pilots);
         ND = std::max<size_t>(ND, s->d.n_data);
     }
-    const size_t key[6] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c)};
+    const size_t key[7] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c), (size_t)c->niter};
     if (memcmp(key, c->buf_key, sizeof(key)) == 0) return;
     for (void* p : c->buf_allocs) (void)hipFree(p);
     c->buf_allocs.clear();
@@ -973,6 +998,9 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.sidr = dalloc<uint16_t>(c, (LK + 32) * R, L);
     b.qre = dalloc<uint16_t>(c, LK * U, L);
     b.qrp = dalloc<uint16_t>(c, LK * U, L);
+    // LS pilot estimates of every stage (k_mic_pilot -> k_mic_data)
+    b.hpa_stages = c->niter + 1;
+    b.hpa = dalloc<double2>(c, (size_t)b.hpa_stages * NP * U, L);
     DSCE_HIP_CHECK(hipMemsetAsync(b.sidr, 0, (LK + 32) * R * sizeof(uint16_t), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));
@@ -1028,10 +1056,14 @@ void copy_col(dsce_ctx* c, double* dst, const double2* src, int rows, int stride
 
 int var_of_stage(int stage, int niter) { return (stage == 0 || stage <= niter / 2) ? 0 : 1; }
 
-void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
+// Realisations [rep0, rep0 + R) with R a multiple of 64; only the first nvalid
+// add to the counters / MSE sums (the rest pad a run's tail to whole waves).
+void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Trace* tr) {
     McBuffers& b = c->buf;
     const Opts& op = c->op;
+    if (R % 64 || nvalid < 1 || nvalid > R) throw ApiError(DSCE_EINVAL, "run_batch: bad batch geometry");
     b.R = R;
+    b.rvalid = nvalid;
     b.tr = nullptr;
     {
         Timed t(c, "k_jakes");
@@ -1060,6 +1092,8 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
         mm.pblk = s.pblk;
         mm.pmask = s.pmask;
         mm.npb = s.npb;
+        mm.dblk = s.dblk;
+        mm.ndb = s.ndb;
         {
             Timed t(c, "tx");
             b.U = R * std::min(chunk, c->nsnr);
@@ -1085,13 +1119,31 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
             }
             if (to && to->y) copy_col(c, to->y, b.y, LK, b.U, tunit);
             if (to && to->h_perfect) copy_col(c, to->h_perfect, b.h, LK, R, tr->lane);
+            // FFT-form OFDM (mic2): the perfect-CSI branch is one k_pic_fft with its
+            // stage 0, the MMSE branch k_mic_pilot + k_mic_data, every stage each
+            if (pfuse && mmse_stages_ok(op, s.k, mm, c->ch, b, c->niter)) {
+                PerfectDetectArgs pd{c->d_counters, (int)si, 0, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
+                {
+                    Timed t(c, "perfect_ic");
+                    s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, false, true);
+                }
+                {
+                    Timed t(c, "k_mic_stages");
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd);
+                }
+                if (to && to->hp_stages)
+                    for (int st = 0; st <= c->niter; ++st)
+                        copy_col(c, to->hp_stages + (size_t)2 * st * NP, b.hpa + (size_t)st * NP * b.U, NP, b.U, tunit);
+                b.tr = nullptr;
+                continue;
+            }
             // With the perfect-CSI branch fused into perfect_ic, the IC iterations
             // are two independent chains after stage 0: MMSE (contraction ->
             // stage, MFMA-bound) on the main stream and perfect CSI on stream2
             // (Opts::streams = 2), joined before the next chunk.
             const bool two = pfuse && op.streams == 2 && !tracing;
-            // pic_ok schemes (OFDM): the whole perfect-CSI chain is one kernel
-            // (k_pic_mfma / k_pic_chain, u in registers across the iterations)
+            // FFT-form OFDM: the whole perfect-CSI chain is one kernel (k_pic_fft,
+            // u in registers across the iterations)
             const bool chain = pfuse && perfect_chain_ok(op, s.k, c->ch, b, c->niter);
             // block-diagonal W + row-local P (OFDM): the MMSE stage of every IC
             // iteration rides in the contraction's epilogue (k_pilot_pre +
@@ -1227,6 +1279,22 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, Trace* tr) {
     DSCE_HIP_CHECK(hipGetLastError());
 }
 
+// Noise sub-streams (include/dsce.h NOISE): SNR index k of noise slot g draws
+// sub-stream snr_base + k + 256 g, a 16-bit field.  With any slot > 0 the SNR
+// part must stay below 256 or the streams of slot g would run into slot g + 1's.
+void check_noise_streams(const dsce_ctx* c, long long base, long long nsnr, int max_slot) {
+    if (max_slot > 0 && base + nsnr > 256)
+        throw ApiError(DSCE_EINVAL, "snr_base + n_snr must be <= 256 when a scheme uses noise slot > 0 (got " +
+                                        std::to_string(base) + " + " + std::to_string(nsnr) + ")");
+    if (base + nsnr + 256LL * max_slot > 65536) throw ApiError(DSCE_EINVAL, "noise sub-stream index exceeds 16 bits");
+}
+
+int max_noise_slot(const dsce_ctx* c) {
+    int m = 0;
+    for (auto& s : c->schemes) m = std::max(m, s->k.noise_slot);
+    return m;
+}
+
 int api_fail(dsce_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
     return code;
@@ -1354,8 +1422,7 @@ int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_
     API_BEGIN
     check_ctx(ctx);
     if (!pn_time || n_snr <= 0 || n_iter < 0) throw ApiError(DSCE_EINVAL, "invalid SNR list");
-    for (auto& s : ctx->schemes)
-        if (s->k.noise_slot > 0 && n_snr > 256) throw ApiError(DSCE_EINVAL, "at most 256 SNR points with noise slots");
+    check_noise_streams(ctx, ctx->op.snr_base, n_snr, max_noise_slot(ctx));
     ctx->pn.assign(pn_time, pn_time + n_snr);
     ctx->nsnr = n_snr;
     ctx->niter = n_iter;
@@ -1482,16 +1549,18 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
     API_BEGIN
     check_ctx(ctx);
     if (!err_counts) throw ApiError(DSCE_EINVAL, "err_counts is null");
-    if (n_rep % 64) throw ApiError(DSCE_EINVAL, "n_rep must be a multiple of 64 (one wavefront of realisations)");
     prepare_run(ctx);
+    // any n_rep (the script's NrRepetitions, script:19 / :44): a tail that is no
+    // multiple of 64 runs as a whole wave whose padding realisations count nothing
     uint64_t done = 0;
     while (done < n_rep) {
         const uint64_t left = n_rep - done;
-        const int R = (int)std::min<uint64_t>((uint64_t)ctx->batch, left);
-        ensure_buffers(ctx, R <= ctx->batch ? ctx->batch : R);
+        const int R = (int)std::min<uint64_t>((uint64_t)ctx->batch, (left + 63) / 64 * 64);
+        const int nvalid = (int)std::min<uint64_t>((uint64_t)R, left);
+        ensure_buffers(ctx, ctx->batch);
         set_mse_buffers(ctx);
-        run_batch(ctx, seed, first_rep + done, R, nullptr);
-        done += (uint64_t)R;
+        run_batch(ctx, seed, first_rep + done, R, nvalid, nullptr);
+        done += (uint64_t)nvalid;
     }
     std::vector<unsigned long long> h(ctx->counters_n);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(unsigned long long),
@@ -1669,13 +1738,19 @@ int dsce_trace_unit_ex(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, i
         tr.k.dec_e = (int*)talloc((size_t)ns * ND * sizeof(int));
         tr.k.dec_p = (int*)talloc((size_t)ns * ND * sizeof(int));
         tr.dev = (TraceK*)talloc(sizeof(TraceK));
-        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yest, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
-        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yperf, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
-        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.hest, 0, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        // all-ones bytes = NaN: "not written by any kernel" (0 is a legitimate value)
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yest, 0xff, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.yperf, 0xff, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        DSCE_HIP_CHECK(hipMemsetAsync(tr.k.hest, 0xff, (size_t)ns * LK * sizeof(double2), ctx->stream));
+        // stages >= 1 of y_est / y_perf: NaN unless the host copies them from a
+        // per-unit buffer (unfused paths) or a kernel writes them (fused paths)
+        for (double* d : {out->yest_stages, out->yperf_stages})
+            if (d)
+                for (size_t i = 2 * (size_t)LK; i < 2 * (size_t)ns * LK; ++i) d[i] = std::nan("");
         DSCE_HIP_CHECK(hipMemsetAsync(tr.k.dec_e, 0xff, (size_t)ns * ND * sizeof(int), ctx->stream));
         DSCE_HIP_CHECK(hipMemsetAsync(tr.k.dec_p, 0xff, (size_t)ns * ND * sizeof(int), ctx->stream));
         // the unit sits at lane 0 of a 64-realisation batch starting at rep
-        run_batch(ctx, seed, rep, 64, &tr);
+        run_batch(ctx, seed, rep, 64, 64, &tr);
         std::vector<double2> ye((size_t)ns * LK), yp((size_t)ns * LK);
         DSCE_HIP_CHECK(hipMemcpyAsync(ye.data(), tr.k.yest, ye.size() * sizeof(double2), hipMemcpyDeviceToHost,
                                       ctx->stream));
@@ -1691,22 +1766,24 @@ int dsce_trace_unit_ex(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, i
             DSCE_HIP_CHECK(hipMemcpyAsync(out->dec_perf, tr.k.dec_p, (size_t)ns * ND * sizeof(int),
                                           hipMemcpyDeviceToHost, ctx->stream));
         DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        // stage 0 of y_est / y_perf is y itself; later stages come from the kernels
-        // (fused paths) unless the host already copied them from y_est / y_perf
-        auto merge = [&](double* dst, const std::vector<double2>& dev, bool copied_unfused) {
+        // stage 0 of y_est / y_perf is y itself; a row of a later stage is what a
+        // kernel wrote (NaN-initialised device trace), else what the host copied
+        // from y_est / y_perf (unfused paths), else NaN (not formed: e.g. pilot
+        // rows of the fused perfect-CSI chains)
+        auto merge = [&](double* dst, const std::vector<double2>& dev) {
             if (!dst) return;
             for (int st = 1; st < ns; ++st)
                 for (int r = 0; r < LK; ++r) {
                     const double2 v = dev[(size_t)st * LK + r];
                     double* d = dst + 2 * ((size_t)st * LK + r);
-                    if (!copied_unfused || v.x != 0.0 || v.y != 0.0) {
+                    if (!std::isnan(v.x)) {
                         d[0] = v.x;
                         d[1] = v.y;
                     }
                 }
         };
-        merge(out->yest_stages, ye, !(s.path & PATH_WPAIR3_FUSED));
-        merge(out->yperf_stages, yp, true);
+        merge(out->yest_stages, ye);
+        merge(out->yperf_stages, yp);
         if (out->y) {
             for (double* d : {out->yest_stages, out->yperf_stages})
                 if (d) memcpy(d, out->y, (size_t)LK * 2 * sizeof(double));
@@ -1764,7 +1841,7 @@ int dsce_set_noise_slot(dsce_ctx* ctx, int32_t id, int32_t slot) {
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
     if (slot < 0 || slot > 255) throw ApiError(DSCE_EINVAL, "noise slot must be 0..255");
-    if (slot > 0 && ctx->nsnr > 256) throw ApiError(DSCE_EINVAL, "at most 256 SNR points with noise slots");
+    check_noise_streams(ctx, ctx->op.snr_base, ctx->nsnr, std::max(slot, max_noise_slot(ctx)));
     s.k.noise_slot = slot;
     API_END
 }
@@ -1844,7 +1921,18 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
     // (ntap x 24 x NP), this stage's window sums (ntap x NP), the channel (ntap x
     // 24), both diag(D_hat) terms (2 x 24) and two DFT-24 at 5 n log2 n flops
     // (counted as flops / 8 CMACs)
-    if (cmac && (s.path & PATH_MIC_FFT)) {
+    if (cmac && (s.path & PATH_MIC_STAGES)) {
+        // k_mic_data (the bench's roofline kernel), per unit and data symbol:
+        // stage 0 window sums (ntap x NP) + diag(D_hat) / one-tap (24); every
+        // IC stage the estimated taps (ntap x 24 x NP), their window sums
+        // (ntap x 24), the channel (ntap x 24), diag(D_hat_prev) v (24), this
+        // stage's window sums (ntap x NP) and diag (24), two DFT-24 at 5 n log2 n
+        // flops (counted as flops / 8 CMACs)
+        const double nt = ctx->ch.ntap, NP = s.d.n_pilots, it = ctx->niter;
+        const double st0 = nt * NP + 24;
+        const double sti = nt * 24 * NP + nt * 24 + nt * 24 + 24 + nt * NP + 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
+        *cmac = (st0 + it * sti) * s.ndb * ctx->nsnr;
+    } else if (cmac && (s.path & PATH_MIC_FFT)) {
         const double nt = ctx->ch.ntap, NP = s.d.n_pilots;
         const double blk = nt * 24 * NP + nt * NP + nt * 24 + 2 * 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
         *cmac = blk * s.k.QH.nblk * ctx->nsnr * ctx->niter;
@@ -1890,7 +1978,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN
@@ -1904,9 +1992,12 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     if (!slot) throw ApiError(DSCE_EINVAL, "unknown option '" + n + "'");
     if (n == "stage_rb" && value != 4 && value != 8 && value != 16) throw ApiError(DSCE_EINVAL, "stage_rb: 4 | 8 | 16");
     if (n == "jakes_rpw" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "jakes_rpw: 1 | 2");
-    if (n == "pic_chain" && (value < 0 || value > 3)) throw ApiError(DSCE_EINVAL, "pic_chain: 0 | 1 | 2 | 3");
+    if (n == "pic_chain" && value != 0 && value != 3)
+        throw ApiError(DSCE_EINVAL, "pic_chain: 0 (per-iteration passes) | 3 (k_pic_fft); the r01 chains 1 / 2 "
+                                    "(k_pic_chain, k_pic_mfma) were retired in r03");
     if (n == "streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "streams: 1 | 2");
     if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
+    if (n == "snr_base") check_noise_streams(ctx, value, ctx->nsnr, max_noise_slot(ctx));
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;
     API_END

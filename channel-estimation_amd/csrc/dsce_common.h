@@ -151,24 +151,9 @@ struct SchemeK {
     const int* row_pcol;          // LK
     const double2* row_pval;      // LK
     int p_diag;
-    // fused perfect-CSI IC pass (pic_ok: every Q^H block's rows are the G
-    // columns of its own samples, e.g. OFDM symbols): per Q^H block the first
-    // sample s0 = klo - max delay and the dense G rows [s0, khi) x 24 columns
-    // starting at the block's first row, at pic_goff
+    // block-local perfect-CSI IC (pic_ok: every Q^H block's rows are the G
+    // columns of its own samples, e.g. OFDM symbols; precondition of pf_ok)
     int pic_ok;
-    int pic_rows;                 // max over blocks of (khi - s0) + (khi - klo): LDS rows of k_pic
-    const int* pic_s0;
-    const long long* pic_goff;
-    const double2* pic_g;
-    // MFMA form of the perfect-CSI chain (k_pic_mfma; pic_ok blocks with at most
-    // 32 window samples, 28 FFT-window samples, 24 rows, max tap delay <= 1):
-    // per Q^H block the A operands of v_mfma_f64_16x16x4 in lane order,
-    // [tile 2][k-step 6][lane 64] of G (rows = window samples s0.., k = the
-    // block's 24 columns) then [tile 2][k-step pm_ksq][lane 64] of Q^H (rows =
-    // the block's rows, k = samples klo..); block stride pm_stride elements
-    int pm_ok, pm_ksq;
-    long long pm_stride;
-    const double2* pm_a;
     // FFT form of the chain (k_pic_fft): every Q^H block is qs DFT24 over its
     // 24-sample window and every G block gs IDFT24 with a cyclic prefix >= the
     // max tap delay (checked entry by entry at pack time); pf_scale = qs gs

@@ -32,6 +32,8 @@ struct Opts {
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
     int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
+    int mic2 = 1;             // FFT-form OFDM: every MMSE stage in one launch pair (k_mic_pilot + k_mic_data)
+                              // and perfect-CSI stage 0 inside k_pic_fft; 0: per-stage k_stage0_fft / k_mic_fft
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -51,6 +53,7 @@ enum : unsigned {
     PATH_MIC_FFT = 1u << 11,       // k_pilot_pre + k_mic_fft (MMSE IC as Q' H_hat G by FFT, OFDM)
     PATH_TXRX_FFT = 1u << 12,      // k_txrx_fft (TX + channel + noisy receiver front by FFT, OFDM)
     PATH_PILOT_FUSED = 1u << 13,   // k_mic_fft also runs the next iteration's pilot pass (pilot_fuse)
+    PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair (mic2)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -68,6 +71,9 @@ struct TraceK {
 
 struct McBuffers {
     int R;            // repetitions per batch (multiple of 64)
+    int rvalid;       // the first rvalid of them count (a tail batch of a run whose
+                      // length is no multiple of 64 pads the last wave; the padding
+                      // realisations are simulated but add nothing to any counter)
     int nsnr;
     int U;            // units of the current SNR chunk = nchunk * R, unit = (snr - snr0) * R + rep
     int snr0;         // first SNR index of the chunk being processed
@@ -98,6 +104,8 @@ struct McBuffers {
     uint16_t* sidr;   // [LK][R]   transmitted symbol index per data row (row-indexed sidx)
     uint16_t* qre;    // [LK][U]   QIDX chains: MMSE decisions per data row
     uint16_t* qrp;    // [LK][U]   QIDX chains: perfect-CSI decisions per data row
+    double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (mic2), or null
+    int hpa_stages;   // stages hpa holds
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
     const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)
@@ -122,6 +130,8 @@ struct MmseK {
     const double2* Bs;    // [var][snr][QH blk][ntap][NP]: Bv summed over each block's FFT window
     const int* pblk;      // QH blocks holding pilot rows (k_pilot_fft)
     int npb;
+    const int* dblk;      // QH blocks without pilot rows (k_mic_data)
+    int ndb;
     const int* pmask;     // [QH blk]: 1 = holds pilot rows
 };
 
@@ -180,6 +190,12 @@ void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const C
 // chains are index-based: k_ls + k_stage0_fft, decisions into qe / qp
 unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
                            bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd);
+// every MMSE stage (0..n_iter) of such a scheme: k_mic_pilot + k_mic_data (mic2);
+// the perfect-CSI branch then runs k_pic_fft with its stage 0
+bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
+                    int niter);
+unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
+                            const PerfectDetectArgs* pd, int niter, int xcd);
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                          const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,
@@ -192,8 +208,9 @@ bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, con
 // true when the chain is k_pic_fft (the only chain with index-based decisions)
 bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
 // qidx: u from the stage's decision indices (StageArgs::qidx; k_pic_fft only)
+// stage0: k_pic_fft also runs the perfect-CSI stage 0 (one-tap y ./ h) first
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter, bool qidx = false);
+                              const PerfectDetectArgs* pd, int niter, bool qidx = false, bool stage0 = false);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)

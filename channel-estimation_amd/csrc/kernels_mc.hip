@@ -16,6 +16,7 @@
 
 #include <math.h>
 #include <algorithm>
+#include <stdexcept>
 #include <type_traits>
 #include <stdlib.h>
 #include <string.h>
@@ -43,9 +44,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // MSE): sum over units and rows of |h_hat - h|^2 (h = diag(D), the perfect-CSI
 // one-tap channel) into err[(scheme * nsnr + snr) * nstage + stage], and of
 // |h|^2 into pow[scheme * nsnr + snr] at stage 0.  One fp64 atomic per wave.
+// valid = false: the lane's unit is a padding realisation of the batch (its
+// rep index >= McBuffers::rvalid) and contributes nothing.
 __device__ __forceinline__ void flush_mse(double e, double pw, double* err, double* pow, int scheme, int nsnr, int snr,
-                                          int nstage, int stage) {
-    const double te = wave_sum_d(e), tp = wave_sum_d(pw);
+                                          int nstage, int stage, bool valid) {
+    const double te = wave_sum_d(valid ? e : 0.0), tp = wave_sum_d(valid ? pw : 0.0);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(&err[((size_t)scheme * nsnr + snr) * nstage + stage], te);
         if (stage == 0) atomicAdd(&pow[(size_t)scheme * nsnr + snr], tp);
@@ -139,11 +142,12 @@ __device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
 // single-lane atomics; device-scope atomics are issued per wave-instruction, so
 // this is 4x fewer of them.  base = counter index of (scheme, csi 0, edge 0,
 // snr, stage); stride_edge = nsnr * nstage; ncsi = 1 skips the perfect-CSI pair.
+// valid: as flush_mse.
 __device__ __forceinline__ void flush_counts(const int (&cnt)[4], unsigned long long* counters, size_t base,
-                                             size_t stride_edge, int ncsi) {
+                                             size_t stride_edge, int ncsi, bool valid) {
     int t[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) t[k] = wave_sum(cnt[k]);
+    for (int k = 0; k < 4; ++k) t[k] = wave_sum(valid ? cnt[k] : 0);
     const int l = threadIdx.x & 63;
     if (l < 2 * ncsi) {
         const int v = l == 0 ? t[0] : l == 1 ? t[1] : l == 2 ? t[2] : t[3];
@@ -579,10 +583,6 @@ struct StoreSoA {
         p[(size_t)row * stride + lane] = v;
     }
 };
-struct TapDelays {
-    int d[DSCE_MAX_TAPS];
-};
-
 // (H t)[n] = sum_tau IR[tau][n] t[n - d_tau]  (GetConvolutionMatrix, FastFading.m:284).
 // NT > 0: exactly NT taps, unrolled so all 2*NT loads of a column are in flight
 // together (load) before the taps are combined; NT == 0: any tap count, loop.
@@ -671,8 +671,9 @@ struct StorePerfectDetect {
     size_t cidx0;                      // counter index of (scheme, csi=1, edge=0, snr=0, stage)
     int cstride_edge, cstride_snr;
     int U, R, snr0, last, M, nI, nQ, real_detect;
+    int rvalid;                        // realisations of the batch that count (McBuffers::rvalid)
     double idd, sI, sQ;
-    // k_pic_mfma's folded slicer (nearest_lin): f = z scale + offset, top = n - 1
+    // the chains' folded slicer (nearest_lin): f = z scale + offset, top = n - 1
     double scI, ofI, topI, scQ, ofQ, topQ;
     double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
     uint16_t* qd;                      // QIDX chains: the branch's decisions, row-indexed [LK][U] (qre / qrp)
@@ -800,7 +801,8 @@ struct StorePerfectDetect {
         }
     }
     __device__ __forceinline__ void finish(int lane) {
-        const int t0 = wave_sum(c0), t1 = wave_sum(c1);
+        const bool valid = lane % R < rvalid;
+        const int t0 = wave_sum(valid ? c0 : 0), t1 = wave_sum(valid ? c1 : 0);
         const int l = threadIdx.x & 63;
         if (l < 2) {                                         // one atomic instruction, two lanes
             const int snr = snr0 + (lane - (int)threadIdx.x) / R;
@@ -945,210 +947,10 @@ unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const
     return 0;
 }
 
-// ---------------------------------------------------------------------------
-// perfect-CSI interference cancellation product (D - diag h) u = Q'(H(G u)) - h.*u
-// (script:541-543), two banded passes.
-// ---------------------------------------------------------------------------
-// The whole perfect-CSI IC chain (iterations 1..n_iter, script:541-561) in one
-// kernel for pic_ok schemes (OFDM): D = Q'HG is block-diagonal there, so the
-// chain of a (unit, Q^H block) never needs another block, and u (the block's
-// re-precoded perfect-CSI decisions) stays in registers across the iterations.
-// A lane PAIR owns a unit: lane h of the pair holds u and the accumulators of
-// the block's rows 12h..12h+11 (48 + 48 VGPRs instead of 96 + 96 for one lane
-// per unit, so 3 waves/SIMD instead of 1).  Per iteration and sample n of the
-// block window [s0, khi): t[n] = G[n, :] u (each lane its 12 columns, the pair
-// adds the halves with one DPP swap; kept in a sliding window of DMAX + 1
-// samples for the tap delays), (H t)[n] = sum_q IR[q][n] t[n - d_q], and
-// acc += Q^H[rows, n] (H t)[n]; then per row y_perf = y - acc + h u, one-tap
-// equalisation by h, slicer, error counts of stage `it`, and the new decision
-// replaces u.  Only y, h, the taps and the transmitted symbol indices are read
-// (L2-shared by the SNR points of a realisation); nothing but the counters is
-// written.  Replaces n_iter x (G u pass + k_band<LoadChannelApplied,
-// StorePerfectDetect>), which moved t, u and y through HBM every iteration.
-// Block = 256 threads = 128 units of one Q^H block (the block's G rows and
-// Q^H columns staged once in LDS); grid: Q^H blocks x units/128, SNR-fastest
-// XCD-aware order (BandOrder with 128-unit groups).
-static constexpr int PCH_UNITS = 128;
-static constexpr int PCH_HALF = DSCE_RB / 2;
-
-__device__ __forceinline__ double swap_pair(double v) {
-    // exchange with the neighbouring lane (quad_perm [1, 0, 3, 2])
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0xb1, 0xf, 0xf, false),
-                            __builtin_amdgcn_mov_dpp(lo, 0xb1, 0xf, 0xf, false));
-}
-
-template <int NT, int DMAX>
-__global__ void __launch_bounds__(256) k_pic_chain(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N,
-                                                   TapDelays dl, StorePerfectDetect o, int niter) {
-    extern __shared__ double2 pic_lds[];
-    int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
-    const int tid = threadIdx.x, half = tid & 1;
-    const int lane = ug * PCH_UNITS + (tid >> 1);             // unit
-    const int U = o.U, R = o.R, rl = lane % R;
-    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk], khi = sk.QH.khi[blk];
-    const int s0 = sk.pic_s0[blk];
-    const int rh = PCH_HALF * half;                           // first row / column of this lane's half
-    // LDS: constellation (256) + slicer tables, then the block's G rows [s0, khi)
-    // x 24 and Q^H columns [klo, khi) x 24 (read as broadcasts)
-    double2* sym = pic_lds;
-    SlicerLds* slt = (SlicerLds*)(pic_lds + 256);
-    double2* sg = pic_lds + 256 + (sizeof(SlicerLds) + 15) / 16;
-    const int ng = (khi - s0) * DSCE_RB, nq = (khi - klo) * DSCE_RB;
-    double2* sq = sg + ng;
-    {
-        const double2* __restrict__ gsrc = sk.pic_g + sk.pic_goff[blk];
-        const double2* __restrict__ qsrc = sk.QH.vals + sk.QH.off[blk];
-        const double2 sv = tid < o.M ? o.symbols[tid] : make_double2(0.0, 0.0);
-        const int gv = tid < o.nI * o.nQ ? o.grid_sym[tid] : 0;
-        const double li = tid < o.nI && tid < 16 ? o.lvI[tid] : 0.0;
-        const double lq = tid < o.nQ && tid < 16 ? o.lvQ[tid] : 0.0;
-        for (int i = tid; i < ng; i += 256) sg[i] = gsrc[i];
-        for (int i = tid; i < nq; i += 256) sq[i] = qsrc[i];
-        sym[tid] = sv;
-        slt->grid[tid] = gv;
-        if (tid < 16) {
-            slt->lvI[tid] = li;
-            slt->lvQ[tid] = lq;
-        }
-    }
-    double2 ur[PCH_HALF];
-#pragma unroll
-    for (int c = 0; c < PCH_HALF; ++c)
-        ur[c] = rh + c < nrows ? o.u[(size_t)(row0 + rh + c) * U + lane] : make_double2(0.0, 0.0);
-    __syncthreads();
-    int dsel[NT];
-#pragma unroll
-    for (int q = 0; q < NT; ++q) dsel[q] = dl.d[q];
-    const int snr = o.snr0 + (ug * PCH_UNITS) / R;
-    for (int it = 1; it <= niter; ++it) {
-        int oz = 0;                                           // opaque zero: no hoisting of the
-        asm volatile("" : "+v"(oz));                          // per-iteration loads out of the loop
-        double2 acc[PCH_HALF];
-#pragma unroll
-        for (int r = 0; r < PCH_HALF; ++r) acc[r] = make_double2(0.0, 0.0);
-        double2 tw[DMAX + 1];
-#pragma unroll
-        for (int j = 0; j <= DMAX; ++j) tw[j] = make_double2(0.0, 0.0);
-        double2 hcur[NT], hnxt[NT];
-#pragma unroll
-        for (int q = 0; q < NT; ++q) hcur[q] = ir[((size_t)q * N + klo + oz) * R + rl];
-        for (int n = s0 + oz; n < khi; ++n) {
-            const bool out_row = n >= klo;
-            if (out_row) {
-                const int nn = n + 1 < khi ? n + 1 : n;
-#pragma unroll
-                for (int q = 0; q < NT; ++q) hnxt[q] = ir[((size_t)q * N + nn) * R + rl];
-            }
-            // t[n] = G[n, :] u: this lane's 12 columns in 3 chains, pair sum by DPP
-            const double2* gr = sg + (n - s0) * DSCE_RB + rh;
-            double2 t0 = make_double2(0.0, 0.0), t1 = t0, t2 = t0;
-#pragma unroll
-            for (int c = 0; c < PCH_HALF; c += 3) {
-                c_fma(t0, gr[c], ur[c]);
-                c_fma(t1, gr[c + 1], ur[c + 1]);
-                c_fma(t2, gr[c + 2], ur[c + 2]);
-            }
-            const double2 tp = c_add(c_add(t0, t1), t2);
-#pragma unroll
-            for (int j = DMAX; j > 0; --j) tw[j] = tw[j - 1];
-            tw[0] = make_double2(tp.x + swap_pair(tp.x), tp.y + swap_pair(tp.y));   // a + b == b + a: same on both lanes
-            if (out_row) {
-                double2 x = make_double2(0.0, 0.0);
-#pragma unroll
-                for (int q = 0; q < NT; ++q) {
-                    double2 tq = tw[0];
-#pragma unroll
-                    for (int j = 1; j <= DMAX; ++j)
-                        if (dsel[q] == j) tq = tw[j];
-                    c_fma(x, hcur[q], tq);
-                }
-                const double2* qk = sq + (n - klo) * DSCE_RB + rh;
-#pragma unroll
-                for (int r = 0; r < PCH_HALF; ++r) c_fma(acc[r], qk[r], x);
-#pragma unroll
-                for (int q = 0; q < NT; ++q) hcur[q] = hnxt[q];
-            }
-        }
-        // epilogue: this lane's 12 rows in groups of 4, every input of a group first
-        int c0 = 0, c1 = 0;
-        const bool last = it == niter;
-#pragma unroll
-        for (int g0 = 0; g0 < PCH_HALF; g0 += 4) {
-            double2 yv[4], hv[4], pv[4];
-            int tx[4], dd[4], cn[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int r = rh + g0 + k;
-                const int row = row0 + (r < nrows ? r : 0) + oz;
-                dd[k] = r < nrows ? o.row_data[row] : -1;
-                cn[k] = o.row_cons[row];
-                pv[k] = o.row_pval[row];
-                yv[k] = o.y[(size_t)row * U + lane];
-                hv[k] = o.h[(size_t)row * R + rl];
-                tx[k] = o.sidx[(size_t)(dd[k] > 0 ? dd[k] : 0) * R + rl];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int r = g0 + k;
-                if (dd[k] < 0) continue;
-                double2 rr = c_sub(yv[k], acc[r]);
-                rr = c_add(rr, c_mul(hv[k], ur[r]));
-                const double2 z = c_div1(rr, hv[k]);
-                const int dp = slice_fast(*slt, o.nI, o.nQ,
-                                          o.real_detect ? make_double2(z.x * o.idd, 0.0)
-                                                        : make_double2(z.x * o.idd, z.y * o.idd),
-                                          o.sI, o.sQ);
-                const int ne = __popc((unsigned)(dp ^ tx[k]));
-                c0 += ne;
-                c1 += cn[k] ? ne : 0;
-                if (o.tr && lane == o.tr->unit) {
-                    o.tr->yperf[(size_t)it * o.tr->LK + row0 + rh + r] = rr;
-                    o.tr->dec_p[(size_t)it * o.tr->ND + dd[k]] = dp;
-                }
-                if (!last) {
-                    double2 av = make_double2(0.0, 0.0);
-                    c_fma(av, pv[k], sym[dp]);
-                    ur[r] = av;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const int s_0 = wave_sum(c0), s_1 = wave_sum(c1);
-        if ((tid & 63) < 2) {
-            const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + ((tid & 1) ? (size_t)o.cstride_edge : 0);
-            const int v = (tid & 1) ? s_1 : s_0;
-            if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
-        }
-    }
-}
-
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 #define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
 
-// ---------------------------------------------------------------------------
-// The perfect-CSI IC chain on the matrix cores (k_pic_mfma, SchemeK::pm_ok: OFDM
-// at C2).  Per Q^H block and IC iteration the chain is two small GEMMs whose A
-// operands are shared by every unit and whose B operands are the units:
-//   T   (window samples x units) = G_blk (samples x 24 columns) U (24 x units)
-//   acc (24 rows x units)        = Q^H_blk (rows x KW samples)  X (KW x units),
-//   X[j][u] = sum_q IR_q[klo + j][u] T[j + maxd - d_q][u]      (H, per unit)
-// on v_mfma_f64_16x16x4_f64 (complex = 4 real MFMAs).  A wave owns 16 units;
-// the D layout (row (lane>>4) + 4 reg, col lane&15) of a 16-row tile register
-// r is exactly the B operand of k-step 4 tile + r, so U (decisions, kept in
-// registers across the iterations) and T feed the next GEMM without data
-// movement; the one-sample shift of the delayed tap is one lane shuffle.  The
-// epilogue (y_perf = y - acc + h u, one-tap by h, slicer, counts, re-precoded
-// decision into U) runs on the D layout of acc, 8 rows per lane.  Only y, h,
-// the taps and the transmitted symbol indices are read; nothing but the
-// counters is written.  Block = 4 waves = 64 units of one Q^H block (its A
-// tables staged in LDS once); grid: Q^H blocks x units/64, SNR-fastest
-// XCD-aware order.
-// f64 MFMA with the A operand negated: the f64 form's blgp field is its neg
-// modifier (bit 0 = neg:[1,0,0]), so -a costs no v_xor / v_mov per k-step
-#define MFMA64NA(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 1)
 
 // Raw buffer view of a wave-uniform base (T8): a 32-bit per-lane byte offset plus
 // a wave-uniform one (SGPR) per load instead of 64-bit address arithmetic.
@@ -1195,12 +997,13 @@ __device__ __forceinline__ double2 qidx_value(bool data, unsigned q, double2 pv,
 // Error counts of a 256-thread block, one atomic per counter per block: every
 // wave packs its totals (errors | no-edge errors << 16, per CSI branch) and
 // wave 0 sums the four waves' words from LDS.  `words` = 1 or 2 branches.
+// valid: as flush_mse.
 __device__ __forceinline__ void block_counts(const int (&packed)[2], int words, int* lds /* [4][2] */,
                                              unsigned long long* counters, size_t base, size_t stride_edge,
-                                             size_t stride_csi) {
+                                             size_t stride_csi, bool valid) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int t0 = wave_sum(packed[0]);
-    const int t1 = words > 1 ? wave_sum(packed[1]) : 0;
+    const int t0 = wave_sum(valid ? packed[0] : 0);
+    const int t1 = words > 1 ? wave_sum(valid ? packed[1] : 0) : 0;
     if (l == 0) {
         lds[2 * w] = t0;
         lds[2 * w + 1] = t1;
@@ -1215,301 +1018,9 @@ __device__ __forceinline__ void block_counts(const int (&packed)[2], int words, 
     }
 }
 
-// SH: bit q set when tap q reads the shifted sample (maxd - d_q = 1), so the
-// tap-delay selects are compile-time.
-//
-// Schedule (software-pipelined across the two row tiles, so the epilogue's
-// VALU / LDS / memory work has independent MFMAs to hide behind):
-//   before the loop      GEMM1 of iteration 1
-//   per iteration it     GEMM2 tile 0 (X formed on the fly and kept)
-//                        GEMM2 tile 1  ||  epilogue tile 0 of it
-//                        GEMM1 k-steps 0-3 of it + 1 (need tile-0 decisions only)
-//                                       ||  epilogue tile 1 of it
-//                        GEMM1 k-steps 4-5 of it + 1
-// Error counts go through LDS per (wave, iteration) and are added to the
-// counters once at the end (no divergent atomic inside the pipelined loop).
+// IC iterations per chain launch (k_pic_fft, k_mic_fft): the per-iteration
+// error counts of a wave go through LDS and are added once at the end.
 static constexpr int PM_MAXIT = 32;
-static constexpr int PM_EPI_VALU = 6;
-
-// N x {1 MFMA, V VALU (+ D LDS reads)} scheduling groups (LLVM SchedGroupMask:
-// MFMA 0x8, VALU 0x2, DS_READ 0x100): the order the compiler emits this
-// region's matrix-core and vector work in
-template <int N, int V, int D>
-__device__ __forceinline__ void sched_interleave() {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x2, V, 0);
-        if (D) __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
-    }
-}
-
-template <int KSQ, int NT, int SH, bool TRACE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
-k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
-    extern __shared__ double2 pm_lds[];
-    int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const int U = o.U, R = o.R;
-    const int unit = ug * WAVE + w * 16 + (l & 15);
-    const int rl = unit % R;
-    const int kq = l >> 4;
-    const int row0 = sk.QH.row0[blk], nrows = sk.QH.nrows[blk], klo = sk.QH.klo[blk];
-    constexpr int NA = (2 * 6 + 2 * KSQ) * 64;
-    double2* sa = pm_lds;                                       // A tables
-    double2* sym = pm_lds + NA;
-    SlicerLds* slt = (SlicerLds*)(sym + 256);
-    // the block's 32 (padded) rows: re-precoding value, data index (-1: pilot or
-    // padding), no-edge flag — read by the epilogue every iteration
-    __shared__ double2 rpv[32];
-    __shared__ int rdc[32];
-    __shared__ double hidl[8][256];                             // 1 / |h|^2 per lane row
-    __shared__ int cntl[4][PM_MAXIT];                           // per wave: n0 + (n1 << 16)
-    {
-        // every global load of the prologue is issued before the first wait
-        // (clamped indices, masked values): guarded loads would each be a branch
-        // with its own vmcnt(0), a chain of serial round trips per block
-        const double2* __restrict__ src = sk.pm_a + (size_t)sk.pm_stride * blk;
-        constexpr int NIT = (NA + 255) / 256;
-        double2 av[NIT];
-#pragma unroll
-        for (int k = 0; k < NIT; ++k) av[k] = src[min(tid + 256 * k, NA - 1)];
-        const double2 sv = o.symbols[min(tid, o.M - 1)];
-        const int gv = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
-        const int rt = min(tid, 31);
-        const int row = row0 + (rt < nrows ? rt : 0);
-        const double2 pv = o.row_pval[row];
-        const int dr = o.row_data[row], cs = o.row_cons[row];
-#pragma unroll
-        for (int k = 0; k < NIT; ++k)
-            if (tid + 256 * k < NA) sa[tid + 256 * k] = av[k];
-        sym[tid] = make_double2(tid < o.M ? sv.x : 0.0, tid < o.M ? sv.y : 0.0);
-        slt->grid[tid] = tid < o.nI * o.nQ ? gv : 0;
-        if (tid < 32) {
-            rpv[tid] = pv;
-            // data index << 1 | no-edge flag, or -1
-            rdc[tid] = tid < nrows && dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
-        }
-    }
-    const double2* ga = sa;
-    const double2* qa = sa + 2 * 6 * 64;
-    // y, h and the taps through buffer views based at the block (32-bit offsets;
-    // pic_mfma_ok bounds them).  Rows past the block's last and samples past N
-    // stay inside the allocations (ensure_buffers pads y, h by 32 rows and the
-    // taps by 4 samples, zeroed) and are masked / multiplied by zero columns.
-    const int rmax = nrows - 1;
-    const int ybase = row0 * U + unit, hbase = row0 * R + rl;
-    const __amdgpu_buffer_rsrc_t yrs = buf_rsrc(o.y + (size_t)row0 * U, (size_t)32 * U * sizeof(double2));
-    const __amdgpu_buffer_rsrc_t hrs = buf_rsrc(o.h + (size_t)row0 * R, (size_t)32 * R * sizeof(double2));
-    const __amdgpu_buffer_rsrc_t trs =
-        buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo) + 4) * R * sizeof(double2));
-    const unsigned yv0 = (unsigned)(kq * U + unit) * 16u, hv0 = (unsigned)(kq * R + rl) * 16u;
-    // U in D layout: ur[t][r] = u[row0 + 16 t + kq + 4 r][unit]
-    double2 ur[2][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int rr = 16 * t + kq + 4 * r;
-            ur[t][r] = o.u[(unsigned)(ybase + min(rr, rmax) * U)];
-        }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            if (16 * t + kq + 4 * r >= nrows) ur[t][r] = make_double2(0.0, 0.0);
-    // 1 / |h|^2 of the lane's 8 rows (iteration-invariant; LDS, not registers)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int rr = 16 * (i >> 2) + kq + 4 * (i & 3);
-        const double2 hh = o.h[(unsigned)(hbase + min(rr, rmax) * R)];
-        hidl[i][tid] = 1.0 / (hh.x * hh.x + hh.y * hh.y);
-    }
-    __syncthreads();
-    // transmitted symbol indices of the lane's 8 rows, fixed for the whole chain:
-    // loaded once, 8 bits each, packed 4 per register (M <= 256)
-    unsigned txp[2] = {0u, 0u};
-    {
-        unsigned short tv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int dc = rdc[16 * (i >> 2) + kq + 4 * (i & 3)];
-            tv[i] = o.sidx[(size_t)(dc >= 0 ? dc >> 1 : 0) * R + rl];
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) txp[i >> 2] |= ((unsigned)tv[i] & 0xffu) << (8 * (i & 3));
-    }
-    const int src_lane = (l + 16) & 63;
-
-    d4 tre[2], tim[2], are[2], aim[2];
-    double2 xs[KSQ];            // X of every k-step (GEMM2's B operand, reused by tile 1)
-    double2 hnext[NT];          // taps of GEMM2's first k-step, requested during GEMM1
-    int ncnt = 0;               // this lane's errors of the current iteration: n0 + (n1 << 16)
-
-    // tap q, sample klo + 4 k + kq: (q N + 4 k) R + kq R + rl past the block base
-    auto ld_taps = [&](int k, double2(&hv)[NT], int oz) {
-#pragma unroll
-        for (int q = 0; q < NT; ++q) hv[q] = buf_ld2(trs, hv0 + (unsigned)oz, (unsigned)((q * N + 4 * k) * R) * 16u);
-    };
-    // GEMM1 k-steps [KB, KE): T += G U (both row tiles)
-    auto gemm1 = [&](auto kb, auto ke) {
-#pragma unroll
-        for (int k = decltype(kb)::value; k < decltype(ke)::value; ++k) {
-            const double2 b = ur[k >> 2][k & 3];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const double2 a = ga[(t * 6 + k) * 64 + l];
-                tre[t] = MFMA64(a.x, b.x, tre[t]);
-                tre[t] = MFMA64NA(a.y, b.y, tre[t]);
-                tim[t] = MFMA64(a.x, b.y, tim[t]);
-                tim[t] = MFMA64(a.y, b.x, tim[t]);
-            }
-        }
-    };
-    // GEMM2 tile 0 with X in B layout formed on the fly (k-step s: sample
-    // klo + 4 s + kq): X[j] = sum_q IR_q[klo + j] T[j + maxd - d_q]
-    auto gemm2_t0 = [&](int oz) {
-#pragma unroll
-        for (int k = 0; k < KSQ; ++k) {
-            // T row j = 4k + kq is register (k&3) of tile k>>2 in this lane; row
-            // j + 1 comes from lane l + 16 (register k), or for kq == 3 from lane
-            // l - 48 (register k + 1)
-            const double2 tc = make_double2(tre[k >> 2][k & 3], tim[k >> 2][k & 3]);
-            const int kn = k + 1 < 8 ? k + 1 : 7;
-            const double2 tn = make_double2(tre[kn >> 2][kn & 3], tim[kn >> 2][kn & 3]);
-            const double2 sv = l >= 16 ? tc : tn;
-            const double2 t1 = make_double2(__shfl(sv.x, src_lane), __shfl(sv.y, src_lane));
-            double2 hcur[NT];
-#pragma unroll
-            for (int q = 0; q < NT; ++q) hcur[q] = hnext[q];
-            if (k + 1 < KSQ) ld_taps(k + 1, hnext, oz);
-            double2 x = make_double2(0.0, 0.0);
-            c_fma(x, hcur[0], (SH & 1) ? t1 : tc);
-            if (NT > 1) c_fma(x, hcur[NT > 1 ? 1 : 0], (SH & 2) ? t1 : tc);
-            xs[k] = x;
-            const double2 a = qa[k * 64 + l];
-            are[0] = MFMA64(a.x, x.x, are[0]);
-            are[0] = MFMA64NA(a.y, x.y, are[0]);
-            aim[0] = MFMA64(a.x, x.y, aim[0]);
-            aim[0] = MFMA64(a.y, x.x, aim[0]);
-        }
-    };
-    auto gemm2_t1 = [&]() {
-#pragma unroll
-        for (int k = 0; k < KSQ; ++k) {
-            const double2 a = qa[(KSQ + k) * 64 + l];
-            const double2 x = xs[k];
-            are[1] = MFMA64(a.x, x.x, are[1]);
-            are[1] = MFMA64NA(a.y, x.y, are[1]);
-            aim[1] = MFMA64(a.x, x.y, aim[1]);
-            aim[1] = MFMA64(a.y, x.x, aim[1]);
-        }
-    };
-    // epilogue of tile t on the D layout of acc: the lane's rows 16 t + kq + 4 r
-    // (register r), branch-free: y_perf = y - acc + h u, one-tap by h, slicer,
-    // counts, re-precoded decision into ur (pilot / padding rows are computed and
-    // masked; after the last iteration the new decisions are simply unused)
-    auto epi = [&](auto tcst, int it, int oz) {
-        constexpr int t = decltype(tcst)::value;
-        double2 yv[4], hv[4];
-        int dc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            dc[r] = rdc[16 * t + kq + 4 * r];
-            yv[r] = buf_ld2(yrs, yv0 + (unsigned)oz, (unsigned)((16 * t + 4 * r) * U) * 16u);
-            hv[r] = buf_ld2(hrs, hv0 + (unsigned)oz, (unsigned)((16 * t + 4 * r) * R) * 16u);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            // one-tap z = y_perf / h with y_perf = y - acc + h u, as (y - acc) / h + u
-            const double2 d = c_sub(yv[r], make_double2(are[t][r], aim[t][r]));
-            const double id = hidl[4 * t + r][tid];
-            const double zx = fma(fma(d.x, hv[r].x, d.y * hv[r].y), id, ur[t][r].x);
-            const double zy = fma(fma(d.y, hv[r].x, -(d.x * hv[r].y)), id, ur[t][r].y);
-            int tI, tQ;
-            const int iI = nearest_lin(zx, o.scI, o.ofI, o.topI, tI);
-            const int iQ = nearest_lin(zy, o.scQ, o.ofQ, o.topQ, tQ);
-            // a decision exactly on a mid-point: the smallest symbol index among the
-            // tied grid points (MATLAB min's first index); otherwise all four
-            // reads are the same entry
-            const int jI = max(iI - tI, 0), jQ = max(iQ - tQ, 0);
-            const int iIn = __umul24(iI, o.nQ), jIn = __umul24(jI, o.nQ);
-            const int dp = min(min(slt->grid[iIn + iQ], slt->grid[jIn + iQ]),
-                               min(slt->grid[iIn + jQ], slt->grid[jIn + jQ]));
-            const bool data = dc[r] >= 0;
-            const int ne = data ? __popc((unsigned)(dp ^ (int)((txp[t] >> (8 * r)) & 0xffu))) : 0;
-            ncnt += ne + ((dc[r] & 1) ? ne << 16 : 0);
-            if (TRACE && data && unit == o.tr->unit) {
-                o.tr->yperf[(size_t)it * o.tr->LK + row0 + 16 * t + kq + 4 * r] = c_add(d, c_mul(hv[r], ur[t][r]));
-                o.tr->dec_p[(size_t)it * o.tr->ND + (dc[r] >> 1)] = dp;
-            }
-            double2 av = make_double2(0.0, 0.0);
-            c_fma(av, rpv[16 * t + kq + 4 * r], sym[dp]);
-            // component-wise select (a struct-valued ?: became an address select
-            // through scratch)
-            ur[t][r].x = data ? av.x : ur[t][r].x;
-            ur[t][r].y = data ? av.y : ur[t][r].y;
-        }
-    };
-    auto flush = [&](int it) {
-        // wave total of iteration it (uniform: every lane writes the same word)
-        cntl[w][it - 1] = wave_sum(ncnt);
-        ncnt = 0;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I4 = std::integral_constant<int, 4>;
-    using I6 = std::integral_constant<int, 6>;
-
-    {
-        int oz = 0;
-        asm volatile("" : "+v"(oz));
-#pragma unroll
-        for (int t = 0; t < 2; ++t) tre[t] = tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
-        ld_taps(0, hnext, oz);
-        gemm1(I0{}, I6{});
-    }
-    for (int it = 1;; ++it) {
-        // the loads below are the same every iteration: an opaque zero keeps the
-        // compiler from hoisting them out of the loop (they would stay live
-        // across it and triple the register footprint)
-        int oz = 0;
-        asm volatile("" : "+v"(oz));
-#pragma unroll
-        for (int t = 0; t < 2; ++t) are[t] = aim[t] = (d4){0.0, 0.0, 0.0, 0.0};
-        gemm2_t0(oz);
-        gemm2_t1();
-        epi(I0{}, it, oz);
-        // interleave: GEMM2 tile 0 with the X formation, then one MFMA of tile 1
-        // between every few epilogue instructions of tile 0
-        sched_interleave<KSQ * 4, 5, 0>();
-        sched_interleave<KSQ * 4, PM_EPI_VALU, 1>();
-        if (it == niter) break;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) tre[t] = tim[t] = (d4){0.0, 0.0, 0.0, 0.0};
-        ld_taps(0, hnext, oz);
-        gemm1(I0{}, I4{});
-        epi(I1{}, it, oz);
-        flush(it);
-        gemm1(I4{}, I6{});
-        sched_interleave<32, PM_EPI_VALU, 1>();
-    }
-    {
-        int oz = 0;
-        asm volatile("" : "+v"(oz));
-        epi(I1{}, niter, oz);
-        flush(niter);
-    }
-    // counters of every iteration: lane 2 (it - 1) + edge of each wave
-    if (l < 2 * niter) {
-        const int it = (l >> 1) + 1, edge = l & 1;
-        const int v = (cntl[w][it - 1] >> (16 * edge)) & 0xffff;
-        const int snr = o.snr0 + (ug * WAVE) / R;
-        const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
-        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
-    }
-}
 
 // ---------------------------------------------------------------------------
 // The perfect-CSI IC chain of OFDM by FFT on the VALU (k_pic_fft, SchemeK::pf_ok).
@@ -1517,8 +1028,8 @@ k_pic_mfma(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Sto
 // Q^H block of symbol k is qs * DFT and its G block is gs * IDFT with a cyclic
 // prefix (OFDM.m GetTXMatrix / GetRXMatrix; pack_scheme verifies every entry),
 // so (Q'HG u)_blk = qs gs FFT24(h_0 .* t + h_1 .* t(-1)), t = IFFT24(u): ~10x
-// fewer flops than the two dense 24 x 24 products k_pic_mfma runs on the matrix
-// cores — and on gfx950 f64 MFMA and VALU work do not overlap
+// fewer flops than two dense 24 x 24 products on the matrix cores (the r01
+// k_pic_mfma) — and on gfx950 f64 MFMA and VALU work do not overlap
 // (profiles/r02_mfma_valu_overlap.txt), so the flop count is what matters.
 // ---------------------------------------------------------------------------
 __constant__ double2 kW24[12] = {
@@ -1602,7 +1113,11 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // y, h and the taps: 4.45 / 5.25 ms vs 2.57 ms per 65536-realisation launch).
 // Block = 256 threads = 64 units of one symbol; grid: symbols x units/64,
 // SNR-fastest XCD-aware order.
-template <int NT, int SH, bool TRACE, bool QIDX>
+// S0 (r03, with k_mic_pilot / k_mic_data): the chain also runs stage 0 of the
+// perfect-CSI branch, the one-tap x = y ./ h (script:450-466), so no stage
+// kernel runs in front: u starts as P [xP; 0] (xs of the pilot rows) and the
+// data rows get the stage-0 decisions in registers.
+template <int NT, int SH, bool TRACE, bool QIDX, bool S0 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     int ug, blk;
@@ -1619,7 +1134,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     __shared__ int rdc[24];
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
     __shared__ double2 twb[2][4];                               // quad-network twiddle of lane r
-    __shared__ int cntl[4][PM_MAXIT];
+    __shared__ int cntl[4][PM_MAXIT + 1];                      // [wave][stage]
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
     // and the channel taps of the lane's samples (registers for all iterations)
     double2 u[6], yh[6], hc[6];
@@ -1643,7 +1158,8 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
 #pragma unroll
         for (int b = 0; b < 6; ++b) {
             const int row = row0 + 4 * b + r;
-            if (QIDX) qv[b] = o.qd[(size_t)row * U + unit];
+            if (S0) u[b] = o.xs[(size_t)row * R + rl];
+            else if (QIDX) qv[b] = o.qd[(size_t)row * U + unit];
             else u[b] = o.u[(size_t)row * U + unit];
             txp[b >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (b & 3));
             yh[b] = o.y[(size_t)row * U + unit];
@@ -1680,13 +1196,53 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    if (QIDX)
+    if (QIDX && !S0)
 #pragma unroll
         for (int a = 0; a < 6; ++a)
             u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
                               (size_t)(row0 + 4 * a + r) * R + rl);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     int ncnt = 0;
+    if (S0) {
+        // stage 0: y / h and 1 / h now, one-tap z = y / h, slicer, counts, decisions
+        int code[6], dp[6];
+        int anytie = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const double2 hh = hc[a], yv = yh[a];
+            const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+            hc[a] = make_double2(hh.x * id, -hh.y * id);
+            yh[a] = c_mulf(yv, hc[a]);
+            int tI, tQ;
+            const int iI = nearest_lin(yh[a].x, o.scI, o.ofI, o.topI, tI);
+            const int iQ = nearest_lin(yh[a].y, o.scQ, o.ofQ, o.topQ, tQ);
+            code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
+            anytie |= tI | tQ;
+            dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+        }
+        if (__ballot(anytie)) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
+                const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
+                dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
+                            min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const bool data = (dmask >> a) & 1;
+            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
+            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)(rdc[4 * a + r] >> 1)] = dp[a];
+            double2 nv = make_double2(0.0, 0.0);
+            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
+            u[a].x = data ? nv.x : u[a].x;
+            u[a].y = data ? nv.y : u[a].y;
+        }
+        cntl[w][0] = wave_sum(rl < o.rvalid ? ncnt : 0);
+        ncnt = 0;
+    }
     for (int it = 1; it <= niter; ++it) {
         // an opaque zero keeps the per-iteration LDS twiddle reads inside the loop
         // (hoisted, they would hold 56 more registers)
@@ -1734,8 +1290,8 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         }
         dft6<-1>(x);
         // y / h and 1 / h at the first epilogue (not before the loop): the
-        // first chain runs while y and h are still in flight
-        if (it == 1)
+        // first chain runs while y and h are still in flight (S0: formed above)
+        if (it == 1 && !S0)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double2 hh = hc[a], yv = yh[a];
@@ -1786,17 +1342,18 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             u[a].x = data ? nv.x : u[a].x;
             u[a].y = data ? nv.y : u[a].y;
         }
-        cntl[w][it - 1] = wave_sum(ncnt);    // uniform: every lane writes the same word
+        cntl[w][it] = wave_sum(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
     }
-    // counters of every iteration, summed over the block's 4 waves: thread
-    // 2 (it - 1) + edge issues the block's one atomic per counter
+    // counters of every stage, summed over the block's 4 waves: thread
+    // 2 (it - it0) + edge issues the block's one atomic per counter
     __syncthreads();
-    if (tid < 2 * niter) {
-        const int it = (tid >> 1) + 1, edge = tid & 1;
+    constexpr int it0 = S0 ? 0 : 1;
+    if (tid < 2 * (niter + 1 - it0)) {
+        const int it = (tid >> 1) + it0, edge = tid & 1;
         int v = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v += (cntl[k][it - 1] >> (16 * edge)) & 0xffff;
+        for (int k = 0; k < 4; ++k) v += (cntl[k][it] >> (16 * edge)) & 0xffff;
         const int snr = o.snr0 + (ug * WAVE) / R;
         const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
         if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
@@ -2231,9 +1788,10 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         __shared__ int bcnt[8];
         const int pk[2] = {ncnt, 0};
         block_counts(pk, 1, bcnt, o.counters, o.cidx0 + (size_t)ma.stage + (size_t)snr * o.cstride_snr,
-                     (size_t)o.cstride_edge, 0);
+                     (size_t)o.cstride_edge, 0, rl < o.rvalid);
     }
-    if (ma.mse_err) flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage);
+    if (ma.mse_err)
+        flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage, rl < o.rvalid);
     if (fz) {
         // the next iteration's pilot pass (PILOT mode above) on this symbol:
         // u = this iteration's decisions, taps Bv(var_cur) hp_new from the
@@ -2405,9 +1963,470 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
         __shared__ int bcnt[8];
         const int pk[2] = {cnt[0] | (cnt[1] << 16), cnt[2] | (cnt[3] << 16)};
         block_counts(pk, 2, bcnt, counters, (((size_t)ma.scheme * 4) * ma.nsnr + snr) * ma.nstage,
-                     (size_t)ma.nsnr * ma.nstage, 2 * (size_t)ma.nsnr * ma.nstage);
+                     (size_t)ma.nsnr * ma.nstage, 2 * (size_t)ma.nsnr * ma.nstage, rl < o.rvalid);
     }
-    if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0);
+    if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0, rl < o.rvalid);
+}
+
+
+// ---------------------------------------------------------------------------
+// The MMSE branch of an FFT-form OFDM scheme with EVERY stage in one launch
+// (r03; rows a13-a16, script:417-537).  The stages of a symbol depend on other
+// symbols only through the LS pilot estimates hP_s (script:487-489), and those
+// come from the pilot symbols alone: y_ic of a pilot symbol at stage s needs
+// only that symbol's stage s - 1 decisions and hP_{s-1}.  So
+//   k_mic_pilot: the npb pilot symbols of 16 units per block (one wave per
+//                symbol), stages 0..niter; per stage y_ic (stage 0: y), LS at
+//                the pilot rows -> hP_s exchanged through LDS (one barrier),
+//                diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q hP_s, one-tap,
+//                detection, counts; hP_s also to HBM (hpa[s]);
+//   k_mic_data:  every other symbol of 64 units per block, stages 0..niter
+//                from hpa, the decisions v in registers across the stages.
+// Stage s >= 1 of a symbol (either kernel): estimated taps of D_hat_{s-1},
+// hhat[q][n] = sum_p Bv(var_{s-1})[q][n][p] hP_{s-1,p} (k_mic_fft's MFMA GEMM,
+// 3M), y_ic = y - Q'(H_hat (G v)) + diag(D_hat_{s-1}) v by the DFT-24 chain,
+// then the stage's one-tap with diag(D_hat_s) (W up to niter / 2, then W0,
+// script:492).  Replaces k_ls + k_stage0_fft (MMSE branch), the pilot pass and
+// the niter k_mic_fft launches: y, the transmitted indices and the row tables
+// are read once per symbol instead of once per stage, decisions never leave
+// the registers, Bv / Bs of both variants are staged once.
+// The tap GEMM's A rows are ordered quarter-major: tile t row 4c + k is tap
+// index 4t + k (q = idx / 6, window sample 6c + idx % 6) of time quarter c,
+// so after the GEMM the lane quad of a unit reads its quarter's 4 taps of the
+// tile from a 16-row per-wave slab (4.4 KB, reused per tile) instead of the
+// 13 KB slab of all tiles (k_mic_fft): 17 instead of 52 KB of LDS per block.
+// ---------------------------------------------------------------------------
+struct Mic2Args {
+    const double2* __restrict__ bv;   // [var][snr][NT][N][NP]
+    const double2* __restrict__ bs;   // [var][snr][nblk][NT][NP]
+    double2* hpa;                     // [stage][NP][U]: LS pilot estimates of every stage
+    const int* blks;                  // this launch's symbol blocks (k_mic_pilot: the pilot blocks)
+    int nb;
+    double* mse_err;
+    double* mse_pow;
+    int nsnr, N, nblk, niter, scheme;
+};
+
+__device__ __forceinline__ int mic_var(int s, int niter) { return (s == 0 || 2 * s <= niter) ? 0 : 1; }
+
+// Estimated taps of the lane's six window samples (quad layout: lane r of a unit
+// holds samples 6 cq + m) for the 16 units of a wave: MFMA GEMM (3M) with
+// A(q, j, p) = Bv[q][klo + j][p] and B = hP (lane (g, jc): pilots 4 ks + g of
+// unit jc), D tiles through the wave's 16-row slab `sl` (17-unit stride).
+template <int NT, int NP, class ALoad>
+__device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A, const double2 (&hb)[NP / 4],
+                                         double2* sl, int l, int cq) {
+    constexpr int NIDX = 6 * NT, NTILE = (NIDX + 3) / 4, NKS = NP / 4;
+    const int g = l >> 4, jc = l & 15, ca = jc >> 2, ka = jc & 3, ul = l >> 2;
+    double br[NKS], bi[NKS], bsm[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+        br[ks] = hb[ks].x;
+        bi[ks] = hb[ks].y;
+        bsm[ks] = hb[ks].x + hb[ks].y;
+    }
+#pragma unroll
+    for (int t = 0; t < NTILE; ++t) {
+        const int idx = 4 * t + ka;
+        const bool ok = idx < NIDX;
+        const int q = idx >= 6 ? 1 : 0, m = idx - 6 * q;
+        d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const double2 a = A(ok ? q : 0, 6 * ca + (ok ? m : 0), 4 * ks + g);
+            const double ar = ok ? a.x : 0.0, ai = ok ? a.y : 0.0;
+            p1 = MFMA64(ar, br[ks], p1);
+            p2 = MFMA64(ai, bi[ks], p2);
+            p3 = MFMA64(ar + ai, bsm[ks], p3);
+        }
+        // D row g + 4 reg = tap index 4t + g of quarter reg, unit jc
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg)
+            sl[(g + 4 * reg) * 17 + jc] = make_double2(p1[reg] - p2[reg], p3[reg] - p1[reg] - p2[reg]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int id2 = 4 * t + k;                     // compile-time
+            if (id2 < NIDX) taps[id2 % 6][id2 / 6] = sl[(4 * cq + k) * 17 + ul];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// x <- qs gs DFT24(sum_q taps_q .* IDFT24(x)(. - d_q)) of one symbol (k_pic_fft's
+// chain; twa / twb: the lane twiddles staged in LDS, output scale folded in twa[1])
+template <int NT, int SH>
+__device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[6][NT], const double2 (*twa)[4][6],
+                                          const double2 (*twb)[4], int r, double sg1, double sg2) {
+    dft6<1>(xx);
+    double2 t[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
+        const double2 pv = dpp_c<QP_XOR2>(p);
+        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+        e = c_mulf(e, twb[0][r]);
+        const double2 qv = dpp_c<QP_XOR1>(e);
+        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+    }
+    const double2 tprev = dpp_c<QP_PREV>(t[5]);
+#pragma unroll
+    for (int m = 5; m >= 0; --m) {
+        const double2 tq = m ? t[m - 1] : tprev;
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) c_fma(acc, tp[m][q], ((SH >> q) & 1) ? tq : t[m]);
+        t[m] = acc;
+    }
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double2 pv = dpp_c<QP_XOR1>(t[m]);
+        double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+        f = c_mulf(f, twb[1][r]);
+        const double2 qv = dpp_c<QP_XOR2>(f);
+        xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+    }
+    dft6<-1>(xx);
+}
+
+// Shared LDS tables of the two kernels: constellation, slicer grid, row tables of
+// the wave's symbol, lane twiddles, the per-row diag(D_hat) weight of a delayed tap.
+struct Mic2Tables {
+    double2 sym[256];
+    int sgrid[256];
+    double2 twa[2][4][6];
+    double2 twb[2][4];
+};
+
+// One-tap + detection of the lane's six rows with diag(D_hat) = hd[a]; returns
+// the decided symbol indices (first-minimum tie rule, SignalConstellation.m:88)
+__device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6], const double2 (&hd)[6],
+                                           const StorePerfectDetect& o, const int* sgrid) {
+    int code[6];
+    int anytie = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const double2 z = c_div1(ye[a], hd[a]);
+        int tI, tQ;
+        const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
+        const int iQ = nearest_lin(z.y, o.scQ, o.ofQ, o.topQ, tQ);
+        code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
+        anytie |= tI | tQ;
+        dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+    }
+    if (__ballot(anytie)) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
+            const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
+            dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
+                        min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
+        }
+    }
+}
+
+// Stages 0..niter of the MMSE branch for one symbol of a unit (the common body of
+// k_mic_pilot and k_mic_data).  PIL: a pilot symbol (LS of every stage into the
+// block's LDS exchange + hpa, one barrier per stage); otherwise hP_s comes from
+// hpa.  Per-stage counters go to cntl[w][s] (one word per wave and stage).
+template <int NT, int SH, int NP, bool TRACE, bool PIL, class ALoad, class BsLoad>
+__device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
+                                            const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
+                                            const double2* wrow, double2* sl, double2 (*shp)[NP][17], int (*cntl),
+                                            const ALoad& A, const BsLoad& Bs, int row0, int unit, int unit_mf,
+                                            int ul, int l, int r, int U, int R, int rl, int snr) {
+    const int cq = (r >> 1) + 2 * (r & 1);
+    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    const bool valid = rl < o.rvalid;
+    // per-unit operands, read once: y, transmitted indices, the rows' constant
+    // part of v (precoded pilots / zero rows), PIL: the transmitted pilots
+    double2 yv[6], v[6], xpv[PIL ? 6 : 1];
+    unsigned txp[2] = {0u, 0u};
+    int pc[PIL ? 6 : 1];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int row = row0 + 4 * a + r;
+        yv[a] = o.y[(size_t)row * U + unit];
+        v[a] = o.xs[(size_t)row * R + rl];
+        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
+        if (PIL) {
+            pc[a] = rpc[4 * a + r];
+            xpv[a] = o.xp[(size_t)min(max(pc[a], 0), NP - 1) * R + rl];
+        }
+    }
+    unsigned dmask = 0u, emask = 0u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int dc = rdc[4 * a + r];
+        dmask |= dc >= 0 ? 1u << a : 0u;
+        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
+    }
+    double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0;       // window sums of the previous stage's taps
+    double2 hb[NP / 4];                                     // B operand of the tap GEMM: hP_{s-1}
+    for (int s = 0; s <= ma.niter; ++s) {
+        double2 ye[6];
+        if (s == 0) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) ye[a] = yv[a];
+        } else {
+            // the previous stage's estimated taps and their window sums
+            double2 taps[6][NT];
+            mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j, p); }, hb, sl,
+                             l, cq);
+            sp0 = sp1 = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+                for (int m = 0; m < 6; ++m) sq = c_add(sq, taps[m][q]);
+                sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+                sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+                if ((SH >> q) & 1) sp1 = c_add(sp1, sq);
+                else sp0 = c_add(sp0, sq);
+            }
+            sp0 = c_mul(scale, sp0);
+            double2 x[6];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) x[a] = v[a];
+            mic_chain<NT, SH>(x, taps, tb.twa, tb.twb, r, sg1, sg2);
+            // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                double2 hpv = sp0;
+                c_fma(hpv, wrow[4 * a + r], sp1);
+                ye[a] = c_sub(yv[a], x[p6(a)]);
+                c_fma(ye[a], hpv, v[a]);
+            }
+        }
+        // this stage's LS pilot estimates (script:412-414 / :487-489)
+        double2 hn4[NP / 4];
+        if (PIL) {
+            double2* hx = shp[s & 1][0];
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                if (pc[a] >= 0 && pc[a] < NP) {
+                    const double2 q = c_div(ye[a], xpv[a]);
+                    const double2 h = make_double2(q.x / sqk, q.y / sqk);
+                    hx[pc[a] * 17 + ul] = h;
+                    ma.hpa[((size_t)s * NP + pc[a]) * U + unit] = h;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
+            if (s < ma.niter)
+#pragma unroll
+                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = hx[(4 * ks + (l >> 4)) * 17 + (l & 15)];
+        } else {
+            const double2* __restrict__ hs = ma.hpa + (size_t)s * NP * U;
+#pragma unroll
+            for (int k = 0; k < NP / 4; ++k) hn4[k] = hs[(size_t)(r * (NP / 4) + k) * U + unit];
+            if (s < ma.niter)
+#pragma unroll
+                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = hs[(size_t)(4 * ks + (l >> 4)) * U + unit_mf];
+        }
+        // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s
+        double2 sn0 = make_double2(0.0, 0.0), sn1 = sn0;
+        const int vs = mic_var(s, ma.niter);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int k = 0; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, r * (NP / 4) + k), hn4[k]);
+            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
+            else sn0 = c_add(sn0, sq);
+        }
+        sn0 = c_mul(scale, sn0);
+        double2 hd[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            hd[a] = sn0;
+            c_fma(hd[a], wrow[4 * a + r], sn1);
+        }
+        int dp[6];
+        mic_detect(dp, ye, hd, o, tb.sgrid);
+        int ncnt = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const bool data = (dmask >> a) & 1;
+            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
+            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            double2 nv = make_double2(0.0, 0.0);
+            c_fma(nv, rpv[4 * a + r], tb.sym[dp[a]]);
+            v[a].x = data ? nv.x : v[a].x;
+            v[a].y = data ? nv.y : v[a].y;
+            if (TRACE && unit == o.tr->unit) {
+                const int row = row0 + 4 * a + r;
+                o.tr->yest[(size_t)s * o.tr->LK + row] = ye[a];
+                o.tr->hest[(size_t)s * o.tr->LK + row] = hd[a];
+                if (data) o.tr->dec_e[(size_t)s * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+            }
+        }
+        cntl[s] = wave_sum(valid ? ncnt : 0);      // uniform: every lane writes the same word
+        if (ma.mse_err) {
+            double me = 0.0, mp = 0.0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double2 hv = o.h[(size_t)(row0 + 4 * a + r) * R + rl];
+                const double dx = hd[a].x - hv.x, dy = hd[a].y - hv.y;
+                me += dx * dx + dy * dy;
+                mp += hv.x * hv.x + hv.y * hv.y;
+            }
+            flush_mse(me, s == 0 ? mp : 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.niter + 1, s, valid);
+        }
+    }
+}
+
+// LDS tables of a block: constellation / slicer grid (256 entries), lane twiddles
+__device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDetect& o, int tid, int nth) {
+    for (int i = tid; i < 256; i += nth) {
+        const double2 a = o.symbols[min(i, o.M - 1)];
+        const int g = o.grid_sym[min(i, o.nI * o.nQ - 1)];
+        tb.sym[i] = make_double2(i < o.M ? a.x : 0.0, i < o.M ? a.y : 0.0);
+        tb.sgrid[i] = i < o.nI * o.nQ ? g : 0;
+    }
+    if (tid < 48) {
+        const int e = ((tid / 6) % 4) * (tid % 6);
+        const double2 tw = kW24[e % 12];
+        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+        const int dir = tid / 24;
+        const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+        tb.twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+    }
+    if (tid >= 48 && tid < 56) {
+        const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
+        tb.twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
+    }
+}
+
+// Row tables of symbol block `blk` for the lanes tid < 24 of a wave-group: re-
+// precoding value, data index << 1 | no-edge (-1: not a data row), pilot column
+// (-1: not a pilot row), diag(D_hat) weight qs gs w^(-l) of a delayed tap
+__device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, double2* wrow, const SchemeK& sk,
+                                          const StorePerfectDetect& o, int row0, int t) {
+    if (t < 24) {
+        const double2 pv = o.row_pval[row0 + t];
+        const int dr = o.row_data[row0 + t], cs = o.row_cons[row0 + t];
+        const int pcr = sk.row_pcol[row0 + t];
+        rpv[t] = pv;
+        rdc[t] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+        rpc[t] = dr < 0 && pcr >= 0 && pcr < sk.NP ? pcr : -1;
+        const double2 t0 = kW24[t % 12];
+        const double2 wl = t >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+        wrow[t] = c_mul(make_double2(o.pf_scale_re, o.pf_scale_im), make_double2(wl.x, -wl.y));
+    }
+}
+
+// One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
+template <int NT, int SH, int NP, bool TRACE>
+__global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
+    __shared__ Mic2Tables tb;
+    __shared__ double2 rpv[4][24], wrow[4][24];
+    __shared__ int rdc[4][24], rpc[4][24];
+    __shared__ double2 bss[4][2][NT][NP];                   // Bs of each wave's symbol, both variants
+    __shared__ double2 sl[4][16 * 17];                      // per-wave tap slab
+    __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
+    __shared__ int cntl[4][PM_MAXIT + 1];
+    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
+    const int U = o.U, R = o.R;
+    const int ug16 = xcd_remap(blockIdx.x, gridDim.x);     // 16-unit group
+    const int ul = l >> 2;
+    const int unit = ug16 * 16 + ul, unit_mf = ug16 * 16 + (l & 15);
+    const int rl = unit % R;
+    const int snr = o.snr0 + (ug16 * 16) / R;
+    const int blk = ma.blks[w];
+    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    mic2_tables(tb, o, tid, blockDim.x);
+    mic2_rows(rpv[w], rdc[w], rpc[w], wrow[w], sk, o, row0, l);
+    {
+        const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
+        bss[w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
+    }
+    __syncthreads();
+    const double2* __restrict__ bvb = ma.bv + ((size_t)snr * NT * ma.N + klo) * NP;
+    const size_t vstride = (size_t)ma.nsnr * NT * ma.N * NP;
+    auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
+    auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
+    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], sl[w], shp, cntl[w], A, Bs,
+                                         row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    __syncthreads();
+    // one atomic per (stage, edge) per block
+    for (int i = tid; i < 2 * (ma.niter + 1); i += blockDim.x) {
+        const int s = i >> 1, edge = i & 1;
+        int v = 0;
+        for (int k = 0; k < nw; ++k) v += (cntl[k][s] >> (16 * edge)) & 0xffff;
+        const size_t i0 = o.cidx0 + (size_t)s + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
+        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+    }
+}
+
+// 64 units x one data symbol per block (4 waves x 16 units)
+template <int NT, int SH, int NP, bool TRACE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 3)))
+k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
+    __shared__ Mic2Tables tb;
+    __shared__ double2 rpv[24], wrow[24];
+    __shared__ int rdc[24], rpc[24];
+    constexpr int BVS = NP + 1;
+    __shared__ double2 sbv[2][NT][24][BVS];                 // Bv of the symbol's window, both variants
+    __shared__ double2 bss[2][NT][NP];
+    __shared__ double2 sl[4][16 * 17];
+    __shared__ int cntl[4][PM_MAXIT + 1];
+    int ug, bi;
+    band_block(ord, ma.nb, ug, bi);
+    const int blk = ma.blks[bi];
+    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int U = o.U, R = o.R;
+    const int snr = o.snr0 + (ug * WAVE) / R;
+    const int ul = l >> 2;
+    const int unit = ug * WAVE + w * 16 + ul, unit_mf = ug * WAVE + w * 16 + (l & 15);
+    const int rl = unit % R;
+    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    {
+        // every global load before the first LDS write (clamped, unconditional)
+        constexpr int NBV = 2 * NT * 24 * NP, PER = (NBV + 255) / 256;
+        double2 bvr[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = min(tid + 256 * k, NBV - 1), var = i / (NT * 24 * NP), q = (i / (24 * NP)) % NT,
+                      rem = i % (24 * NP);
+            bvr[k] = ma.bv[(((size_t)(var * ma.nsnr + snr) * NT + q) * ma.N + klo) * NP + rem];
+        }
+        const int ib = min(tid, 2 * NT * NP - 1), var = ib / (NT * NP), q = (ib / NP) % NT, p = ib % NP;
+        const double2 bsv = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
+        mic2_tables(tb, o, tid, 256);
+        mic2_rows(rpv, rdc, rpc, wrow, sk, o, row0, tid);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = min(tid + 256 * k, NBV - 1);
+            sbv[i / (NT * 24 * NP)][(i / (24 * NP)) % NT][(i / NP) % 24][i % NP] = bvr[k];
+        }
+        bss[var][q][p] = bsv;
+    }
+    __syncthreads();
+    auto A = [&](int var, int q, int j, int p) { return sbv[var][q][j][p]; };
+    auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
+    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, sl[w], nullptr, cntl[w], A, Bs, row0,
+                                          unit, unit_mf, ul, l, r, U, R, rl, snr);
+    __syncthreads();
+    for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
+        const int s = i >> 1, edge = i & 1;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v += (cntl[k][s] >> (16 * edge)) & 0xffff;
+        const size_t i0 = o.cidx0 + (size_t)s + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
+        if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2582,37 +2601,8 @@ static void launch_pass2_nt(hipStream_t s, const SchemeK& sk, const ChannelK& ch
     }
 }
 
-// (ntap, max delay) pairs with a k_pic_chain instance
-static int pic_chain_variant(const ChannelK& ch) {
-    int md = 0;
-    for (int q = 0; q < ch.ntap; ++q) md = std::max(md, ch.tap_delay[q]);
-    if (ch.ntap == 1 && md == 0) return 1;
-    if (ch.ntap == 2 && md == 1) return 2;
-    if (ch.ntap == 3 && md == 2) return 3;
-    return 0;
-}
-
-// Opts::pic_chain: 0 = per-iteration passes, 1 = k_pic_chain (VALU), 2 = k_pic_mfma
-// where the scheme allows it, else k_pic_chain, 3 (default) = k_pic_fft where the
-// scheme allows it, else as 2
-// k_pic_mfma's SH for the channel's taps (-1: no instance)
-static int pic_mfma_shift(const ChannelK& ch) {
-    if (ch.ntap == 1) return 0;
-    if (ch.ntap != 2) return -1;
-    const int maxd = std::max(ch.tap_delay[0], ch.tap_delay[1]);
-    const int sh = (maxd - ch.tap_delay[0]) | ((maxd - ch.tap_delay[1]) << 1);
-    return sh == 1 || sh == 2 ? sh : -1;
-}
-
-static bool pic_mfma_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
-    // k_pic_mfma's 32-bit offsets: u / h element offsets, buffer byte offsets of
-    // 32 rows of y and of the taps (ensure_buffers pads y, h and the taps)
-    const bool fits = (long long)sk.LK * b.U < (1ll << 31) && (long long)32 * b.U * 16 < (1ll << 32) &&
-                      ((long long)ch.ntap * ch.N + 4) * b.R * 16 < (1ll << 32);
-    return sk.pm_ok && op.pic_chain >= 2 && pic_mfma_shift(ch) >= 0 && (sk.pm_ksq == 6 || sk.pm_ksq == 7) && fits &&
-           niter >= 1 && niter <= PM_MAXIT;
-}
-
+// Opts::pic_chain: 0 = per-iteration passes (G u pass + Q^H H pass), 3 (default)
+// = k_pic_fft where the scheme allows it, else the passes.
 // k_pic_fft's SH for the channel's taps (-1: no instance): delays <= 1
 static int pic_fft_shift(const ChannelK& ch) {
     if (ch.ntap < 1 || ch.ntap > 2) return -1;
@@ -2666,12 +2656,11 @@ bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, co
 }
 
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
-    if (pic_fft_ok(op, sk, ch, b, niter) || pic_mfma_ok(op, sk, ch, b, niter)) return true;
-    return sk.pic_ok && pic_chain_variant(ch) && op.pic_chain != 0 && b.R % PCH_UNITS == 0;
+    return pic_fft_ok(op, sk, ch, b, niter);
 }
 
-// Detection operands of the chain kernels (k_pic_fft / k_pic_mfma / k_pic_chain /
-// k_mic_fft): tables, slicer folded for nearest_lin, counters of branch `csi`
+// Detection operands of the chain kernels (k_pic_fft / k_mic_fft /
+// k_stage0_fft): tables, slicer folded for nearest_lin, counters of branch `csi`
 // (0 MMSE, 1 perfect CSI; the stage is added per iteration).
 static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, const PerfectDetectArgs* pd, int csi) {
     StorePerfectDetect o{};
@@ -2693,6 +2682,7 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.cstride_snr = pd->nstage;
     o.U = b.U;
     o.R = b.R;
+    o.rvalid = b.rvalid;
     o.snr0 = b.snr0;
     o.M = sk.M;
     o.nI = sk.nI;
@@ -2777,6 +2767,63 @@ unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, cons
     return PATH_MIC_FFT | pf;
 }
 
+// Every stage of the MMSE branch of an FFT-form OFDM scheme (k_mic_pilot over the
+// pilot symbols, then k_mic_data over the others; see Mic2Args).
+bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
+                    int niter) {
+    return op.mic2 && mmse_fft_ok(op, sk, mm, ch, b) && mm.npb >= 1 && mm.npb <= 4 && mm.ndb >= 1 && b.hpa &&
+           niter >= 1 && niter <= PM_MAXIT && b.hpa_stages >= niter + 1 && op.pic_chain == 3 &&
+           pic_fft_ok(op, sk, ch, b, niter) && (long long)(niter + 1) * sk.NP * b.U < (1ll << 40);
+}
+
+unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
+                            const PerfectDetectArgs* pd, int niter, int xcd) {
+    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
+    Mic2Args ma{};
+    ma.bv = mm.Bv;
+    ma.bs = mm.Bs;
+    ma.hpa = b.hpa;
+    ma.mse_err = b.mse_err;
+    ma.mse_pow = b.mse_pow;
+    ma.nsnr = mm.nsnr;
+    ma.N = ch.N;
+    ma.nblk = sk.QH.nblk;
+    ma.niter = niter;
+    ma.scheme = pd->scheme;
+    const int sh = pic_fft_shift(ch);
+    // pilot symbols: one wave each, 16 units per block
+    ma.blks = mm.pblk;
+    ma.nb = mm.npb;
+    {
+        const dim3 grid(b.U / 16), blk(64 * mm.npb);
+#define LAUNCH_MP(NTV, SHV)                                                                                  \
+    do {                                                                                                     \
+        if (b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true>), grid, blk, 0, s, sk, ma, o);        \
+        else hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false>), grid, blk, 0, s, sk, ma, o);            \
+    } while (0)
+        if (ch.ntap == 1) LAUNCH_MP(1, 0);
+        else if (sh == 1) LAUNCH_MP(2, 1);
+        else LAUNCH_MP(2, 2);
+#undef LAUNCH_MP
+    }
+    ma.blks = mm.dblk;
+    ma.nb = mm.ndb;
+    {
+        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
+        const dim3 grid((b.U / WAVE) * mm.ndb), blk(256);
+#define LAUNCH_MD(NTV, SHV)                                                                                  \
+    do {                                                                                                     \
+        if (b.tr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o);     \
+        else hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o);         \
+    } while (0)
+        if (ch.ntap == 1) LAUNCH_MD(1, 0);
+        else if (sh == 1) LAUNCH_MD(2, 1);
+        else LAUNCH_MD(2, 2);
+#undef LAUNCH_MD
+    }
+    return PATH_MIC_FFT | PATH_MIC_STAGES;
+}
+
 // The pilot pre-pass of the structured MMSE IC (k_mic_fft in PILOT mode): y_ic of
 // IC iteration `stage` at the pilot rows only (script:482-489) -> hp_new, over
 // the symbol blocks that hold pilots (4 of 14 at C2); MFMA taps, no detection.
@@ -2815,11 +2862,28 @@ void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const C
 }
 
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter, bool qidx) {
+                              const PerfectDetectArgs* pd, int niter, bool qidx, bool stage0) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 1);
     qidx = qidx && pic_fft_ok(op, sk, ch, b, niter);
-    TapDelays dl{};
-    for (int q = 0; q < ch.ntap; ++q) dl.d[q] = ch.tap_delay[q];
+    if (stage0) {
+        if (!pic_fft_ok(op, sk, ch, b, niter)) throw std::logic_error("launch_perfect_chain: stage 0 needs k_pic_fft");
+        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
+        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+#define LAUNCH_PF0(NTV, SHV)                                                                                           \
+    do {                                                                                                               \
+        if (b.tr)                                                                                                      \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o,      \
+                               niter);                                                                                 \
+    } while (0)
+        const int sh = pic_fft_shift(ch);
+        if (ch.ntap == 1) LAUNCH_PF0(1, 0);
+        else if (sh == 1) LAUNCH_PF0(2, 1);
+        else LAUNCH_PF0(2, 2);
+#undef LAUNCH_PF0
+        return PATH_PIC_FFT;
+    }
     if (pic_fft_ok(op, sk, ch, b, niter)) {
         o.pf_scale_re = sk.pf_scale.x;
         o.pf_scale_im = sk.pf_scale.y;
@@ -2844,40 +2908,7 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
 #undef LAUNCH_PF
         return PATH_PIC_FFT;
     }
-    if (pic_mfma_ok(op, sk, ch, b, niter)) {
-        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
-        const size_t lds = ((size_t)(2 * 6 + 2 * sk.pm_ksq) * 64 + 256) * sizeof(double2) + sizeof(SlicerLds);
-        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_PM(KS, NTV, SHV)                                                                                   \
-    do {                                                                                                          \
-        if (b.tr)                                                                                                 \
-            hipLaunchKernelGGL((k_pic_mfma<KS, NTV, SHV, true>), grid, blk, lds, s, sk, om, b.ir, ch.N, o, niter); \
-        else                                                                                                      \
-            hipLaunchKernelGGL((k_pic_mfma<KS, NTV, SHV, false>), grid, blk, lds, s, sk, om, b.ir, ch.N, o, niter);\
-    } while (0)
-        const int sh = pic_mfma_shift(ch);
-        if (sk.pm_ksq == 6) {
-            if (ch.ntap == 1) LAUNCH_PM(6, 1, 0);
-            else if (sh == 1) LAUNCH_PM(6, 2, 1);
-            else LAUNCH_PM(6, 2, 2);
-        } else {
-            if (ch.ntap == 1) LAUNCH_PM(7, 1, 0);
-            else if (sh == 1) LAUNCH_PM(7, 2, 1);
-            else LAUNCH_PM(7, 2, 2);
-        }
-#undef LAUNCH_PM
-        return PATH_PIC_MFMA;
-    }
-    const BandOrder ord{b.U / PCH_UNITS, b.U / b.R, b.R / PCH_UNITS, op.xcd};
-    const size_t plds = 256 * sizeof(double2) + sizeof(SlicerLds) + 16 + (size_t)sk.pic_rows * DSCE_RB * sizeof(double2);
-    const dim3 grid((b.U / PCH_UNITS) * sk.QH.nblk), blk(256);
-    switch (pic_chain_variant(ch)) {
-        case 1: hipLaunchKernelGGL((k_pic_chain<1, 0>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
-        case 2: hipLaunchKernelGGL((k_pic_chain<2, 1>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
-        case 3: hipLaunchKernelGGL((k_pic_chain<3, 2>), grid, blk, plds, s, sk, ord, b.ir, ch.N, dl, o, niter); break;
-        default: break;
-    }
-    return PATH_PIC_CHAIN;
+    throw std::logic_error("launch_perfect_chain: no chain kernel for this scheme (perfect_chain_ok is false)");
 }
 
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
@@ -2907,6 +2938,7 @@ unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, con
     o.cstride_snr = pd->nstage;
     o.U = b.U;
     o.R = b.R;
+    o.rvalid = b.rvalid;
     o.snr0 = b.snr0;
     o.last = pd->last;
     o.M = sk.M;
@@ -3091,6 +3123,7 @@ struct FuseArgs {
     double* mse_pow;
     const TraceK* tr;              // null unless tracing (dsce_trace_unit_ex)
     int var, stage, nstage, last, scheme;
+    int rvalid;                    // realisations of the batch that count (McBuffers::rvalid)
 };
 
 template <int RBP, int NKS, bool FUSE, bool WDA_3M>
@@ -3355,8 +3388,8 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
         }
     }
     flush_counts(cnt, fa.counters, (((size_t)fa.scheme * 4) * nsnr + snr) * fa.nstage + fa.stage,
-                 (size_t)nsnr * fa.nstage, 1);
-    if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage);
+                 (size_t)nsnr * fa.nstage, 1, rl < fa.rvalid);
+    if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage, rl < fa.rvalid);
 }
 
 template <int RBP, int NKS, bool FUSE, bool WDA_3M = false>
@@ -3475,6 +3508,7 @@ unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, con
     fa.nstage = n_iter + 1;
     fa.last = last ? 1 : 0;
     fa.scheme = scheme_index;
+    fa.rvalid = b.rvalid;
     const dim3 grid(b.U / 64, mm.Pb.nblk);
     // Opts::wda_3m = 0: diag(D_hat) of the epilogue with four real MFMAs per k-step
     if (op.wda_3m)
@@ -3559,6 +3593,7 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
 
 struct StageArgs {
     int stage, var, nsnr, nstage, scheme, last, perfect, R, U, snr0, xcd_order;
+    int rvalid;                // realisations of the batch that count (McBuffers::rvalid)
     int qidx;                  // p_diag schemes: decisions as symbol indices (qe / qp) instead of v / u
     const TraceK* tr;          // null unless tracing (dsce_trace_unit_ex)
     const double2* ysrc_e;     // y (stage 0) or y_est
@@ -3606,7 +3641,7 @@ __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const 
             mp += hv.x * hv.x + hv.y * hv.y;
         }
     }
-    if (st.mse_err) flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage);
+    if (st.mse_err) flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage, rl < st.rvalid);
 }
 
 // (2) data-symbol decisions and bit-error counts, grid (U/64, ceil(ND/32)).
@@ -3655,7 +3690,7 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
         }
     }
     flush_counts(cnt, counters, (((size_t)st.scheme * 4) * st.nsnr + snr) * st.nstage + st.stage,
-                 (size_t)st.nsnr * st.nstage, 2);
+                 (size_t)st.nsnr * st.nstage, 2, rl < st.rvalid);
 }
 
 // (3) re-precoding of the quantised decisions for the next IC iteration:
@@ -3818,7 +3853,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                 me += dx * dx + dy * dy;
                 mp += hh[r].x * hh[r].x + hh[r].y * hh[r].y;
             }
-        flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage);
+        flush_mse(me, mp, st.mse_err, st.mse_pow, st.scheme, st.nsnr, snr, st.nstage, st.stage, rl < st.rvalid);
     }
     const double idd = 1.0 / sk.data_div;
     const double sI = sk.slI, sQ = sk.slQ;
@@ -3879,7 +3914,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
         }
     }
     flush_counts(cnt, counters, (((size_t)st.scheme * 4) * st.nsnr + snr) * st.nstage + st.stage,
-                 (size_t)st.nsnr * st.nstage, PERF ? 2 : 1);
+                 (size_t)st.nsnr * st.nstage, PERF ? 2 : 1, rl < st.rvalid);
 }
 
 template <int NPT>
@@ -3934,6 +3969,7 @@ unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const Mm
     st.last = last ? 1 : 0;
     st.tr = b.tr;
     st.R = b.R;
+    st.rvalid = b.rvalid;
     st.U = b.U;
     st.snr0 = b.snr0;
     st.xcd_order = op.xcd;
@@ -3969,6 +4005,7 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
     // LS pilot estimates of stage 0 into b.hp (k_ls), then the symbol-block stage
     StageArgs st{};
     st.R = b.R;
+    st.rvalid = b.rvalid;
     st.U = b.U;
     st.ysrc_e = b.y;
     hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);

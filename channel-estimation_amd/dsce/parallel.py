@@ -12,15 +12,17 @@ import numpy as np
 
 
 def shard_range(first_rep, n_rep, world, rank, align=64):
-    """Contiguous slice of [first_rep, first_rep + n_rep) for `rank`; slice
-    lengths are multiples of `align` (one wavefront of realisations) except
-    possibly the last."""
-    if n_rep % align:
-        raise ValueError("n_rep must be a multiple of %d" % align)
-    blocks = n_rep // align
-    lo = (blocks * rank) // world
-    hi = (blocks * (rank + 1)) // world
-    return first_rep + lo * align, (hi - lo) * align
+    """Contiguous slice of [first_rep, first_rep + n_rep) for `rank`.  Slice
+    boundaries sit on multiples of `align` (one wavefront of realisations) so
+    every rank but the one holding the end of the range runs whole waves; any
+    n_rep is allowed (dsce_run pads a partial tail wave and counts only its
+    real realisations, so the slices still add up to the one-rank counts)."""
+    if n_rep < 0 or align < 1:
+        raise ValueError("n_rep must be >= 0 and align >= 1")
+    blocks = (n_rep + align - 1) // align
+    lo = min((blocks * rank) // world * align, n_rep)
+    hi = min((blocks * (rank + 1)) // world * align, n_rep)
+    return first_rep + lo, hi - lo
 
 
 def allreduce_counts(counts, device=None):

@@ -28,7 +28,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--config", default="default", help="default (C2-C4) | c5 | paper | doubly_flat (config 1)")
     ap.add_argument("--schemes", default="fbmc_aux,fbmc_cod,ofdm")
-    ap.add_argument("--reps", type=int, default=None, help="realisations (multiple of 64; default: the config's)")
+    ap.add_argument("--reps", type=int, default=None, help="realisations (any count; default: the config's NrRepetitions)")
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--seed", type=int, default=0x5EED0000)
     ap.add_argument("--out", default=None, help="result JSON")
@@ -64,8 +64,9 @@ def main(argv=None):
     names = tuple(a.schemes.split(","))
     from dsce.engine import gpu_tx
     S = build_setup(a.config, schemes=names, tx=gpu_tx(device))      # G / Q on the GPU (row f1)
-    reps = a.reps if a.reps is not None else S.n_repetitions
-    reps = max(64, (reps + 63) // 64 * 64)          # one wavefront of realisations per step
+    reps = a.reps if a.reps is not None else S.n_repetitions    # script:19 / :44, exactly (no rounding)
+    if reps < 1:
+        raise SystemExit("--reps must be >= 1")
     nsnr = len(S.snr_db)
     if a.shard == "snr":
         # SNR points [s0, s0 + ns) on this rank, every realisation
@@ -84,7 +85,7 @@ def main(argv=None):
     bits = None
     setup_s, t0 = 0.0, time.perf_counter()
     if mine:                                         # a rank with an empty shard contributes zeros
-        eng = build_engine(Sr, device=device, batch=min(a.batch, mine), options=options)
+        eng = build_engine(Sr, device=device, batch=max(64, min(a.batch, mine)), options=options)
         setup_s = time.perf_counter() - t0
         sub = np.zeros(eng.counter_shape(), dtype=np.int64)
         if a.mse:
@@ -169,8 +170,9 @@ def _doubly_flat(a):
     sim = DoublyFlatSim(build_doubly_flat_setup(interpolation=a.interpolation), batch=a.batch)
     setup_s = time.perf_counter() - t0
     S = sim.setup
-    reps = a.reps if a.reps is not None else S.n_repetitions
-    reps = max(64, (reps + 63) // 64 * 64)
+    reps = a.reps if a.reps is not None else S.n_repetitions    # SimpleVersion_DoublyFlat.m:13, exactly
+    if reps < 1:
+        raise SystemExit("--reps must be >= 1")
     t0 = time.perf_counter()
     counts = sim.run(a.seed, 0, reps)
     secs = time.perf_counter() - t0

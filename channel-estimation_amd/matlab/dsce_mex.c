@@ -1,7 +1,14 @@
 /*
  * dsce_mex.c — MEX gateway binding the reference's MATLAB host to libdsce.so
- * (include/dsce.h).  Build (MATLAB R2018a+, interleaved complex):
- *   mex -R2018a -I../../include dsce_mex.c -L../dsce -ldsce
+ * (include/dsce.h).  Build:
+ *   MATLAB R2018a+ (interleaved complex):   mex -R2018a -I../../include dsce_mex.c -L../dsce -ldsce
+ *   MATLAB R2013b / R2016a (README.md:19-20, separate real / imaginary planes):
+ *                                           mex -I../../include dsce_mex.c -L../dsce -ldsce
+ * The complex storage is chosen at compile time by MATLAB's own
+ * MX_HAS_INTERLEAVED_COMPLEX (set by -R2018a): with split planes every complex
+ * input is interleaved into a scratch array before the ABI call and every
+ * complex output is written interleaved to scratch and split into
+ * mxGetPr / mxGetPi afterwards (the ABI is interleaved only).
  * MATLAB's mex.h is not part of this image; the gateway's
  * argument checking is exercised on the CPU by tests/test_mex_gateway.py
  * against a test-only mex.h stand-in and a recording stub of the C-ABI.
@@ -40,6 +47,19 @@
 #include "dsce.h"
 #include "mex.h"
 
+#ifndef MX_HAS_INTERLEAVED_COMPLEX
+#define MX_HAS_INTERLEAVED_COMPLEX 0
+#endif
+
+/* real doubles / int64 of an array in either storage API */
+#if MX_HAS_INTERLEAVED_COMPLEX
+#define DSCE_DOUBLES(a) mxGetDoubles(a)
+#define DSCE_INT64S(a) mxGetInt64s(a)
+#else
+#define DSCE_DOUBLES(a) mxGetPr(a)
+#define DSCE_INT64S(a) ((int64_t*)mxGetData(a))
+#endif
+
 static dsce_ctx* g_ctx = NULL;
 
 static void cleanup(void) {
@@ -72,18 +92,74 @@ static int64_t integer(const mxArray* a, int i, int64_t lo) {
 static const double* real_doubles(const mxArray* a, int i, size_t n_expected) {
     if (!mxIsDouble(a) || mxIsComplex(a)) bad(i, "a real double array");
     if (n_expected != (size_t)-1 && mxGetNumberOfElements(a) != n_expected) bad(i, "of the expected length");
-    return mxGetDoubles(a);
+    return DSCE_DOUBLES(a);
 }
 
-/* interleaved complex view of a double array (real inputs promoted into *tmp) */
+/* interleaved complex view of a double array (the ABI's storage): real inputs
+ * are promoted, and with split planes (pre-R2018a) the planes are interleaved,
+ * into *tmp (a scratch array the caller destroys) */
 static const double* cplx(const mxArray* a, int i, size_t rows, size_t cols, mxArray** tmp) {
     if (!mxIsDouble(a)) bad(i, "a double array");
     if ((rows != (size_t)-1 && mxGetM(a) != rows) || (cols != (size_t)-1 && mxGetN(a) != cols))
         bad(i, "of the expected size");
+#if MX_HAS_INTERLEAVED_COMPLEX
     if (mxIsComplex(a)) return (const double*)mxGetComplexDoubles(a);
     *tmp = mxDuplicateArray(a);
     if (!mxMakeArrayComplex(*tmp)) mexErrMsgIdAndTxt("dsce:type", "cannot make argument %d complex", i + 1);
     return (const double*)mxGetComplexDoubles(*tmp);
+#else
+    {
+        const size_t n = mxGetNumberOfElements(a);
+        const double* re = mxGetPr(a);
+        const double* im = mxIsComplex(a) ? mxGetPi(a) : NULL;
+        double* z;
+        size_t k;
+        *tmp = mxCreateDoubleMatrix((mwSize)(2 * (n ? n : 1)), 1, mxREAL);
+        z = mxGetPr(*tmp);
+        for (k = 0; k < n; ++k) {
+            z[2 * k] = re[k];
+            z[2 * k + 1] = im ? im[k] : 0.0;
+        }
+        return z;
+    }
+#endif
+}
+
+/* A complex output: the ABI writes interleaved (re, im) pairs into the buffer
+ * out_begin returns; out_end moves them into the array's storage (split planes
+ * before R2018a; nothing to do with interleaved storage). */
+typedef struct {
+    mxArray* arr;
+    mxArray* scratch;
+} cplx_out;
+
+static double* out_begin(cplx_out* o, mxArray* arr) {
+    o->arr = arr;
+    o->scratch = NULL;
+#if MX_HAS_INTERLEAVED_COMPLEX
+    return (double*)mxGetComplexDoubles(arr);
+#else
+    {
+        const size_t n = mxGetNumberOfElements(arr);
+        o->scratch = mxCreateDoubleMatrix((mwSize)(2 * (n ? n : 1)), 1, mxREAL);
+        return mxGetPr(o->scratch);
+    }
+#endif
+}
+
+static void out_end(cplx_out* o) {
+#if !MX_HAS_INTERLEAVED_COMPLEX
+    const size_t n = mxGetNumberOfElements(o->arr);
+    const double* z = mxGetPr(o->scratch);
+    double *re = mxGetPr(o->arr), *im = mxGetPi(o->arr);
+    size_t k;
+    for (k = 0; k < n; ++k) {
+        re[k] = z[2 * k];
+        im[k] = z[2 * k + 1];
+    }
+#endif
+    if (o->scratch) mxDestroyArray(o->scratch);
+    o->scratch = NULL;
 }
 
 static dsce_dims dims_of(int32_t id) {
@@ -153,7 +229,7 @@ static void c_add_scheme(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prh
     for (i = 0; i < np; ++i) pil[i] = (int32_t)pp[i] - 1;
     for (i = 0; i < nd; ++i) {
         dat[i] = dp ? (int32_t)dp[i] - 1 : 0;
-        cons[i] = mxIsLogical(prhs[8]) ? (mxGetLogicals(prhs[8])[i] ? 1 : 0) : (mxGetDoubles(prhs[8])[i] != 0.0);
+        cons[i] = mxIsLogical(prhs[8]) ? (mxGetLogicals(prhs[8])[i] ? 1 : 0) : (DSCE_DOUBLES(prhs[8])[i] != 0.0);
     }
     d.n_tx_symbols = (int32_t)(np + nd);
     d.n_pilots = (int32_t)np;
@@ -198,8 +274,9 @@ static void c_run(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     dm[0] = (mwSize)(d.n_iter + 1); dm[1] = (mwSize)d.n_snr; dm[2] = 2; dm[3] = 2; dm[4] = (mwSize)d.n_schemes;
     plhs[0] = mxCreateNumericArray(5, dm, mxINT64_CLASS, mxREAL);
     if ((int64_t)mxGetNumberOfElements(plhs[0]) != d.n_counters) mexErrMsgIdAndTxt("dsce:state", "counter shape");
+    /* any nRep >= 0: the script's NrRepetitions (script:19 / :44) as is */
     check(dsce_run(g_ctx, (uint64_t)integer(prhs[1], 1, 0), (uint64_t)integer(prhs[2], 2, 0),
-                   (uint64_t)integer(prhs[3], 3, 0), (int64_t*)mxGetInt64s(plhs[0])), "dsce_run");
+                   (uint64_t)integer(prhs[3], 3, 0), DSCE_INT64S(plhs[0])), "dsce_run");
 }
 
 static void c_bits_per_rep(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -207,25 +284,36 @@ static void c_bits_per_rep(int nlhs, mxArray* plhs[], int nrhs, const mxArray* p
     (void)nlhs; (void)nrhs;
     check(dsce_bits_per_rep(g_ctx, scheme_id(prhs[1], 1), b), "dsce_bits_per_rep");
     plhs[0] = mxCreateDoubleMatrix(2, 1, mxREAL);
-    mxGetDoubles(plhs[0])[0] = (double)b[0];
-    mxGetDoubles(plhs[0])[1] = (double)b[1];
+    DSCE_DOUBLES(plhs[0])[0] = (double)b[0];
+    DSCE_DOUBLES(plhs[0])[1] = (double)b[1];
 }
 
 static void c_channel_realise(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const dsce_dims d = dims_of(0);
     (void)nlhs; (void)nrhs;
+    cplx_out o;
+    double* z;
+    int rc;
     plhs[0] = mxCreateDoubleMatrix((mwSize)d.n_samples, (mwSize)d.n_taps, mxCOMPLEX);
-    check(dsce_channel_realise(g_ctx, (uint64_t)integer(prhs[1], 1, 0), (uint64_t)integer(prhs[2], 2, 0),
-                               (double*)mxGetComplexDoubles(plhs[0])), "dsce_channel_realise");
+    z = out_begin(&o, plhs[0]);
+    rc = dsce_channel_realise(g_ctx, (uint64_t)integer(prhs[1], 1, 0), (uint64_t)integer(prhs[2], 2, 0), z);
+    out_end(&o);
+    check(rc, "dsce_channel_realise");
 }
 
 static void c_get_W(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const int32_t id = scheme_id(prhs[1], 1);
     const dsce_dims d = dims_of(id);
     (void)nlhs; (void)nrhs;
+    const int32_t k = (int32_t)integer(prhs[2], 2, 1) - 1, var = (int32_t)integer(prhs[3], 3, 0);
+    cplx_out o;
+    double* z;
+    int rc;
     plhs[0] = mxCreateDoubleMatrix((mwSize)d.lk * (mwSize)d.lk * (mwSize)d.n_pilots, 1, mxCOMPLEX);
-    check(dsce_get_W(g_ctx, id, (int32_t)integer(prhs[2], 2, 1) - 1, (int32_t)integer(prhs[3], 3, 0),
-                     (double*)mxGetComplexDoubles(plhs[0])), "dsce_get_W");
+    z = out_begin(&o, plhs[0]);
+    rc = dsce_get_W(g_ctx, id, k, var, z);
+    out_end(&o);
+    check(rc, "dsce_get_W");
 }
 
 static void c_mmse_onetap(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -235,16 +323,21 @@ static void c_mmse_onetap(int nlhs, mxArray* plhs[], int nrhs, const mxArray* pr
     mxArray* t = NULL;
     const double* hp;
     size_t n;
+    int32_t k, var;
+    cplx_out o;
+    double* z;
     (void)nlhs; (void)nrhs;
     if (mxGetM(prhs[4]) != (size_t)d.n_pilots) bad(4, "an NP x n matrix of LS pilot estimates");
     n = mxGetN(prhs[4]);
     if (n < 1) bad(4, "non-empty");
+    k = (int32_t)integer(prhs[2], 2, 1) - 1;
+    var = (int32_t)integer(prhs[3], 3, 0);
     hp = cplx(prhs[4], 4, (size_t)d.n_pilots, n, &t);
     plhs[0] = mxCreateDoubleMatrix((mwSize)d.lk, (mwSize)n, mxCOMPLEX);
+    z = out_begin(&o, plhs[0]);
     {
-        const int rc = dsce_mmse_onetap(g_ctx, id, (int32_t)integer(prhs[2], 2, 1) - 1,
-                                        (int32_t)integer(prhs[3], 3, 0), hp, (int32_t)n,
-                                        (double*)mxGetComplexDoubles(plhs[0]));
+        const int rc = dsce_mmse_onetap(g_ctx, id, k, var, hp, (int32_t)n, z);
+        out_end(&o);
         if (t) mxDestroyArray(t);
         check(rc, "dsce_mmse_onetap");
     }
@@ -277,7 +370,7 @@ static void c_scheme_dims(int nlhs, mxArray* plhs[], int nrhs, const mxArray* pr
     double* o;
     (void)nlhs; (void)nrhs;
     plhs[0] = mxCreateDoubleMatrix(1, 9, mxREAL);
-    o = mxGetDoubles(plhs[0]);
+    o = DSCE_DOUBLES(plhs[0]);
     o[0] = d.n_samples; o[1] = d.n_taps; o[2] = d.lk; o[3] = d.n_pilots; o[4] = d.n_data;
     o[5] = d.n_tx_symbols; o[6] = d.n_schemes; o[7] = d.n_snr; o[8] = d.n_iter;
 }

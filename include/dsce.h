@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 3
+#define DSCE_ABI_VERSION 4
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
@@ -186,8 +186,8 @@ typedef struct {
 #define DSCE_PATH_WPAIR3          (1u << 1)   /* k_wpair3: MFMA pair-tile contraction, 3M products        */
 #define DSCE_PATH_WPAIR4M         (1u << 2)   /* k_wpair: pair tiles, 4 real MFMAs per complex product     */
 #define DSCE_PATH_WCONTRACT_VALU  (1u << 3)   /* k_wcontract_valu                                         */
-#define DSCE_PATH_PIC_MFMA        (1u << 4)   /* k_pic_mfma: perfect-CSI IC chain on the matrix cores      */
-#define DSCE_PATH_PIC_CHAIN       (1u << 5)   /* k_pic_chain: perfect-CSI IC chain on the VALU             */
+#define DSCE_PATH_PIC_MFMA        (1u << 4)   /* retired in ABI 4 (k_pic_mfma); never set                  */
+#define DSCE_PATH_PIC_CHAIN       (1u << 5)   /* retired in ABI 4 (k_pic_chain); never set                 */
 #define DSCE_PATH_PIC_PASSES      (1u << 6)   /* perfect-CSI IC as two banded passes per iteration         */
 #define DSCE_PATH_STAGE_FUSED     (1u << 7)   /* k_ls + k_stage_fused                                      */
 #define DSCE_PATH_STAGE_SPLIT     (1u << 8)   /* k_ls_hest + k_detect + k_precode                          */
@@ -196,6 +196,8 @@ typedef struct {
 #define DSCE_PATH_MIC_FFT         (1u << 11)  /* k_pilot_pre + k_mic_fft: MMSE IC as Q' H_hat G by FFT (OFDM) */
 #define DSCE_PATH_TXRX_FFT        (1u << 12)  /* k_txrx_fft: TX + channel + noisy receiver front by FFT (OFDM) */
 #define DSCE_PATH_PILOT_FUSED     (1u << 13)  /* k_mic_fft also runs the next IC iteration's pilot pass       */
+#define DSCE_PATH_MIC_STAGES      (1u << 14)  /* k_mic_pilot + k_mic_data: every MMSE stage of an FFT-form OFDM
+                                                 scheme in one launch pair; k_pic_fft with the perfect-CSI stage 0 */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -218,7 +220,11 @@ int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold);
 int dsce_set_batch(dsce_ctx* ctx, int32_t reps_per_batch);
 
 /* Runs realisations [first_rep, first_rep + n_rep) for every scheme and SNR and
- * ADDS the bit-error counts into err_counts (layout above).  Synchronous. */
+ * ADDS the bit-error counts into err_counts (layout above).  Synchronous.  Any
+ * n_rep >= 0 (the script's NrRepetitions = 25 / 1000, script:19 / :44): the
+ * device works in whole wavefronts of 64 realisations, and the padding
+ * realisations of a tail wave are simulated but counted nowhere (nor in the MSE
+ * sums), so counts over [a, b) equal the sum over any split of [a, b). */
 int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts);
 
 /* Bits per realisation of a scheme: [0] all data bits, [1] no-edge bits. */
@@ -286,14 +292,15 @@ int dsce_scheme_dims(dsce_ctx* ctx, int32_t scheme_id, dsce_dims* dims);
 int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
 /* Kernel-selection options (defaults = the measured-best path; for A/B runs and
  * tests): xcd, fuse_stage, wpair_3m (-1 auto), wda_3m, pic_chain (0 passes,
- * 1 VALU chain, 2 MFMA chain, 3 FFT chain where the scheme's G / Q allow it), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
+ * 3 FFT chain where the scheme's G / Q allow it, else passes), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
  * snr_chunk (0 all), streams (1|2), jakes_rpw (1|2), wtrim (read by
  * dsce_build_mmse), wcontract_valu, mmse_ic (1: the MMSE IC iterations of an FFT-form
  * OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}
  * (k_mic_fft; equal to the W contraction of script:482-511 to rounding, checked
  * at dsce_build_mmse), 0: the W contraction everywhere), qidx, stage0_fft,
  * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic, pilot_fuse (the OFDM fast-path pieces,
- * 1 = on), snr_base (0..255: the noise of SNR index k is sub-stream
+ * 1 = on), mic2 (1 = every MMSE stage of FFT-form OFDM in k_mic_pilot + k_mic_data and the
+ * perfect-CSI stage 0 in k_pic_fft; 0 = the per-stage kernels), snr_base (0..255: the noise of SNR index k is sub-stream
  * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
  * one-rank run's noise).  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);

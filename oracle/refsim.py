@@ -227,7 +227,8 @@ def nearest(x, symbols):
 # ---------------------------------------------------------------------------
 # Monte-Carlo loop (script:350-564)
 # ---------------------------------------------------------------------------
-def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margin_eps=1e-9, trace=None):
+def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margin_eps=1e-9, trace=None,
+             w_sparse=False):
     """Literal restatement of the Monte-Carlo body.
 
     ``chan``: dict(N, dt, pdp, pdp_norm, idx_taps, fD, paths, model).
@@ -240,6 +241,12 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
     nbits=int64[ns, 2 edge], mse_err=float[ns, nsnr, 1+n_iter], mse_pow=float[ns, nsnr]).
     The MSE sums (|h_hat - h|^2 per stage, |h|^2, h = diag(D)) are build-defined
     (the reference computes none): the checker of dsce_get_mse.
+
+    ``w_sparse``: form D_hat = reshape(W hP) (script:417-425, :493-511) as a
+    sparse (LK^2 x NP) product over W's stored non-zeros instead of the
+    literal full(W) .* hP summed over the third dimension.  Same terms, same
+    thresholded W; only the summation order over p differs (rounding level).
+    Used for the C5 FBMC schemes, where full(W) is 1 GB per evaluation.
     """
     ns = len(schemes)
     nsnr = len(pn_time)
@@ -253,6 +260,19 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
         m = sc["bits_per_symbol"]
         nbits[si, 0] = sc["n_data"] * m * n_rep
         nbits[si, 1] = int(np.sum(sc["considered"])) * m * n_rep
+    wsp = {}
+    if w_sparse:
+        for si, sc in enumerate(schemes):
+            LK, NP = sc["G"].shape[1], len(sc["pilot_pos"])
+            for key in ("W", "W0"):
+                for isnr in range(len(pn_time)):
+                    wsp[si, key, isnr] = sp.csr_matrix(mmse[si][key][:, isnr].reshape(LK * LK, NP, order="F"))
+
+    def d_hat(si, key, isnr, hp, LK, NP):
+        if w_sparse:
+            return (wsp[si, key, isnr] @ hp).reshape(LK, LK, order="F")
+        return (mmse[si][key][:, isnr].reshape(LK, LK, NP, order="F") * hp[None, None, :]).sum(axis=2)
+
     for rep in range(first_rep, first_rep + n_rep):
         ir = jakes_ir(seed, rep, N, chan["dt"], chan["pdp_norm"], chan["idx_taps"], chan["fD"],
                       chan["paths"], chan.get("model", "Jakes"))
@@ -278,8 +298,6 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
             r0 = H @ s                                                           # script:383-385
             D = (Q.conj().T @ (H @ G))                                           # script:388-389
             h = np.diag(D).copy()
-            W = mmse[si]["W"]
-            W0 = mmse[si]["W0"]
             cons_bits = np.repeat(sc["considered"], mbit)
             Dnd = D - np.diag(h)
 
@@ -308,7 +326,7 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                 r = r0 + noise
                 y = Q.conj().T @ r                                               # script:406-409
                 hP = y[sc["pilot_pos"]] / xP / np.sqrt(sc["kappa"])              # script:412-414
-                Dest = (W[:, isnr].reshape(LK, LK, NP, order="F") * hP[None, None, :]).sum(axis=2)
+                Dest = d_hat(si, "W", isnr, hP, LK, NP)
                 hest = np.diag(Dest).copy()
                 mse_err[si, isnr, 0] += np.sum(np.abs(hest - h) ** 2)
                 mse_pow[si, isnr] += np.sum(np.abs(h) ** 2)
@@ -340,8 +358,8 @@ def simulate(seed, first_rep, n_rep, chan, schemes, pn_time, n_iter, mmse, margi
                     v = P @ np.concatenate([xP, zD_est])                           # script:482-484
                     yic = y - (Dt - np.diag(ht)) @ v
                     hPt = yic[sc["pilot_pos"]] / xP / np.sqrt(sc["kappa"])         # script:487-489
-                    Wv = W if it <= n_iter / 2 else W0                              # script:492
-                    Dt = (Wv[:, isnr].reshape(LK, LK, NP, order="F") * hPt[None, None, :]).sum(axis=2)
+                    Dt = d_hat(si, "W" if it <= n_iter / 2 else "W0", isnr, hPt, LK, NP)   # script:492
+
                     ht = np.diag(Dt).copy()
                     mse_err[si, isnr, it] += np.sum(np.abs(ht - h) ** 2)
                     _, idx, mg = detect(yic / ht)                                  # script:519-537

@@ -330,12 +330,20 @@ def _hadamard(n):
     return H
 
 
+# The interferer threshold of IIC.m:72-73 / :113-114 in exact-arithmetic
+# semantics: magnitudes equal to it up to TIE_RTOL count as >= (at C4 it falls
+# inside a class of 8 interferers equal in exact arithmetic, whose floating-point
+# order is an FFT rounding accident; MATLAB's own choice is unknowable offline).
+# The product mirror uses the same rule (dsce/estimation.py TIE_RTOL).
+TIE_RTOL = 1e-12
+
+
 def _considered(D, PM, threshold):
     """IIC.m:72-76 / :113-123: -(pilot number) at the positions a pilot
-    considers (>= threshold), 1..NP at the pilots (column-major numbering)."""
+    considers (>= threshold, TIE_RTOL), 1..NP at the pilots (column-major numbering)."""
     pm = col(PM)
     NP = int(np.sum(pm == 1))
-    temp = np.abs(D[pm == 1, :]) >= threshold                           # NP x LK
+    temp = np.abs(D[pm == 1, :]) >= threshold * (1.0 - TIE_RTOL)       # NP x LK
     ci = (temp.T * -(np.arange(1, NP + 1))[None, :]).sum(axis=1)        # reshape(temp', L, K, NP) .* -(1:NP)
     ci = ci.astype(float)
     ci[pm == 1] = np.arange(1, NP + 1)

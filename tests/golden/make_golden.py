@@ -140,7 +140,7 @@ def main():
     if "setup" in only:
         json.dump(setup_fixture("default", ("fbmc_aux", "fbmc_cod", "ofdm")),
                   open(os.path.join(HERE, "setup_default.json"), "w"))
-        json.dump(setup_fixture("c5", ("fbmc_aux", "ofdm")), open(os.path.join(HERE, "setup_c5.json"), "w"))
+        json.dump(setup_fixture("c5", ("fbmc_aux", "fbmc_cod", "ofdm")), open(os.path.join(HERE, "setup_c5.json"), "w"))
     for tag in ("c3", "c4", "c5"):
         if tag in only:
             json.dump(oracle_fixture(tag), open(os.path.join(HERE, "oracle_%s_small.json" % tag), "w"))

@@ -50,7 +50,7 @@ _MMSE = {}
 def oracle_mmse(S, name):
     """R_hP, R_est, R_noI, R_Dij, W, W0 of scheme `name` (refsim.mmse_setup,
     script:208-313) from the oracle's own G / Q / P and channel (cached)."""
-    key = (S.name, tuple(S.snr_db), S.n_iter, tuple(sorted(S.schemes)), name)
+    key = (S.name, tuple(S.snr_db), S.n_iter, tuple(sorted(S.schemes)), name, S.zero_threshold)
     if key not in _MMSE:
         from oracle import refsim
         ch = S.chan
@@ -100,11 +100,12 @@ def engine(S, schemes=None, batch=None, options=None, device=0):
     return eng
 
 
-def simulate(S, seed, first, n, names, trace=None):
-    """oracle/refsim.simulate over schemes `names` of S."""
+def simulate(S, seed, first, n, names, trace=None, w_sparse=False):
+    """oracle/refsim.simulate over schemes `names` of S (w_sparse: D_hat from W's
+    stored non-zeros, see refsim.simulate)."""
     from oracle import refsim
     return refsim.simulate(seed, first, n, S.chan, [S.schemes[k] for k in names], S.pn_time, S.n_iter,
-                           [oracle_mmse(S, k) for k in names], trace=trace)
+                           [oracle_mmse(S, k) for k in names], trace=trace, w_sparse=w_sparse)
 
 
 def product_scheme_dict(sc):

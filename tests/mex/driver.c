@@ -1,5 +1,11 @@
 /* TEST-ONLY driver: calls the gateway's mexFunction like MATLAB would and
- * prints, per case, OK + output sizes or the error identifier. */
+ * prints, per case, OK + output sizes or the error identifier.
+ *   drv                       the fixed case list below
+ *   drv replay cmd:nrhs:nlhs ...
+ *                             one call per triple, with default arguments of the
+ *                             right class and size for each argument position
+ *                             (tests/test_mex_gateway.py replays every
+ *                             dsce_mex(...) call of INTEGRATION.md this way) */
 #include <setjmp.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -20,10 +26,11 @@ static mxArray* S(const char* s) {
     return a;
 }
 static mxArray* D(double v) { return mxCreateDoubleScalar(v); }
+/* element i = (1 + i % 7) - (1 + i % 5) j, or 1 + i % 7 when real (mex_stub.c checks
+ * that the ABI receives exactly these values, interleaved) */
 static mxArray* M(size_t m, size_t n, int cplx) {
     mxArray* a = mxCreateDoubleMatrix(m, n, cplx ? mxCOMPLEX : mxREAL);
-    double* p = a->data;
-    for (size_t i = 0; i < m * n * (cplx ? 2 : 1); ++i) p[i] = 1.0 + (double)(i % 7);
+    for (size_t i = 0; i < m * n; ++i) tst_set_c(a, i, 1.0 + (double)(i % 7), cplx ? -(1.0 + (double)(i % 5)) : 0.0);
     return a;
 }
 static mxArray* Lg(size_t n) {
@@ -34,22 +41,98 @@ static mxArray* Lg(size_t n) {
     return a;
 }
 
+static mxArray* g_last_out;
+
 static void call(const char* tag, int nlhs, int nrhs, mxArray** in) {
     mxArray* out[2] = {NULL, NULL};
     printf("%s:\n", tag);
+    g_last_out = NULL;
     if (setjmp(g_err_jmp)) {
         printf("%s -> ERR %s\n", tag, g_err_id);
         return;
     }
     mexFunction(nlhs, out, nrhs, (const mxArray**)in);
+    g_last_out = out[0];
     if (out[0])
         printf("%s -> OK %zux%zu\n", tag, mxGetM(out[0]), mxGetN(out[0]));
     else
         printf("%s -> OK\n", tag);
 }
 
-int main(void) {
+/* the complex outputs the stub writes: channel_realise element k = 2k + (2k+1) j;
+ * mmse_onetap element k = (a + 2k) - (k + 0.25) j with a = the input sum */
+static void check_out(const char* tag, int which) {
+    int ok = g_last_out != NULL && mxIsComplex(g_last_out);
+    double a0 = 0.0;
+    for (size_t k = 0; ok && k < mxGetNumberOfElements(g_last_out); ++k) {
+        double re, im;
+        tst_get_c(g_last_out, k, &re, &im);
+        if (k == 0) a0 = re;
+        if (which == 0) ok = re == 2.0 * k && im == 2.0 * k + 1;
+        else ok = im == -0.5 * (2.0 * k + 1) && re - 2.0 * k == a0;
+    }
+    printf("check %s output %s\n", tag, ok ? "OK" : "BAD");
+}
+
+/* default argument `pos` of command `cmd` (replay mode): the class and size the
+ * gateway expects, for the stub engine's dimensions (mex_stub.c) */
+static mxArray* S(const char* s);
+static mxArray* Lg(size_t n);
+static mxArray* default_arg(const char* cmd, int pos) {
+    if (pos == 0) return S(cmd);
+    if (!strcmp(cmd, "create")) return D(0);
+    if (!strcmp(cmd, "set_channel")) {
+        const double v[7] = {0, 360e3, 0, 540, 1158.2, 200, 0};
+        return pos == 2 ? M(2, 1, 0) : D(v[pos < 7 ? pos : 0]);
+    }
+    if (!strcmp(cmd, "set_snr")) return pos == 1 ? M(7, 1, 0) : D(4);
+    if (!strcmp(cmd, "add_scheme")) {
+        switch (pos) {
+            case 1: return D(24);
+            case 2: return D(14);
+            case 3: case 4: return M(540, 336, 1);
+            case 5: return M(336, 336, 0);
+            case 6: return M(16, 1, 0);
+            case 7: return M(320, 1, 0);
+            case 8: return Lg(320);
+            case 9: return M(256, 1, 1);
+            case 10: return D(2.1);
+            case 11: return D(1.02);
+            case 14: return D(2);
+            case 15: return D(1);
+            default: return D(0);
+        }
+    }
+    if (!strcmp(cmd, "build_mmse")) return D(1e-8);
+    if (!strcmp(cmd, "set_batch")) return D(8192);
+    if (!strcmp(cmd, "run")) return D(pos == 3 ? 25 : pos == 1 ? 1 : 0);
+    if (!strcmp(cmd, "channel_realise")) return D(pos == 1 ? 1 : 3);
+    if (!strcmp(cmd, "get_W")) return D(pos == 3 ? 0 : 1);
+    if (!strcmp(cmd, "mmse_onetap")) return pos == 4 ? M(16, 1, 1) : D(pos == 2 ? 4 : pos == 3 ? 0 : 1);
+    if (!strcmp(cmd, "set_noise_slot")) return D(pos == 1 ? 1 : 0);
+    if (!strcmp(cmd, "set_interpolation")) return pos == 2 ? M(336, 16, 0) : D(1);
+    if (!strcmp(cmd, "set_option")) return pos == 1 ? S("xcd") : D(1);
+    return D(1);   /* bits_per_rep, scheme_dims, path_info: scheme id 1 */
+}
+
+static int replay(int argc, char** argv) {
+    for (int i = 2; i < argc; ++i) {
+        char cmd[64];
+        int nrhs = 0, nlhs = 0;
+        mxArray* a[24];
+        if (sscanf(argv[i], "%63[^:]:%d:%d", cmd, &nrhs, &nlhs) != 3 || nrhs < 1 || nrhs > 24) {
+            printf("replay %s -> ERR parse\n", argv[i]);
+            continue;
+        }
+        for (int k = 0; k < nrhs; ++k) a[k] = default_arg(cmd, k);
+        call(argv[i], nlhs, nrhs, a);
+    }
+    return 0;
+}
+
+int main(int argc, char** argv) {
     mxArray* a[20];
+    if (argc > 1 && !strcmp(argv[1], "replay")) return replay(argc, argv);
     a[0] = S("run"); a[1] = D(1); a[2] = D(0); a[3] = D(64);
     call("run_before_create", 1, 4, a);
     a[0] = S("create");
@@ -60,6 +143,7 @@ int main(void) {
     call("run_old_7_args", 1, 7, a);
     a[0] = S("mmse_onetap"); a[1] = D(1); a[2] = D(4); a[3] = D(0); a[4] = M(16, 1, 1);
     call("mmse_onetap_documented_5_args", 1, 5, a);
+    check_out("mmse_onetap", 1);
     a[4] = M(16, 3, 0);
     call("mmse_onetap_3_vectors_real", 1, 5, a);
     a[4] = M(15, 1, 1);
@@ -75,6 +159,7 @@ int main(void) {
     call("get_W_scheme_0", 1, 4, a);
     a[0] = S("channel_realise"); a[1] = D(1); a[2] = D(3);
     call("channel_realise", 1, 3, a);
+    check_out("channel_realise", 0);
     a[3] = D(540); a[4] = D(2);
     call("channel_realise_old_5_args", 1, 5, a);
     a[0] = S("add_scheme"); a[1] = D(24); a[2] = D(14); a[3] = M(540, 336, 1); a[4] = M(540, 336, 1);

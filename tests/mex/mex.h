@@ -9,6 +9,17 @@
 #include <stddef.h>
 #include <stdint.h>
 
+/* MATLAB's two complex storage APIs: R2018a+ (-R2018a) interleaved, R2013b /
+ * R2016a separate real / imaginary planes (README.md:19-20).  The test builds
+ * the gateway once per API; -DDSCE_TEST_SPLIT selects the split one, and the
+ * other API's accessors are then not declared (a gateway that used them would
+ * not compile). */
+#ifdef DSCE_TEST_SPLIT
+#define MX_HAS_INTERLEAVED_COMPLEX 0
+#else
+#define MX_HAS_INTERLEAVED_COMPLEX 1
+#endif
+
 typedef size_t mwSize;
 typedef bool mxLogical;
 typedef enum { mxDOUBLE_CLASS, mxINT64_CLASS, mxLOGICAL_CLASS, mxCHAR_CLASS } mxClassID;
@@ -18,7 +29,8 @@ typedef struct mxArray_tag {
     mxClassID cls;
     int cplx;
     size_t m, n;
-    void* data;
+    void* data;          /* interleaved API: (re, im) pairs; split API: real plane */
+    void* imag;          /* split API: imaginary plane of a complex array */
     char* str;
 } mxArray;
 
@@ -27,17 +39,23 @@ double mxGetScalar(const mxArray* a);
 size_t mxGetNumberOfElements(const mxArray* a);
 size_t mxGetM(const mxArray* a);
 size_t mxGetN(const mxArray* a);
+#if MX_HAS_INTERLEAVED_COMPLEX
 double* mxGetDoubles(const mxArray* a);
 mxComplexDouble* mxGetComplexDoubles(const mxArray* a);
-mxLogical* mxGetLogicals(const mxArray* a);
 int64_t* mxGetInt64s(const mxArray* a);
+int mxMakeArrayComplex(mxArray* a);
+#else
+double* mxGetPr(const mxArray* a);
+double* mxGetPi(const mxArray* a);
+void* mxGetData(const mxArray* a);
+#endif
+mxLogical* mxGetLogicals(const mxArray* a);
 bool mxIsComplex(const mxArray* a);
 bool mxIsDouble(const mxArray* a);
 bool mxIsNumeric(const mxArray* a);
 bool mxIsLogical(const mxArray* a);
 bool mxIsChar(const mxArray* a);
 mxArray* mxDuplicateArray(const mxArray* a);
-int mxMakeArrayComplex(mxArray* a);
 void mxDestroyArray(mxArray* a);
 mxArray* mxCreateDoubleScalar(double v);
 mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c);
@@ -48,4 +66,8 @@ void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
 int mexAtExit(void (*fn)(void));
 void mexLock(void);
 void mexUnlock(void);
+
+/* test helpers (driver.c / mex_stub.c): element k of a complex array, either API */
+void tst_get_c(const mxArray* a, size_t k, double* re, double* im);
+void tst_set_c(mxArray* a, size_t k, double re, double im);
 #endif

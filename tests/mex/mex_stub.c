@@ -17,7 +17,7 @@ char g_err_id[64];
 /* ---- mex / mx ---------------------------------------------------------- */
 static size_t elsize(const mxArray* a) {
     switch (a->cls) {
-        case mxDOUBLE_CLASS: return a->cplx ? 16 : 8;
+        case mxDOUBLE_CLASS: return a->cplx && MX_HAS_INTERLEAVED_COMPLEX ? 16 : 8;
         case mxINT64_CLASS: return 8;
         case mxLOGICAL_CLASS: return 1;
         default: return 1;
@@ -26,8 +26,27 @@ static size_t elsize(const mxArray* a) {
 static mxArray* mk(mxClassID c, int cplx, size_t m, size_t n) {
     mxArray* a = calloc(1, sizeof *a);
     a->cls = c; a->cplx = cplx; a->m = m; a->n = n;
-    a->data = calloc(m * n ? m * n : 1, elsize(a));
+    a->data = calloc(m * n != 0 ? m * n : 1, elsize(a));
+    if (!MX_HAS_INTERLEAVED_COMPLEX && c == mxDOUBLE_CLASS && cplx) a->imag = calloc(m * n != 0 ? m * n : 1, 8);
     return a;
+}
+void tst_get_c(const mxArray* a, size_t k, double* re, double* im) {
+    if (MX_HAS_INTERLEAVED_COMPLEX) {
+        *re = ((double*)a->data)[(a->cplx ? 2 : 1) * k];
+        *im = a->cplx ? ((double*)a->data)[2 * k + 1] : 0.0;
+    } else {
+        *re = ((double*)a->data)[k];
+        *im = a->cplx ? ((double*)a->imag)[k] : 0.0;
+    }
+}
+void tst_set_c(mxArray* a, size_t k, double re, double im) {
+    if (MX_HAS_INTERLEAVED_COMPLEX) {
+        ((double*)a->data)[(a->cplx ? 2 : 1) * k] = re;
+        if (a->cplx) ((double*)a->data)[2 * k + 1] = im;
+    } else {
+        ((double*)a->data)[k] = re;
+        if (a->cplx) ((double*)a->imag)[k] = im;
+    }
 }
 int mxGetString(const mxArray* a, char* buf, mwSize len) {
     if (a->cls != mxCHAR_CLASS || strlen(a->str) + 1 > len) return 1;
@@ -43,10 +62,16 @@ double mxGetScalar(const mxArray* a) {
 size_t mxGetNumberOfElements(const mxArray* a) { return a->m * a->n; }
 size_t mxGetM(const mxArray* a) { return a->m; }
 size_t mxGetN(const mxArray* a) { return a->n; }
+#if MX_HAS_INTERLEAVED_COMPLEX
 double* mxGetDoubles(const mxArray* a) { return (a->cls == mxDOUBLE_CLASS && !a->cplx) ? a->data : NULL; }
 mxComplexDouble* mxGetComplexDoubles(const mxArray* a) { return (a->cls == mxDOUBLE_CLASS && a->cplx) ? a->data : NULL; }
-mxLogical* mxGetLogicals(const mxArray* a) { return a->cls == mxLOGICAL_CLASS ? a->data : NULL; }
 int64_t* mxGetInt64s(const mxArray* a) { return a->cls == mxINT64_CLASS ? a->data : NULL; }
+#else
+double* mxGetPr(const mxArray* a) { return a->cls == mxDOUBLE_CLASS ? a->data : NULL; }
+double* mxGetPi(const mxArray* a) { return a->cls == mxDOUBLE_CLASS ? a->imag : NULL; }
+void* mxGetData(const mxArray* a) { return a->data; }
+#endif
+mxLogical* mxGetLogicals(const mxArray* a) { return a->cls == mxLOGICAL_CLASS ? a->data : NULL; }
 bool mxIsComplex(const mxArray* a) { return a->cplx; }
 bool mxIsDouble(const mxArray* a) { return a->cls == mxDOUBLE_CLASS; }
 bool mxIsNumeric(const mxArray* a) { return a->cls == mxDOUBLE_CLASS || a->cls == mxINT64_CLASS; }
@@ -55,19 +80,22 @@ bool mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }
 mxArray* mxDuplicateArray(const mxArray* a) {
     mxArray* b = mk(a->cls, a->cplx, a->m, a->n);
     memcpy(b->data, a->data, a->m * a->n * elsize(a));
+    if (a->imag) memcpy(b->imag, a->imag, a->m * a->n * 8);
     return b;
 }
+#if MX_HAS_INTERLEAVED_COMPLEX
 int mxMakeArrayComplex(mxArray* a) {
     if (a->cls != mxDOUBLE_CLASS || a->cplx) return a->cplx;
     double* re = a->data;
-    double* c = calloc(a->m * a->n ? 2 * a->m * a->n : 2, 8);
+    double* c = calloc(a->m * a->n != 0 ? 2 * a->m * a->n : 2, 8);
     for (size_t i = 0; i < a->m * a->n; ++i) c[2 * i] = re[i];
     free(re);
     a->data = c;
     a->cplx = 1;
     return 1;
 }
-void mxDestroyArray(mxArray* a) { if (a) { free(a->data); free(a->str); free(a); } }
+#endif
+void mxDestroyArray(mxArray* a) { if (a) { free(a->data); free(a->imag); free(a->str); free(a); } }
 mxArray* mxCreateDoubleScalar(double v) { mxArray* a = mk(mxDOUBLE_CLASS, 0, 1, 1); ((double*)a->data)[0] = v; return a; }
 mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c) { return mk(mxDOUBLE_CLASS, c == mxCOMPLEX, m, n); }
 mxArray* mxCreateNumericArray(mwSize nd, const mwSize* dims, mxClassID cls, mxComplexity c) {
@@ -109,8 +137,24 @@ int dsce_scheme_dims(dsce_ctx* c, int32_t id, dsce_dims* d) {
 }
 int dsce_set_channel(dsce_ctx* c, const dsce_channel_desc* d) { (void)c; printf("  set_channel N=%d taps=%d\n", d->n_samples, d->n_taps); return 0; }
 int dsce_set_snr(dsce_ctx* c, const double* p, int32_t n, int32_t it) { (void)c; (void)p; printf("  set_snr %d %d\n", n, it); return 0; }
+/* the driver's test arrays (driver.c M()): element i = (1 + i % 7) - (1 + i % 5) j
+ * (complex) or 1 + i % 7 (real); the ABI must see them interleaved */
+static int interleaved_ok(const double* z, size_t n, int was_complex) {
+    for (size_t i = 0; i < n; ++i)
+        if (z[2 * i] != 1.0 + (double)(i % 7) || z[2 * i + 1] != (was_complex ? -(1.0 + (double)(i % 5)) : 0.0))
+            return 0;
+    return 1;
+}
 int dsce_add_scheme(dsce_ctx* c, const dsce_scheme_desc* d, int32_t* id) {
     (void)c;
+    {
+        const size_t ng = (size_t)SN * d->n_subcarriers * d->n_symbols;
+        const size_t np = (size_t)d->n_subcarriers * d->n_symbols * d->n_tx_symbols;
+        printf("  check add_scheme values %s\n",
+               interleaved_ok(d->G, ng, 1) && interleaved_ok(d->Q, ng, 1) && interleaved_ok(d->P, np, 0) &&
+                       interleaved_ok(d->symbols, (size_t)d->mod_order, 1)
+                   ? "OK" : "BAD");
+    }
     /* read every input like the engine does */
     double acc = 0.0;
     size_t n = (size_t)SN * d->n_subcarriers * d->n_symbols;
@@ -134,7 +178,7 @@ int dsce_run(dsce_ctx* c, uint64_t s, uint64_t f, uint64_t n, int64_t* e) {
 int dsce_bits_per_rep(dsce_ctx* c, int32_t id, int64_t* b) { (void)c; (void)id; b[0] = 2560; b[1] = 1280; return 0; }
 int dsce_channel_realise(dsce_ctx* c, uint64_t s, uint64_t r, double* ir) {
     (void)c; (void)s; (void)r;
-    for (int i = 0; i < 2 * SN * STAPS; ++i) ir[i] = i;
+    for (int i = 0; i < 2 * SN * STAPS; ++i) ir[i] = i;      /* element k = 2k + (2k + 1) j */
     return 0;
 }
 int dsce_get_W(dsce_ctx* c, int32_t id, int32_t k, int32_t v, double* w) {
@@ -148,7 +192,8 @@ int dsce_mmse_onetap(dsce_ctx* c, int32_t id, int32_t k, int32_t v, const double
     double a = 0.0;
     if (k < 0 || k >= SSNR) return DSCE_EINVAL;
     for (int i = 0; i < 2 * SNP * n; ++i) a += hp[i];
-    for (int i = 0; i < 2 * SLK * n; ++i) h[i] = a;
+    printf("  check mmse_onetap values %s\n", interleaved_ok(hp, (size_t)SNP * n, 1) || interleaved_ok(hp, (size_t)SNP * n, 0) ? "OK" : "BAD");
+    for (int i = 0; i < 2 * SLK * n; ++i) h[i] = (i & 1) ? -0.5 * i : a + i;
     return 0;
 }
 int dsce_set_noise_slot(dsce_ctx* c, int32_t id, int32_t s) { (void)c; (void)id; (void)s; return 0; }
@@ -156,6 +201,7 @@ int dsce_set_interpolation(dsce_ctx* c, int32_t id, const double* I) {
     (void)c; (void)id;
     double a = 0.0;
     for (int i = 0; i < 2 * SLK * SNP; ++i) a += I[i];
+    printf("  check set_interpolation values %s\n", interleaved_ok(I, (size_t)SLK * SNP, 0) ? "OK" : "BAD");
     printf("  set_interpolation (%g)\n", a != a ? 1.0 : 0.0);
     return 0;
 }

@@ -1,8 +1,11 @@
 """C5 (48 subcarriers at SR 720 kHz, N = 1080, NP = 32 pilots, 3
 channel taps; build-defined scale-up of the script's geometry) against the CPU
-oracle: Jakes taps, pilot correlations, W / W0, per-unit traces of every stage
-and (OFDM) bit-error counts.  Two of the 16 SNR points keep the literal oracle
-(dense Q'HG, full(W)) within a couple of minutes."""
+oracle, all three schemes of BASELINE config 5 (OFDM, FBMC auxiliary = Fig. 3,
+FBMC data spreading = Fig. 4): Jakes taps, pilot correlations, W / W0, per-unit
+traces of every stage and bit-error counts over 64 realisations.  Two of the
+16 SNR points (one for FBMC) keep the oracle within a couple of minutes; for
+FBMC the oracle forms D_hat from W's stored non-zeros (refsim.simulate
+w_sparse: full(W) is 1 GB per evaluation at LK = 1440, NP = 32)."""
 import numpy as np
 import pytest
 
@@ -26,16 +29,17 @@ def _check_w(eng, mm, nsnr):
             assert np.all((np.abs(wg - wo) <= tol) | border), (k, var)
 
 
-def _check_trace(S, name, eng, rep, snrs):
-    """Every stage of a unit: y, hP, diag(D_hat), y_est, y_perf, decisions."""
+def _check_trace(S, name, eng, rep, snrs, yperf=False, w_sparse=False):
+    """Every stage of a unit: y, hP, diag(D_hat), y_est (y_perf: also the
+    perfect-CSI IC input of every row, unfused FBMC passes), decisions."""
     tr = {}
-    harness.simulate(S, SEED, rep, 1, [name], trace=tr)
+    harness.simulate(S, SEED, rep, 1, [name], trace=tr, w_sparse=w_sparse)
     for k in snrs:
         g = eng.trace_unit(0, SEED, rep, k)
         u = tr["units"][k]
         np.testing.assert_allclose(g["y"], u["y"], rtol=0, atol=1e-10)
         for st in range(S.n_iter + 1):
-            for key in ("hp", "hest", "yest"):
+            for key in ("hp", "hest", "yest") + (("yperf",) if yperf else ()):
                 np.testing.assert_allclose(g[key][st], u[key][st], rtol=0, atol=1e-9, err_msg="%s %d" % (key, st))
             for key, mk in (("dec_e", "margin_e"), ("dec_p", "margin_p")):
                 assert np.all((g[key][st] == u[key][st]) | (u[mk][st] < 1e-9)), (key, st)
@@ -64,11 +68,29 @@ def test_c5_ofdm_matches_oracle():
     eng.close()
 
 
-def test_c5_fbmc_aux_matches_oracle():
-    S = harness.setup("c5", schemes=("fbmc_aux",), snr_db=SNR[1:])
-    assert S.schemes["fbmc_aux"]["G"].shape[1] == 1440
+def _check_counts(S, name, eng, first, n, w_sparse=False):
+    cg = eng.run(SEED, first, n)
+    res = harness.simulate(S, SEED, first, n, [name], w_sparse=w_sparse)
+    assert cg.shape == res["err"].shape
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
+    assert res["err"].sum() > 0
+    return cg
+
+
+@pytest.mark.parametrize("name", ["fbmc_aux", "fbmc_cod"])
+def test_c5_fbmc_matches_oracle(name):
+    """C5 FBMC auxiliary (Fig. 3) and data spreading (Fig. 4, IIC.m:106-210,
+    despread detection script:436, :520) at 48 x 30: W / W0 of the 32-pilot
+    estimator, a per-element trace of every stage of one unit (y_perf of every
+    row: the unfused perfect-CSI passes), and the counts of 64 realisations."""
+    S = harness.setup("c5", schemes=(name,), snr_db=SNR[1:])
+    sc = S.schemes[name]
+    assert sc["G"].shape[1] == 1440 and len(sc["pilot_pos"]) == 32 and bool(sc["despread"]) == (name == "fbmc_cod")
     eng = harness.engine(S, batch=64)
-    mm = harness.oracle_mmse(S, "fbmc_aux")
+    mm = harness.oracle_mmse(S, name)
     _check_w(eng, mm, 1)
-    _check_trace(S, "fbmc_aux", eng, 2, (0,))
+    _check_trace(S, name, eng, 2, (0,), yperf=True, w_sparse=True)
+    _check_counts(S, name, eng, 0, 64, w_sparse=True)
+    path = eng.path_info(0)
+    assert ("stage_split" in path) == (name == "fbmc_cod") and "pic_passes" in path, path
     eng.close()

@@ -69,12 +69,15 @@ def test_mmse_estimator_matches_oracle(ofdm):
 
 # ---------------------------------------------------------------------------
 # The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
-# k_pilot_pre + k_mic_fft (Q' H_hat G by FFT) for the MMSE IC stages, k_pic_fft
-# for the perfect-CSI IC chain, k_stage_fused for the one-tap stage); the W
+# k_txrx_fft for TX / channel / noisy receiver front, k_pic_fft for the whole
+# perfect-CSI branch (stage 0 + IC chain), k_mic_pilot + k_mic_data for every
+# stage of the MMSE branch (Q' H_hat G by FFT)); the r02 per-stage path
+# (k_stage0_fft + k_mic_fft with the fused pilot pass, mic2 0) and the W
 # contraction (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"mic_fft", "pilot_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
-W_PATH = BENCH_PATH - {"mic_fft", "pilot_fused"} | {"wpair3_fused"}
+BENCH_PATH = {"mic_fft", "mic_stages", "pic_fft", "noise_fused", "txrx_fft"}
+STAGE_PATH = {"mic_fft", "pilot_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
+W_PATH = STAGE_PATH - {"mic_fft", "pilot_fused"} | {"wpair3_fused"}
 
 
 def _check_trace(g, u, name, tol=1e-9):
@@ -100,11 +103,11 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
     oracle (literal W of script:493-511): k_mic_fft's y_est and diag(D_hat),
     k_pilot_pre's LS pilots, k_pic_fft's y_perf (data rows: the chain forms
     only those) and both branches' decisions; the same for the fused W
-    contraction (mmse_ic 0) and the matrix-core chain k_pic_mfma (pic_chain 2)."""
+    contraction (mmse_ic 0)."""
     S, eng, mm = ofdm
     rows = S.schemes["ofdm"]["data_pos"]
-    for chain, mic, path in ((3, 1, BENCH_PATH), (3, 0, W_PATH), (2, 1, BENCH_PATH - {"pic_fft"} | {"pic_mfma"})):
-        eng.set_option("pic_chain", chain)
+    for mic2, mic, path in ((1, 1, BENCH_PATH), (0, 1, STAGE_PATH), (1, 0, W_PATH)):
+        eng.set_option("mic2", mic2)
         eng.set_option("mmse_ic", mic)
         for rep in (5, 70):
             tr = {}
@@ -113,10 +116,10 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
                 g = eng.trace_unit(0, SEED, rep, k)
                 assert path <= eng.path_info(0), eng.path_info(0)
                 u = tr["units"][k]
-                ns = _check_trace(g, u, "chain %d rep %d snr %d" % (chain, rep, k))
+                ns = _check_trace(g, u, "mic2 %d mmse_ic %d rep %d snr %d" % (mic2, mic, rep, k))
                 for st in range(1, ns):
                     np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
-    eng.set_option("pic_chain", 3)
+    eng.set_option("mic2", 1)
     eng.set_option("mmse_ic", 1)
 
 
@@ -156,8 +159,11 @@ def test_ic_iteration_counts_match_oracle(n_iter):
     eng = harness.engine(S, batch=64)
     cg = eng.run(SEED, 0, 64)
     path = eng.path_info(0)
-    assert BENCH_PATH - {"pilot_fused"} <= path, path
-    assert ("pilot_fused" in path) == (n_iter >= 2), path
+    assert BENCH_PATH <= path, path
+    eng.set_option("mic2", 0)                   # the per-stage path: the pilot pass fuses from niter 2 on
+    assert np.array_equal(eng.run(SEED, 0, 64), cg)
+    assert ("pilot_fused" in eng.path_info(0)) == (n_iter >= 2), eng.path_info(0)
+    eng.set_option("mic2", 1)
     res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
     assert cg.shape == res["err"].shape
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
@@ -202,6 +208,10 @@ def test_fbmc_error_counts(fbmc):
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
     _check_mse(eng, res)
     eng.enable_mse(False)
+    # ragged runs (padding lanes of a partial wave count nothing): the same
+    # 64 realisations as 25 + 39, and as 1 + 63
+    np.testing.assert_array_equal(eng.run(SEED, 64, 25) + eng.run(SEED, 89, 39), cg)
+    np.testing.assert_array_equal(eng.run(SEED, 64, 1) + eng.run(SEED, 65, 63), cg)
 
 
 def _check_mse(eng, res):
@@ -239,6 +249,63 @@ def test_counts_are_additive_and_batch_invariant(ofdm):
     c = eng.run(SEED, 0, 512)
     eng.set_batch(256)
     np.testing.assert_array_equal(a, c)
+
+
+def test_any_repetition_count(ofdm):
+    """dsce_run takes the script's own NrRepetitions as is — 25 (script:19) and
+    1000 (the paper's, script:44) — not only multiples of one wavefront: the
+    padding realisations of a partial wave are simulated but counted nowhere.
+    25 realisations against the oracle (counts and MSE sums); 1000 against
+    every split and batch size; 0 realisations add nothing."""
+    S, eng, _ = ofdm
+    eng.enable_mse()
+    c25 = eng.run(SEED, 0, 25)
+    assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+    res = harness.simulate(S, SEED, 0, 25, ["ofdm"])
+    assert np.abs(c25 - res["err"]).sum() <= 8 * res["borderline"].sum(), c25 - res["err"]
+    _check_mse(eng, res)
+    eng.enable_mse(False)
+    assert not eng.run(SEED, 0, 0).any()
+    a = eng.run(SEED, 0, 1000)
+    np.testing.assert_array_equal(eng.run(SEED, 0, 25) + eng.run(SEED, 25, 975), a)
+    np.testing.assert_array_equal(eng.run(SEED, 0, 999) + eng.run(SEED, 999, 1), a)
+    eng.set_batch(64)
+    np.testing.assert_array_equal(sum(eng.run(SEED, 25 * k, 25) for k in range(40)), a)
+    np.testing.assert_array_equal(eng.run(SEED, 0, 1000), a)
+    eng.set_batch(256)
+    # the W-contraction path of the same scheme masks its padding lanes too
+    eng.set_option("mmse_ic", 0)
+    np.testing.assert_array_equal(eng.run(SEED, 0, 25) + eng.run(SEED, 25, 975), eng.run(SEED, 0, 1000))
+    c25w = eng.run(SEED, 0, 25)
+    eng.set_option("mmse_ic", 1)
+    assert np.abs(c25w - res["err"]).sum() <= 8 * res["borderline"].sum()
+
+
+def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
+    """build_mic keeps the structured MMSE IC (k_mic_fft: D_hat = Q' H_hat G)
+    only if Q' H_hat G reproduces EVERY entry of the thresholded W — the
+    off-diagonal entries the IC subtraction uses (script:482-484), not just
+    diag(D_hat).  At ZeroThreshold 1e-5 (instead of the script's 1e-8,
+    script:34) the diagonal still agrees (oracle: 0 x tolerance) but the
+    entries the threshold drops off the diagonal do not (1.04 x): the engine
+    must fall back to the W contraction and still equal the oracle's literal
+    thresholded W."""
+    from types import SimpleNamespace
+    S = SimpleNamespace(**vars(harness.setup("default", schemes=("ofdm",))))
+    S.zero_threshold = 1e-5
+    eng = harness.engine(S, batch=64)
+    cg = eng.run(SEED, 0, 64)
+    path = eng.path_info(0)
+    assert "mic_fft" not in path and "wpair3_fused" in path, path
+    res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
+    eng.close()
+    # the script's threshold keeps the structured path (C2: 6e-5 x tolerance)
+    S.zero_threshold = 1e-8
+    eng = harness.engine(S, batch=64)
+    eng.run(SEED, 0, 64)
+    assert "mic_fft" in eng.path_info(0)
+    eng.close()
 
 
 def test_psace_mmse_plugin(ofdm):
@@ -283,9 +350,8 @@ def test_stage_variants_agree(name):
     XCD-aware work order on/off, SNR-chunked receiver, two streams, 4-MFMA
     instead of 3M complex products, the VALU contraction, the MMSE stage as its
     own kernels instead of fused into the contraction, the perfect-CSI chain as
-    per-iteration passes / VALU chain instead of k_pic_fft, the fused
+    per-iteration passes instead of k_pic_fft, the fused
     epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave,
-    the matrix-core perfect-CSI chain (k_pic_mfma) instead of the FFT chain,
     the W contraction instead of the structured MMSE IC (k_mic_fft), decisions
     passed between the stages as v / u instead of symbol indices, k_mic_fft's
     taps on the VALU instead of the matrix cores, the pilot pre-pass from W's
@@ -306,11 +372,11 @@ def test_stage_variants_agree(name):
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(rb))
     eng.set_option("stage_rb", 8)
     variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2}, {"streams": 2}, {"wpair_3m": 0},
-                {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0}, {"pic_chain": 1}, {"pic_chain": 2},
+                {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0},
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
                 {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
-                {"mic_yic": 0}, {"pilot_fuse": 0})
+                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
@@ -328,6 +394,9 @@ def test_options_are_validated():
         eng.set_option("no_such_option", 1)
     with pytest.raises(DsceError):
         eng.set_option("stage_rb", 5)
+    for retired in (1, 2):                      # k_pic_chain / k_pic_mfma, retired in r03
+        with pytest.raises(DsceError):
+            eng.set_option("pic_chain", retired)
     assert eng.get_option("fuse_stage") == 1
     eng.close()
 

@@ -3,6 +3,10 @@ against a test-only mex.h stand-in and a recording stub of the C-ABI, run
 under AddressSanitizer: every command checks its argument count and classes,
 and every output is sized from dsce_scheme_dims (the stub writes exactly what
 the engine writes, so an undersized output would be a reported heap overflow).
+The gateway is built twice: for MATLAB's interleaved complex API (R2018a+) and
+for the split real / imaginary planes of R2013b / R2016a (README.md:19-20).
+Every dsce_mex(...) call in INTEGRATION.md and in the PSACE 'MMSE' patch is
+replayed through it, so the documented binding cannot drift from the gateway.
 MATLAB itself is not in the image; this checks the gateway's own logic."""
 import os
 import re
@@ -17,24 +21,146 @@ MEX = os.path.join(harness.ROOT, "tests", "mex")
 GATEWAY = os.path.join(harness.PKG, "matlab", "dsce_mex.c")
 
 
-@pytest.fixture(scope="module")
-def results(tmp_path_factory):
-    if not shutil.which("gcc"):
-        pytest.skip("gcc not available")
-    d = tmp_path_factory.mktemp("mex")
-    exe = str(d / "drv")
+INTEGRATION = os.path.join(harness.ROOT, "INTEGRATION.md")
+PATCH = os.path.join(harness.PKG, "matlab", "psace_mmse.patch")
+
+
+def _build(d, split):
+    exe = str(d / ("drv_split" if split else "drv"))
     subprocess.run(["gcc", "-std=c11", "-g", "-O1", "-fsanitize=address", "-fno-omit-frame-pointer",
-                    "-DMATLAB_MEX_FILE", "-D_GNU_SOURCE", "-I", MEX, "-I", os.path.join(harness.ROOT, "include"),
-                    GATEWAY, os.path.join(MEX, "mex_stub.c"), os.path.join(MEX, "driver.c"), "-o", exe, "-lm"],
+                    "-Werror=implicit-function-declaration", "-DMATLAB_MEX_FILE", "-D_GNU_SOURCE"]
+                   + (["-DDSCE_TEST_SPLIT"] if split else [])
+                   + ["-I", MEX, "-I", os.path.join(harness.ROOT, "include"),
+                      GATEWAY, os.path.join(MEX, "mex_stub.c"), os.path.join(MEX, "driver.c"), "-o", exe, "-lm"],
                    check=True)
-    out = subprocess.run([exe], capture_output=True, text=True, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"),
-                         timeout=120)
+    return exe
+
+
+def _run(exe, args=()):
+    out = subprocess.run([exe, *args], capture_output=True, text=True,
+                         env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"), timeout=120)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert "AddressSanitizer" not in out.stderr, out.stderr[-3000:]
     res = {}
-    for m in re.finditer(r"^(\w+) -> (OK|ERR) ?(\S*)$", out.stdout, re.M):
+    for m in re.finditer(r"^(\S+) -> (OK|ERR) ?(\S*)$", out.stdout, re.M):
         res[m.group(1)] = (m.group(2), m.group(3))
+    return res, out.stdout
+
+
+@pytest.fixture(scope="module", params=["interleaved", "split"])
+def built(request, tmp_path_factory):
+    if not shutil.which("gcc"):
+        pytest.skip("gcc not available")
+    return _build(tmp_path_factory.mktemp("mex"), request.param == "split")
+
+
+@pytest.fixture(scope="module")
+def results(built):
+    res, stdout = _run(built)
+    assert "BAD" not in stdout, [l for l in stdout.splitlines() if "BAD" in l]
+    assert stdout.count("check ") >= 6
     return res
+
+
+# ---------------------------------------------------------------------------
+# dsce_mex(...) calls of a MATLAB text: (command, number of inputs, outputs)
+# ---------------------------------------------------------------------------
+def _strip_comment(line):
+    q = False
+    for i, ch in enumerate(line):
+        if ch == "'":
+            q = not q
+        elif ch == "%" and not q:
+            return line[:i]
+    return line
+
+
+def _statements(text):
+    out, cur = [], ""
+    for line in text.splitlines():
+        line = _strip_comment(line).rstrip()
+        if line.endswith("..."):
+            cur += line[:-3] + " "
+            continue
+        out.append(cur + line)
+        cur = ""
+    if cur:
+        out.append(cur)
+    return out
+
+
+def _calls(text):
+    calls = []
+    for st in _statements(text):
+        for m in re.finditer(r"dsce_mex\(", st):
+            i, depth, q, args, a0 = m.end(), 1, False, [], m.end()
+            while i < len(st) and depth:
+                ch = st[i]
+                if ch == "'":
+                    q = not q
+                elif not q and ch in "([{":
+                    depth += 1
+                elif not q and ch in ")]}":
+                    depth -= 1
+                    if depth == 0:
+                        args.append(st[a0:i].strip())
+                elif not q and ch == "," and depth == 1:
+                    args.append(st[a0:i].strip())
+                    a0 = i + 1
+                i += 1
+            assert depth == 0, "unbalanced dsce_mex call: " + st
+            lhs = st[:m.start()].rstrip()
+            nlhs = 0
+            if lhs.endswith("=") and not lhs.endswith("=="):
+                head = lhs[:-1].strip()
+                nlhs = len(head.strip("[]").split(",")) if head.startswith("[") else 1
+            calls.append((args[0].strip("'"), len(args), nlhs))
+    return calls
+
+
+def _integration_calls():
+    text = open(INTEGRATION).read()
+    code = "\n".join(re.findall(r"```matlab\n(.*?)```", text, re.S))
+    inline = [c for c in re.findall(r"`(dsce_mex\([^`]*\))`", text) if "..." not in c]
+    return _calls(code + "\n" + "\n".join(inline))
+
+
+def _patch_calls():
+    plus = [l[1:] for l in open(PATCH).read().splitlines() if l.startswith("+") and not l.startswith("+++")]
+    return _calls("\n".join(plus))
+
+
+def test_integration_md_calls_run_through_the_gateway(built):
+    """Every dsce_mex(...) call INTEGRATION.md documents (and the one inside the
+    PSACE 'MMSE' patch) is accepted by the gateway with that many inputs and
+    outputs: a documented call the gateway rejects (round-2: 'run' with 7
+    arguments) fails here."""
+    calls = _integration_calls() + _patch_calls()
+    cmds = {c[0] for c in calls}
+    assert {"create", "set_channel", "set_snr", "add_scheme", "build_mmse", "run", "bits_per_rep",
+            "mmse_onetap", "set_interpolation", "set_noise_slot"} <= cmds, cmds
+    assert ("run", 4, 1) in calls and ("mmse_onetap", 5, 1) in _patch_calls()
+    # create first (the gateway refuses any other command before it)
+    triples = ["create:1:0"] + ["%s:%d:%d" % c for c in calls if c[0] != "create"]
+    res, stdout = _run(built, ["replay", *triples])
+    assert "BAD" not in stdout
+    for t in triples:
+        assert res.get(t, ("missing",))[0] == "OK", (t, res.get(t), stdout[-2000:])
+
+
+def test_psace_patch_applies_to_the_reference(tmp_path):
+    """The patch applies cleanly to the reference's class (when the reference
+    is present: this container, not the GPU box) and leaves no error() stub."""
+    ref = "/root/reference/+ChannelEstimation/PilotSymbolAidedChannelEstimation.m"
+    if not os.path.exists(ref) or not shutil.which("patch"):
+        pytest.skip("reference or patch(1) not available")
+    d = tmp_path / "+ChannelEstimation"
+    d.mkdir()
+    shutil.copy(ref, d / "PilotSymbolAidedChannelEstimation.m")
+    out = subprocess.run(["patch", "-p1", "-i", PATCH], cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    body = (d / "PilotSymbolAidedChannelEstimation.m").read_text()
+    assert "Needs to be" not in body and body.count("dsce_mex('mmse_onetap'") == 1
 
 
 def test_outputs_sized_from_engine_state(results):

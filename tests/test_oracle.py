@@ -218,7 +218,7 @@ def _same(a, b, path="", rtol=1e-10):
 
 
 @pytest.mark.parametrize("name,fname,schemes", [("default", "setup_default.json", ("fbmc_aux", "fbmc_cod", "ofdm")),
-                                                ("c5", "setup_c5.json", ("fbmc_aux", "ofdm"))])
+                                                ("c5", "setup_c5.json", ("fbmc_aux", "fbmc_cod", "ofdm"))])
 def test_setup_fixtures(name, fname, schemes):
     got = json.loads(json.dumps(_golden().setup_fixture(name, schemes)))
     _same(got, json.load(open(os.path.join(GOLD, fname))))
@@ -232,3 +232,24 @@ def test_oracle_fixtures(tag):
     ref = json.load(open(os.path.join(GOLD, "oracle_%s_small.json" % tag)))
     assert got["err_reps_0_2"] == ref["err_reps_0_2"] and got["nbits"] == ref["nbits"]
     _same(got, ref, rtol=1e-9)
+
+
+def test_sparse_w_contraction_equals_literal_full_w():
+    """refsim.simulate(w_sparse=True) forms D_hat = reshape(W hP) from W's stored
+    non-zeros (used for the C5 FBMC parity tests, where full(W) is 1 GB per
+    evaluation) instead of the literal full(W) .* hP summed over the third
+    dimension (script:417-425, :493-511): identical counts, traces equal to
+    summation-order rounding.  C4 (FBMC data spreading), 2 realisations."""
+    import harness
+    from oracle import refsim
+    S = harness.setup("default", schemes=("fbmc_cod",), snr_db=[35.0])
+    mm = harness.oracle_mmse(S, "fbmc_cod")
+    sc = S.schemes["fbmc_cod"]
+    ta, tb = {}, {}
+    a = refsim.simulate(0x5EED0004, 3, 2, S.chan, [sc], S.pn_time, S.n_iter, [mm], trace=ta)
+    b = refsim.simulate(0x5EED0004, 3, 2, S.chan, [sc], S.pn_time, S.n_iter, [mm], trace=tb, w_sparse=True)
+    np.testing.assert_array_equal(a["err"], b["err"])
+    np.testing.assert_allclose(a["mse_err"], b["mse_err"], rtol=1e-12)
+    for ua, ub in zip(ta["units"], tb["units"]):
+        for key in ("hp", "hest", "yest", "yperf"):
+            np.testing.assert_allclose(np.array(ub[key]), np.array(ua[key]), rtol=0, atol=1e-12)

@@ -68,12 +68,11 @@ def test_precoders_cancel_pilot_interference(both):
 def test_product_host_mirror_equals_oracle_setup(both, key):
     O, S = both
     o, p = O["schemes"][key], S.schemes[key]
-    tie = key == "fbmc_cod"          # P and its no-edge mask: see test_coding_precoder_tie_class
-    for f in (("G", "Q") if tie else ("G", "Q", "P")):
+    for f in ("G", "Q", "P"):
         a, b = o[f], getattr(p, f)
         assert a.shape == b.shape, (key, f)
         np.testing.assert_allclose(b, a, rtol=0, atol=1e-12 * np.abs(a).max(), err_msg="%s %s" % (key, f))
-    for f, g in (("pilot_pos", "pilot_pos"), ("data_pos", "data_pos"), ("considered", "considered_symbols"))[:2 if tie else 3]:
+    for f, g in (("pilot_pos", "pilot_pos"), ("data_pos", "data_pos"), ("considered", "considered_symbols")):
         np.testing.assert_array_equal(np.asarray(getattr(p, g)), np.asarray(o[f]), err_msg="%s %s" % (key, f))
     for f in ("kappa", "data_div"):
         assert abs(getattr(p, f) - o[f]) <= 1e-12 * abs(o[f]), (key, f)
@@ -88,11 +87,12 @@ def test_coding_precoder_tie_class(both):
     pilot's interferer set is |D(pilot, :)| >= the 21st-largest corner
     interference magnitude (IIC.m:113-114), and at C4 that threshold falls
     inside a class of 8 interferers whose magnitudes are equal in exact
-    arithmetic (0.0368577...); which 4 of them pass depends on the last bit of
-    the FFTs (MATLAB's FFTW: unknowable offline, so the choice is unpinned).
-    Pinned: per pilot the same number of interferers and the same set outside
-    the tie class, the same data-symbol count and power reduction, and both
-    precoders cancel the imaginary interference at the pilots (SIR)."""
+    arithmetic (0.0368577...).  With a plain floating-point >= the members
+    that pass depend on the last bit of the FFTs (MATLAB's FFTW choice is
+    unknowable offline; the two restatements used to pick different ones).
+    Both now apply the rule in exact-arithmetic semantics (TIE_RTOL = 1e-12:
+    the whole class passes), so product and oracle build the same precoder;
+    against MATLAB the C4 precoder stays unpinned."""
     O, S = both
     m = O["schemes"]["fbmc_cod"]["iic"]
     prod = S.schemes["fbmc_cod"].extras["iic"]
@@ -107,11 +107,14 @@ def test_coding_precoder_tie_class(both):
     thr = np.sort(osu.col(IM))[::-1][20]
     ci_o, ci_p = np.asarray(m["considered"]), np.asarray(prod.ConsideredInterferenceMatrix).reshape(-1, order="F")
     pil = np.flatnonzero(pm == 1)
+    n_tie = 0
     for ip in range(1, len(pil) + 1):
         so, sp = set(np.flatnonzero(ci_o == -ip)), set(np.flatnonzero(ci_p == -ip))
-        assert len(so) == len(sp)
-        for x in so ^ sp:
-            assert abs(abs(D[pil[ip - 1], x]) - thr) <= 1e-12 * thr, (ip, x)
+        assert so == sp, ip
+        tie = {x for x in range(D.shape[1]) if abs(abs(D[pil[ip - 1], x]) - thr) <= 1e-12 * thr}
+        assert tie <= so, ip                            # the whole exact-arithmetic tie class passes
+        n_tie += len(tie)
+    assert n_tie > 0                                    # the tie exists at C4
     assert m["ND"] == prod.NrDataSymbols and abs(m["DPR"] - prod.DataPowerReduction) < 1e-12
     assert np.all(prod.SIR_dB > 28.0) and np.all(m["SIR_dB"] > 28.0)
 
