@@ -337,8 +337,10 @@ def main():
     # roofline of the dominant kernel (the MMSE IC: k_mic_fft where the scheme is
     # FFT-form OFDM, else the W contraction k_wcontract; HIP events on the
     # engine's stream)
+    md_l, _ = eng.kernel_time("k_mic_data")
     mic_l, mic_ms = eng.kernel_time("k_mic_fft")
-    kname = "k_mic_fft" if mic_l else "k_wcontract"
+    kname = "k_mic_data" if md_l else "k_mic_fft" if mic_l else "k_wcontract"
+    mic_l = mic_l or md_l
     launches, wc_ms = eng.kernel_time(kname)
     flops = 0.0
     executed = 0.0
@@ -364,7 +366,8 @@ def main():
     hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
     bound = "hbm" if hbm_frac is not None and achieved_tf and hbm_frac > achieved_tf / FP64_PEAK_TFLOPS else "mfma"
     kernels = {}
-    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_fft", "perfect_ic", "k_stage"):
+    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_fft", "k_mic_pilot", "k_mic_data",
+              "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
         kernels[k] = {"launches": n, "ms": round(ms, 3)}
     ber = {}
@@ -403,7 +406,12 @@ def main():
         "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
                    "parallelism": "dp%d" % world, "options": options},
         "roofline": {"bound": bound,
-                     "kernel": ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v; H_hat = Bv hP "
+                     "kernel": ("k_mic_data: every MMSE stage (one-tap + IC iterations) of the OFDM symbols without "
+                                "pilots, decisions in registers: per stage H_hat = Bv hP on the matrix cores (3M), "
+                                "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain, one-tap + detection on the "
+                                "VALU; FP64 roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both "
+                                "peaks 78.6 TF)") if kname == "k_mic_data" else
+                               ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v; H_hat = Bv hP "
                                 "on the matrix cores (3M), DFT-24 chain + one-tap + detection on the VALU; FP64 "
                                 "roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both peaks "
                                 "78.6 TF)") if mic_l else
@@ -422,7 +430,11 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
                      "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
                      "flops_per_launch": flops / launches if launches else None,
-                     "work_model": ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
+                     "work_model": ("per unit and data symbol: stage 0 window sums ntap x NP + 24; per IC stage the "
+                                    "estimated taps ntap x 24 x NP CMACs, their window sums ntap x 24, the channel "
+                                    "ntap x 24, diag(D_hat_prev) v 24, this stage's window sums ntap x NP and diag 24 "
+                                    "(8 flops per CMAC) + two DFT-24 at 5 n log2 n flops") if kname == "k_mic_data" else
+                                   ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
                                     "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
                                     "at 5 n log2 n flops; with pilot_fuse (iterations 1..niter-1) also the next iteration's pilot-symbol "
                                     "chains (taps, channel, diag(D_hat) u, two DFT-24); peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else

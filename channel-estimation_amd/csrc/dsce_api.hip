@@ -1128,8 +1128,12 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                     s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, false, true);
                 }
                 {
-                    Timed t(c, "k_mic_stages");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd);
+                    Timed t(c, "k_mic_pilot");
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1);
+                }
+                {
+                    Timed t(c, "k_mic_data");
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2);
                 }
                 if (to && to->hp_stages)
                     for (int st = 0; st <= c->niter; ++st)

@@ -194,8 +194,9 @@ unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, co
 // the perfect-CSI branch then runs k_pic_fft with its stage 0
 bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
                     int niter);
+// part: 1 = k_mic_pilot, 2 = k_mic_data (the data kernel reads the pilot kernel's hpa)
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd);
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part);
 unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
                          int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                          const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,

@@ -34,6 +34,17 @@ __device__ __forceinline__ int wave_sum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// Integer wave sum by DPP (quad perms, half-row / row mirrors, row broadcasts)
+// instead of six ds_bpermute round trips; every lane returns the total.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+    v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false);   // row_mirror: every lane holds its row's sum
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 into rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1240,7 +1251,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             u[a].x = data ? nv.x : u[a].x;
             u[a].y = data ? nv.y : u[a].y;
         }
-        cntl[w][0] = wave_sum(rl < o.rvalid ? ncnt : 0);
+        cntl[w][0] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);
         ncnt = 0;
     }
     for (int it = 1; it <= niter; ++it) {
@@ -1342,7 +1353,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             u[a].x = data ? nv.x : u[a].x;
             u[a].y = data ? nv.y : u[a].y;
         }
-        cntl[w][it] = wave_sum(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
+        cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
     }
     // counters of every stage, summed over the block's 4 waves: thread
@@ -2136,29 +2147,26 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
 template <int NT, int SH, int NP, bool TRACE, bool PIL, class ALoad, class BsLoad>
 __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
                                             const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
-                                            const double2* wrow, double2* sl, double2 (*shp)[NP][17], int (*cntl),
-                                            const ALoad& A, const BsLoad& Bs, int row0, int unit, int unit_mf,
-                                            int ul, int l, int r, int U, int R, int rl, int snr) {
+                                            const double2* wrow, double2* sl, double2 (*shp)[NP][17],
+                                            const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
+                                            int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
+                                            int snr) {
     const int cq = (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
     const double sqk = 1.0 / sk.inv_sqrt_kappa;
     const bool valid = rl < o.rvalid;
     // per-unit operands, read once: y, transmitted indices, the rows' constant
-    // part of v (precoded pilots / zero rows), PIL: the transmitted pilots
-    double2 yv[6], v[6], xpv[PIL ? 6 : 1];
+    // part of v (precoded pilots / zero rows); PIL: the transmitted pilots come
+    // from the block's LDS table xpb[pilot][unit]
+    double2 yv[6], v[6];
     unsigned txp[2] = {0u, 0u};
-    int pc[PIL ? 6 : 1];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int row = row0 + 4 * a + r;
         yv[a] = o.y[(size_t)row * U + unit];
         v[a] = o.xs[(size_t)row * R + rl];
         txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        if (PIL) {
-            pc[a] = rpc[4 * a + r];
-            xpv[a] = o.xp[(size_t)min(max(pc[a], 0), NP - 1) * R + rl];
-        }
     }
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
@@ -2168,17 +2176,46 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
     double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0;       // window sums of the previous stage's taps
-    double2 hb[NP / 4];                                     // B operand of the tap GEMM: hP_{s-1}
+    // B operand of the tap GEMM (hP_{s-1}) and this stage's LS pilots (a quarter
+    // per lane, for diag(D_hat_s)); the data kernel prefetches both for stage
+    // s + 1 at the end of stage s and folds hn4 into the window sums sn at once
+    double2 hb[NP / 4], hn4[NP / 4];
+    // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s: window sums sn0 / sn1
+    auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
+        sn0 = sn1 = make_double2(0.0, 0.0);
+        const int vs = mic_var(s, ma.niter);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            double2 sq = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int k = 0; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
+            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
+            else sn0 = c_add(sn0, sq);
+        }
+        sn0 = c_mul(scale, sn0);
+    };
     for (int s = 0; s <= ma.niter; ++s) {
+        // an opaque zero in the per-stage LDS indices: hoisted out of the stage
+        // loop, the operator / twiddle reads of both variants would stay live
+        // across it (k_pic_fft's lesson)
+        int oz = 0;
+        asm volatile("" : "+v"(oz));
+        const int ro = r + oz;
+        double2 sn0, sn1;
         double2 ye[6];
         if (s == 0) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) ye[a] = yv[a];
         } else {
             // the previous stage's estimated taps and their window sums
+            if (PIL)
+#pragma unroll
+                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = shp[(s - 1) & 1][4 * ks + (l >> 4)][l & 15];
             double2 taps[6][NT];
-            mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j, p); }, hb, sl,
-                             l, cq);
+            mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); }, hb,
+                             sl, l, cq);
             sp0 = sp1 = make_double2(0.0, 0.0);
 #pragma unroll
             for (int q = 0; q < NT; ++q) {
@@ -2194,62 +2231,44 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
-            mic_chain<NT, SH>(x, taps, tb.twa, tb.twb, r, sg1, sg2);
+            mic_chain<NT, SH>(x, taps, tb.twa, tb.twb, ro, sg1, sg2);
             // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 double2 hpv = sp0;
-                c_fma(hpv, wrow[4 * a + r], sp1);
+                c_fma(hpv, wrow[4 * a + ro], sp1);
                 ye[a] = c_sub(yv[a], x[p6(a)]);
                 c_fma(ye[a], hpv, v[a]);
             }
         }
         // this stage's LS pilot estimates (script:412-414 / :487-489)
-        double2 hn4[NP / 4];
         if (PIL) {
             double2* hx = shp[s & 1][0];
+            (void)hx;
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-                if (pc[a] >= 0 && pc[a] < NP) {
-                    const double2 q = c_div(ye[a], xpv[a]);
+                const int pc = rpc[4 * a + r];
+                if (pc >= 0) {
+                    const double2 q = c_div(ye[a], xpb[pc][ul]);
                     const double2 h = make_double2(q.x / sqk, q.y / sqk);
-                    hx[pc[a] * 17 + ul] = h;
-                    ma.hpa[((size_t)s * NP + pc[a]) * U + unit] = h;
+                    hx[pc * 17 + ul] = h;
+                    ma.hpa[((size_t)s * NP + pc) * U + unit] = h;
                 }
             }
             __syncthreads();
 #pragma unroll
             for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
-            if (s < ma.niter)
-#pragma unroll
-                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = hx[(4 * ks + (l >> 4)) * 17 + (l & 15)];
+            diag_sums(s, ro, sn0, sn1);
         } else {
-            const double2* __restrict__ hs = ma.hpa + (size_t)s * NP * U;
 #pragma unroll
-            for (int k = 0; k < NP / 4; ++k) hn4[k] = hs[(size_t)(r * (NP / 4) + k) * U + unit];
-            if (s < ma.niter)
-#pragma unroll
-                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = hs[(size_t)(4 * ks + (l >> 4)) * U + unit_mf];
+            for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
+            diag_sums(s, ro, sn0, sn1);
         }
-        // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s
-        double2 sn0 = make_double2(0.0, 0.0), sn1 = sn0;
-        const int vs = mic_var(s, ma.niter);
-#pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            double2 sq = make_double2(0.0, 0.0);
-#pragma unroll
-            for (int k = 0; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, r * (NP / 4) + k), hn4[k]);
-            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
-            if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
-            else sn0 = c_add(sn0, sq);
-        }
-        sn0 = c_mul(scale, sn0);
         double2 hd[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             hd[a] = sn0;
-            c_fma(hd[a], wrow[4 * a + r], sn1);
+            c_fma(hd[a], wrow[4 * a + ro], sn1);
         }
         int dp[6];
         mic_detect(dp, ye, hd, o, tb.sgrid);
@@ -2270,7 +2289,13 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 if (data) o.tr->dec_e[(size_t)s * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
             }
         }
-        cntl[s] = wave_sum(valid ? ncnt : 0);      // uniform: every lane writes the same word
+        cntl[s] = wave_sum_dpp(valid ? ncnt : 0);  // uniform: every lane writes the same word
+        if (!PIL && s < ma.niter) {
+            // stage s + 1's operands: hP_s (tap GEMM) and hP_{s+1} (diag)
+            const double2* __restrict__ hs = ma.hpa + (size_t)s * NP * U;
+#pragma unroll
+            for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = hs[(size_t)(4 * ks + (l >> 4)) * U + unit_mf];
+        }
         if (ma.mse_err) {
             double me = 0.0, mp = 0.0;
 #pragma unroll
@@ -2334,6 +2359,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __shared__ double2 bss[4][2][NT][NP];                   // Bs of each wave's symbol, both variants
     __shared__ double2 sl[4][16 * 17];                      // per-wave tap slab
     __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
+    __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
     __shared__ int cntl[4][PM_MAXIT + 1];
     const int tid = threadIdx.x, l = tid & 63, r = l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
@@ -2351,13 +2377,17 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
         const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
         bss[w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
     }
+    for (int i = tid; i < NP * 16; i += blockDim.x) {
+        const int u16 = ug16 * 16 + (i & 15);
+        xpb[i >> 4][i & 15] = o.xp[(size_t)(i >> 4) * R + u16 % R];
+    }
     __syncthreads();
     const double2* __restrict__ bvb = ma.bv + ((size_t)snr * NT * ma.N + klo) * NP;
     const size_t vstride = (size_t)ma.nsnr * NT * ma.N * NP;
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
     auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], sl[w], shp, cntl[w], A, Bs,
-                                         row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], sl[w], shp, xpb, cntl[w], A,
+                                         Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     // one atomic per (stage, edge) per block
     for (int i = tid; i < 2 * (ma.niter + 1); i += blockDim.x) {
@@ -2371,7 +2401,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
 
 // 64 units x one data symbol per block (4 waves x 16 units)
 template <int NT, int SH, int NP, bool TRACE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 3)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[24], wrow[24];
@@ -2416,8 +2446,8 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __syncthreads();
     auto A = [&](int var, int q, int j, int p) { return sbv[var][q][j][p]; };
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, sl[w], nullptr, cntl[w], A, Bs, row0,
-                                          unit, unit_mf, ul, l, r, U, R, rl, snr);
+    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, sl[w], nullptr, nullptr, cntl[w], A, Bs,
+                                          row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
         const int s = i >> 1, edge = i & 1;
@@ -2777,7 +2807,7 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
 }
 
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd) {
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     Mic2Args ma{};
     ma.bv = mm.Bv;
@@ -2794,7 +2824,7 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     // pilot symbols: one wave each, 16 units per block
     ma.blks = mm.pblk;
     ma.nb = mm.npb;
-    {
+    if (part & 1) {
         const dim3 grid(b.U / 16), blk(64 * mm.npb);
 #define LAUNCH_MP(NTV, SHV)                                                                                  \
     do {                                                                                                     \
@@ -2808,7 +2838,7 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     }
     ma.blks = mm.dblk;
     ma.nb = mm.ndb;
-    {
+    if (part & 2) {
         const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
         const dim3 grid((b.U / WAVE) * mm.ndb), blk(256);
 #define LAUNCH_MD(NTV, SHV)                                                                                  \
