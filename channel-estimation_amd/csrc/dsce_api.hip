@@ -1982,7 +1982,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

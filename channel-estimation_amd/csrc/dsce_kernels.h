@@ -32,6 +32,7 @@ struct Opts {
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
     int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
+    int jakes_mom = 1;        // Jakes taps of the read windows by phase moments (k_jakes_mom) where exact enough
     int mic2 = 1;             // FFT-form OFDM: every MMSE stage in one launch pair (k_mic_pilot + k_mic_data)
                               // and perfect-CSI stage 0 inside k_pic_fft; 0: per-stage k_stage0_fft / k_mic_fft
 };

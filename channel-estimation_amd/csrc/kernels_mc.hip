@@ -142,6 +142,21 @@ __device__ __forceinline__ int slice_fast(const SlicerLds& t, int nI, int nQ, do
     return min(min(b0, b1), min(b2, b3));
 }
 
+// 1 / x by v_rcp_f64 and two Newton steps (5 instructions; the IEEE division is
+// ~10 with its scale / fixup for denormals and overflow, which these operands —
+// |h|^2 of a channel estimate — never reach); error ~1 ulp
+__device__ __forceinline__ double recip_fast(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+// a / b with one fast reciprocal
+__device__ __forceinline__ double2 c_div_fast(double2 a, double2 b) {
+    const double id = recip_fast(b.x * b.x + b.y * b.y);
+    return make_double2((a.x * b.x + a.y * b.y) * id, (a.y * b.x - a.x * b.y) * id);
+}
 // a / b with one division (rounding-level differences to c_div)
 __device__ __forceinline__ double2 c_div1(double2 a, double2 b) {
     const double id = 1.0 / (b.x * b.x + b.y * b.y);
@@ -214,6 +229,13 @@ __device__ __forceinline__ double2 c_mul_fma(double2 z, double2 w) {
 }
 
 static constexpr int JCH_MAX = 16;
+
+// a double from the neighbouring lane of the pair (DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ double dpp_d_xor1(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0xb1, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(lo, 0xb1, 0xf, 0xf, false));
+}
 // RPW realisations per wave (LPR = 64 / RPW lanes each): with N = 540 two
 // realisations of 32 chunks of 17 samples keep every lane busy with twice the
 // chunk length of one realisation per wave (the per-chunk cis is amortised over
@@ -352,6 +374,108 @@ static void launch_jakes_t(hipStream_t s, const ChannelK& ch, uint64_t seed, uin
                        seed, rep0, R, ir, chunk_n0, nchunk);
 }
 
+// The same sum of sinusoids over a 24-sample chunk by phase moments (r03):
+// with theta_p = 2 pi fD_p dt (radians per sample), the chunk centre c and
+// z_p = exp(j 2 pi (phi_p + fD_p c dt)),
+//   sum_p exp(j 2 pi (phi_p + fD_p (c + k) dt)) = sum_p z_p exp(j theta_p k)
+//     = sum_m M_m (j k)^m / m!,   M_m = sum_p z_p theta_p^m,   |k| <= 11.5,
+// exact up to the Taylor remainder sum_p |theta_p k|^(MT+1) / (MT+1)!: the
+// launcher uses it only while |theta| 11.5 <= 0.3 (C2: 0.233; remainder
+// < 1e-14 at 200 paths, far inside the 1e-12 parity tolerance of the IR).  Per
+// path and chunk one cis and MT (multiply + 2 FMAs) instead of the recurrence's
+// 24 x (2 FMAs + accumulation); the moments of the lane pair's two path halves
+// are summed by one exchange, then each lane evaluates its 12 samples by Horner
+// (2 FMAs per term).  ~1.8x fewer instructions than k_jakes on the same chunks.
+template <int RPW, int MT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_jakes_mom(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restrict__ ir, const int* __restrict__ chunk_n0,
+            int nchunk) {
+    constexpr int JCH = 24, H = JCH / 2, PS = 2;
+    extern __shared__ double sm[];
+    constexpr int LPR = WAVE / RPW;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = RPW == 1 ? 0 : lane / LPR, sl = RPW == 1 ? lane : lane % LPR;
+    const int P = ch.paths;
+    double* ds = sm + (size_t)(wv * RPW + sub) * 3 * P;
+    double* ph = ds + P;
+    double* th = ph + P;
+    const int tap = blockIdx.z;
+    const int rl = (blockIdx.y * 4 + wv) * RPW + sub;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    for (int p = sl; p < P; p += LPR) {
+        const uint32_t e = (uint32_t)(tap + ch.ntap * p);       // rand([Ntap 1 Paths]) column-major
+        const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, e >> 1);
+        const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, e >> 1);
+        const double t = (e & 1) ? u53(wt.z, wt.w) : u53(wt.x, wt.y);
+        const double phi = (e & 1) ? u53(wp.z, wp.w) : u53(wp.x, wp.y);
+        const double d = (ch.model == 0) ? cos((t * 2.0) * M_PI) * ch.fD : (2.0 * (t - 0.5)) * ch.fD;
+        ds[p] = d;
+        ph[p] = phi;
+        th[p] = TWO_PI * (d * ch.dt);
+    }
+    __syncthreads();
+    const int ck = blockIdx.x * (LPR / PS) + sl / PS, par = sl % PS;
+    if (ck >= nchunk) return;
+    const int n0 = chunk_n0[ck];
+    if (n0 >= ch.N) return;
+    const double tc = ((double)n0 + 0.5 * (JCH - 1)) * ch.dt;
+    double2 M[MT + 1];
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) M[m] = make_double2(0.0, 0.0);
+    const int pend = (par + 1) * P / PS;
+    int p = par * P / PS;
+    for (; p + 1 < pend; p += 2) {
+        const double2 z0 = cis_turns(ph[p] + ds[p] * tc), z1 = cis_turns(ph[p + 1] + ds[p + 1] * tc);
+        const double t0 = th[p], t1 = th[p + 1];
+        M[0].x += z0.x + z1.x;
+        M[0].y += z0.y + z1.y;
+        double w0 = 1.0, w1 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            w1 *= t1;
+            M[m].x = fma(z1.x, w1, fma(z0.x, w0, M[m].x));
+            M[m].y = fma(z1.y, w1, fma(z0.y, w0, M[m].y));
+        }
+    }
+    if (p < pend) {
+        const double2 z0 = cis_turns(ph[p] + ds[p] * tc);
+        const double t0 = th[p];
+        M[0].x += z0.x;
+        M[0].y += z0.y;
+        double w0 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            M[m].x = fma(z0.x, w0, M[m].x);
+            M[m].y = fma(z0.y, w0, M[m].y);
+        }
+    }
+    // the lane pair's moments summed (a + b == b + a: both lanes hold the same total)
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) {
+        M[m].x += dpp_d_xor1(M[m].x);
+        M[m].y += dpp_d_xor1(M[m].y);
+    }
+    const double gs = ch.sqrt_pdp[tap] / sqrt((double)P);
+#pragma unroll
+    for (int k = 0; k < H; ++k) {
+        // sample n0 + kk, offset kk - 11.5 from the centre: Horner in (j kp)
+        const int kk = k + H * par;
+        const double kp = (double)kk - 0.5 * (JCH - 1);
+        double2 acc = M[MT];
+#pragma unroll
+        for (int m = MT - 1; m >= 0; --m) {
+            const double sc = kp / (double)(m + 1);
+            const double ax = acc.x;
+            acc.x = fma(-sc, acc.y, M[m].x);
+            acc.y = fma(sc, ax, M[m].y);
+        }
+        const int n = n0 + kk;
+        if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(gs * acc.x, gs * acc.y);
+    }
+}
+
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
 // u2 = u53(w2,w3), (re, im) = sqrt(-2 log(1-u1)) (cos, sin)(2 pi u2).
 __device__ __forceinline__ double2 normal_pair(uint4 w) {
@@ -443,6 +567,15 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
     // splitting the paths (12-sample chunks, one lane each: 2.37 ms per
     // 65536 realisations at C2, the per-chunk cis ~45 % of the instructions)
     if (jc && jc->n0 && op.jakes_win && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024) {
+        // the phase-moment form where its Taylor remainder is negligible
+        // (|theta| (LEN - 1) / 2 <= 0.3), else the recurrence
+        if (op.jakes_mom && JakesChunks::LEN == 24 && TWO_PI * fabs(ch.fD) * ch.dt * 11.5 <= 0.3) {
+            constexpr int RPW = 2, CPW = WAVE / RPW / 2;
+            dim3 grid((jc->n + CPW - 1) / CPW, R / (4 * RPW), ch.ntap);
+            hipLaunchKernelGGL((k_jakes_mom<RPW, 12>), grid, dim3(256), (size_t)4 * RPW * 3 * ch.paths * sizeof(double),
+                               s, ch, seed, rep0, R, ir, jc->n0, jc->n);
+            return;
+        }
         launch_jakes_t<JakesChunks::LEN, 2, 2>(s, ch, seed, rep0, R, ir, jc->n0, jc->n);
         return;
     }
@@ -2121,7 +2254,7 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
     int anytie = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-        const double2 z = c_div1(ye[a], hd[a]);
+        const double2 z = c_div_fast(ye[a], hd[a]);
         int tI, tQ;
         const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
         const int iQ = nearest_lin(z.y, o.scQ, o.ofQ, o.topQ, tQ);
@@ -2175,7 +2308,11 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0;       // window sums of the previous stage's taps
+    // window sums of the previous stage's estimated taps: diag(D_hat_{s-1}) of the
+    // y_ic correction.  They equal Bs hP_{s-1} (Bs = Bv summed over the window),
+    // i.e. the previous stage's own diag sums sn, which are kept instead of
+    // summing the 12 taps again
+    double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0;
     // B operand of the tap GEMM (hP_{s-1}) and this stage's LS pilots (a quarter
     // per lane, for diag(D_hat_s)); the data kernel prefetches both for stage
     // s + 1 at the end of stage s and folds hn4 into the window sums sn at once
@@ -2216,18 +2353,6 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             double2 taps[6][NT];
             mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); }, hb,
                              sl, l, cq);
-            sp0 = sp1 = make_double2(0.0, 0.0);
-#pragma unroll
-            for (int q = 0; q < NT; ++q) {
-                double2 sq = make_double2(0.0, 0.0);
-#pragma unroll
-                for (int m = 0; m < 6; ++m) sq = c_add(sq, taps[m][q]);
-                sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-                sq = c_add(sq, dpp_c<QP_XOR2>(sq));
-                if ((SH >> q) & 1) sp1 = c_add(sp1, sq);
-                else sp0 = c_add(sp0, sq);
-            }
-            sp0 = c_mul(scale, sp0);
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
@@ -2270,6 +2395,8 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             hd[a] = sn0;
             c_fma(hd[a], wrow[4 * a + ro], sn1);
         }
+        sp0 = sn0;
+        sp1 = sn1;
         int dp[6];
         mic_detect(dp, ye, hd, o, tb.sgrid);
         int ncnt = 0;
