@@ -2172,7 +2172,7 @@ __device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A,
 #pragma unroll
     for (int t = 0; t < NTILE; ++t) {
         const int idx = 4 * t + ka;
-        const bool ok = idx < NIDX;
+        const bool ok = (NIDX % 4 == 0) || idx < NIDX;        // compile-time true when the tiles are full
         const int q = idx >= 6 ? 1 : 0, m = idx - 6 * q;
         d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
 #pragma unroll
@@ -2287,7 +2287,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     const int cq = (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    const double sqk = 1.0 / sk.inv_sqrt_kappa;
+    const double isqk = sk.inv_sqrt_kappa;
     const bool valid = rl < o.rvalid;
     // per-unit operands, read once: y, transmitted indices, the rows' constant
     // part of v (precoded pilots / zero rows); PIL: the transmitted pilots come
@@ -2321,15 +2321,21 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
         sn0 = sn1 = make_double2(0.0, 0.0);
         const int vs = mic_var(s, ma.niter);
+        bool f0 = true, f1 = true;                          // compile-time: first tap of each sum assigns
 #pragma unroll
         for (int q = 0; q < NT; ++q) {
-            double2 sq = make_double2(0.0, 0.0);
+            double2 sq = c_mul(Bs(vs, q, ro * (NP / 4)), hn4[0]);
 #pragma unroll
-            for (int k = 0; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
+            for (int k = 1; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
             sq = c_add(sq, dpp_c<QP_XOR1>(sq));
             sq = c_add(sq, dpp_c<QP_XOR2>(sq));
-            if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
-            else sn0 = c_add(sn0, sq);
+            if ((SH >> q) & 1) {
+                sn1 = f1 ? sq : c_add(sn1, sq);
+                f1 = false;
+            } else {
+                sn0 = f0 ? sq : c_add(sn0, sq);
+                f0 = false;
+            }
         }
         sn0 = c_mul(scale, sn0);
     };
@@ -2341,6 +2347,9 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         asm volatile("" : "+v"(oz));
         const int ro = r + oz;
         double2 sn0, sn1;
+        if (!PIL)
+#pragma unroll
+            for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
         double2 ye[6];
         if (s == 0) {
 #pragma unroll
@@ -2374,8 +2383,8 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             for (int a = 0; a < 6; ++a) {
                 const int pc = rpc[4 * a + r];
                 if (pc >= 0) {
-                    const double2 q = c_div(ye[a], xpb[pc][ul]);
-                    const double2 h = make_double2(q.x / sqk, q.y / sqk);
+                    const double2 q = c_div_fast(ye[a], xpb[pc][ul]);
+                    const double2 h = make_double2(q.x * isqk, q.y * isqk);
                     hx[pc * 17 + ul] = h;
                     ma.hpa[((size_t)s * NP + pc) * U + unit] = h;
                 }
@@ -2385,8 +2394,6 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
             diag_sums(s, ro, sn0, sn1);
         } else {
-#pragma unroll
-            for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
             diag_sums(s, ro, sn0, sn1);
         }
         double2 hd[6];
