@@ -101,7 +101,9 @@ def cpu_baseline_leg(seconds, workload, index=0):
             if el >= seconds / 3 and n >= 1:
                 break
         rates.append(n / el)
-    print(json.dumps({"rates": rates, "reps": n_total}))
+    import resource
+    print(json.dumps({"rates": rates, "reps": n_total,
+                      "maxrss_bytes": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024}))
 
 
 def host_info():
@@ -129,6 +131,29 @@ def _leg_env(threads=1):
     return env
 
 
+def progress(msg):
+    """A heartbeat on stderr (the GPU runner kills a command silent for 3 minutes)."""
+    print("[bench %.0fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+HOST_MEM_BUDGET = 160e9          # bytes the CPU-baseline pool may hold at once
+
+
+def _wait_all(procs, timeout):
+    t0 = last = time.perf_counter()
+    while any(p.poll() is None for p in procs):
+        if time.perf_counter() - t0 > timeout:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(1.0)
+        if time.perf_counter() - last >= 30.0:
+            last = time.perf_counter()
+            progress("cpu baseline: %d of %d processes running" % (sum(p.poll() is None for p in procs), len(procs)))
+
+
 def run_cpu_baseline(seconds, workload):
     """Two legs of the oracle on the host, each about seconds / 2: one process
     with single-threaded BLAS, and a pool of P such processes running at once
@@ -142,15 +167,23 @@ def run_cpu_baseline(seconds, workload):
     pool = max(1, min(pool, host.get("affinity") or pool))
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds", str(seconds / 2),
            "--config", workload]
-    one = subprocess.run(cmd, env=_leg_env(), capture_output=True, text=True, timeout=900)
+    progress("cpu baseline: one process")
+    one = subprocess.Popen(cmd, env=_leg_env(), stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+    _wait_all([one], 900)
+    out1, _ = one.communicate()
     if one.returncode != 0:
         return None
-    leg1 = json.loads(one.stdout.strip().splitlines()[-1])
+    leg1 = json.loads(out1.strip().splitlines()[-1])
+    # the pool within the host memory one command may use (the GPU box caps it at
+    # ~270 GB; C5's oracle setup holds the dense W of three schemes per process)
+    pool = max(1, min(pool, int(HOST_MEM_BUDGET / max(leg1.get("maxrss_bytes", 1), 1))))
+    progress("cpu baseline: %d processes" % pool)
     procs = [subprocess.Popen(cmd + ["--leg-index", str(i + 1)], env=_leg_env(), stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL, text=True) for i in range(pool)]
+    _wait_all(procs, 900)
     legs = []
     for pr in procs:
-        out, _ = pr.communicate(timeout=900)
+        out, _ = pr.communicate()
         if pr.returncode != 0:
             return None
         legs.append(json.loads(out.strip().splitlines()[-1]))
@@ -305,6 +338,8 @@ def main():
     t_setup = time.perf_counter()
     eng = build_engine(S, device=device, batch=batch, options=options)
     setup_s = time.perf_counter() - t_setup
+    if rank == 0:
+        progress("setup done (%.1f s)" % setup_s)
     counts = np.zeros(eng.counter_shape(), dtype=np.int64)
     base = rank * (args.steps + args.warmup) * B
     for w in range(args.warmup):
@@ -322,6 +357,8 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
     el = time.perf_counter() - t0
+    if rank == 0:
+        progress("%d timed steps: %.3f s" % (args.steps, el))
     if dist:
         import torch
         dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else "cpu"
@@ -337,23 +374,27 @@ def main():
     # roofline of the dominant kernel (the MMSE IC: k_mic_fft where the scheme is
     # FFT-form OFDM, else the W contraction k_wcontract; HIP events on the
     # engine's stream)
-    md_l, _ = eng.kernel_time("k_mic_data")
-    mic_l, mic_ms = eng.kernel_time("k_mic_fft")
-    kname = "k_mic_data" if md_l else "k_mic_fft" if mic_l else "k_wcontract"
-    mic_l = mic_l or md_l
+    # each scheme's MMSE kernel: k_mic_data (every stage in one launch pair), k_mic_fft
+    # (per-iteration FFT form) or the W contraction; the dominant one by measured time
+    # carries the roofline, with the work model of the schemes it runs
+    def mmse_kernel(p):
+        return "k_mic_data" if "mic_stages" in p else "k_mic_fft" if "mic_fft" in p else "k_wcontract"
+    paths = [eng.path_info(sid) for sid in range(len(schemes))]
+    kname = max({mmse_kernel(p) for p in paths}, key=lambda k: eng.kernel_time(k)[1])
+    mic_l = kname != "k_wcontract"
     launches, wc_ms = eng.kernel_time(kname)
     flops = 0.0
     executed = 0.0
-    paths = []
-    for sid in range(len(schemes)):
+    for sid, p in enumerate(paths):
+        if mmse_kernel(p) != kname:
+            continue
         cmac_per_rep, _ = eng.work_model(sid)
         f = cmac_per_rep * 8.0 * B * args.steps
-        p = eng.path_info(sid)
-        paths.append(sorted(p))
         flops += f
         # matrix-core flops actually executed per counted flop: 3 real MFMAs per
         # complex product in the 3M form, 4 in the 4M form
-        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and "mic_fft" not in p else 1.0)
+        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and not mic_l else 1.0)
+    paths = [sorted(p) for p in paths]
     achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     peak_meas = eng.fp64_mfma_peak()

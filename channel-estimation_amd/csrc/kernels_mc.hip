@@ -458,6 +458,18 @@ k_jakes_mom(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restric
         M[m].y += dpp_d_xor1(M[m].y);
     }
     const double gs = ch.sqrt_pdp[tap] / sqrt((double)P);
+    // M_m / m! (compile-time reciprocals): Horner then takes two FMAs per term
+    // (a kp / (m + 1) per term compiles to an IEEE division sequence: 1.27 ->
+    // 1.15 ms per 65536 realisations at C2)
+    {
+        double f = 1.0;
+#pragma unroll
+        for (int m = 2; m <= MT; ++m) {
+            f /= (double)m;                                     // constant-folded
+            M[m].x *= f;
+            M[m].y *= f;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < H; ++k) {
         // sample n0 + kk, offset kk - 11.5 from the centre: Horner in (j kp)
@@ -466,10 +478,9 @@ k_jakes_mom(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restric
         double2 acc = M[MT];
 #pragma unroll
         for (int m = MT - 1; m >= 0; --m) {
-            const double sc = kp / (double)(m + 1);
             const double ax = acc.x;
-            acc.x = fma(-sc, acc.y, M[m].x);
-            acc.y = fma(sc, ax, M[m].y);
+            acc.x = fma(-kp, acc.y, M[m].x);
+            acc.y = fma(kp, ax, M[m].y);
         }
         const int n = n0 + kk;
         if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(gs * acc.x, gs * acc.y);

@@ -18,4 +18,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAF
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_fetch" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_fetch.log 2>&1 || { echo fetch_fail; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_write" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_write.log 2>&1 || { echo write_fail; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_sq" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_sq.log 2>&1 || { echo sq_fail; exit 1; }
+python3 tools/pmc_table.py $out/prof_fetch $out/prof_write $out/prof_sq > $out/table.txt || { echo table_fail; exit 1; }
 echo all_ok
