@@ -1224,6 +1224,15 @@ __device__ __forceinline__ double2 c_mulf(double2 a, double2 b) {
     return make_double2(fma(a.x, b.x, -(a.y * b.y)), fma(a.x, b.y, a.y * b.x));
 }
 
+// e * w of the quad network's middle twiddle: 1 on lanes 0-2, +i (S = 1, forward)
+// or -i (S = -1, inverse) on lane 3 -- as selects (five 32-bit ops) instead of a
+// complex product (four f64 ops)
+template <int S>
+__device__ __forceinline__ double2 quad_tw(double2 e, bool r3) {
+    const double nx = S > 0 ? -e.y : e.y, ny = S > 0 ? e.x : -e.x;
+    return make_double2(r3 ? nx : e.x, r3 ? ny : e.y);
+}
+
 // DPP move of a double / complex within each quad of lanes (quad_perm control)
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
@@ -1288,7 +1297,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     __shared__ double2 rpv[24];
     __shared__ int rdc[24];
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
-    __shared__ double2 twb[2][4];                               // quad-network twiddle of lane r
     __shared__ int cntl[4][PM_MAXIT + 1];                      // [wave][stage]
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
     // and the channel taps of the lane's samples (registers for all iterations)
@@ -1336,10 +1344,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             const int tc = min(tid, 47), dir = tc / 24;
             const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
             twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        }
-        if (tid >= 48 && tid < 56) {
-            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
-            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
         }
     }
     __syncthreads();
@@ -1417,7 +1421,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             const double2 p = c_mulf(x[p6(m)], twa[0][ro][m]);
             const double2 pv = dpp_c<QP_XOR2>(p);
             double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-            e = c_mulf(e, twb[0][ro]);
+            e = quad_tw<1>(e, r == 3);
             const double2 qv = dpp_c<QP_XOR1>(e);
             t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
         }
@@ -1439,7 +1443,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         for (int m = 0; m < 6; ++m) {
             const double2 pv = dpp_c<QP_XOR1>(t[m]);
             double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-            f = c_mulf(f, twb[1][ro]);
+            f = quad_tw<-1>(f, r == 3);
             const double2 qv = dpp_c<QP_XOR2>(f);
             x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][ro][m]);
         }
@@ -1602,7 +1606,6 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
     __shared__ int rdc[24];
     __shared__ double2 wrow[24];                                // qs gs w^(-l): diag(D_hat) weight of a delayed tap
     __shared__ double2 twa[2][4][6];
-    __shared__ double2 twb[2][4];
     // per-unit operands (the rows' v and y, the previous stage's pilots, all NP,
     // shared by the quad, and a quarter of this stage's: lane r holds pilots
     // 4r..4r+3 of the window sums), requested after the table / operator loads
@@ -1692,10 +1695,6 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
             const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
             wrow[lr0] = c_mul(scale, make_double2(wl.x, -wl.y));
-        }
-        if (tid >= 48 && tid < 56) {
-            const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
-            twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
         }
     }
     __syncthreads();
@@ -1810,7 +1809,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
             const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
             const double2 pv = dpp_c<QP_XOR2>(p);
             double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-            e = c_mulf(e, twb[0][r]);
+            e = quad_tw<1>(e, r == 3);
             const double2 qv = dpp_c<QP_XOR1>(e);
             t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
         }
@@ -1827,7 +1826,7 @@ k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
         for (int m = 0; m < 6; ++m) {
             const double2 pv = dpp_c<QP_XOR1>(t[m]);
             double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-            f = c_mulf(f, twb[1][r]);
+            f = quad_tw<-1>(f, r == 3);
             const double2 qv = dpp_c<QP_XOR2>(f);
             xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
         }
@@ -2213,10 +2212,10 @@ __device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A,
 }
 
 // x <- qs gs DFT24(sum_q taps_q .* IDFT24(x)(. - d_q)) of one symbol (k_pic_fft's
-// chain; twa / twb: the lane twiddles staged in LDS, output scale folded in twa[1])
+// chain; twa: the lane twiddles staged in LDS, output scale folded in twa[1])
 template <int NT, int SH>
 __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[6][NT], const double2 (*twa)[4][6],
-                                          const double2 (*twb)[4], int r, double sg1, double sg2) {
+                                          int r, double sg1, double sg2) {
     dft6<1>(xx);
     double2 t[6];
 #pragma unroll
@@ -2224,7 +2223,7 @@ __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[
         const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
         const double2 pv = dpp_c<QP_XOR2>(p);
         double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-        e = c_mulf(e, twb[0][r]);
+        e = quad_tw<1>(e, r == 3);
         const double2 qv = dpp_c<QP_XOR1>(e);
         t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
     }
@@ -2241,7 +2240,7 @@ __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[
     for (int m = 0; m < 6; ++m) {
         const double2 pv = dpp_c<QP_XOR1>(t[m]);
         double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-        f = c_mulf(f, twb[1][r]);
+        f = quad_tw<-1>(f, r == 3);
         const double2 qv = dpp_c<QP_XOR2>(f);
         xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
     }
@@ -2254,7 +2253,6 @@ struct Mic2Tables {
     double2 sym[256];
     int sgrid[256];
     double2 twa[2][4][6];
-    double2 twb[2][4];
 };
 
 // One-tap + detection of the lane's six rows with diag(D_hat) = hd[a]; returns
@@ -2376,7 +2374,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
-            mic_chain<NT, SH>(x, taps, tb.twa, tb.twb, ro, sg1, sg2);
+            mic_chain<NT, SH>(x, taps, tb.twa, ro, sg1, sg2);
             // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
@@ -2470,10 +2468,6 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
         const int dir = tid / 24;
         const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
         tb.twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-    }
-    if (tid >= 48 && tid < 56) {
-        const int dir = (tid - 48) / 4, rr = (tid - 48) % 4;
-        tb.twb[dir][rr] = rr == 3 ? make_double2(0.0, dir ? -1.0 : 1.0) : make_double2(1.0, 0.0);
     }
 }
 
@@ -2640,7 +2634,6 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     const int cq = (r >> 1) + 2 * (r & 1);
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
     __shared__ double2 twa[2][4][6];
-    __shared__ double2 twb[2][4];
     __shared__ double2 wrow[24];
     __shared__ double ssc[TXRX_MAXSNR];                        // sqrt(Pn / 2) of the chunk's SNR points
     const double2 gs = sk.pf_gs, qs = sk.pf_qs, ps = sk.pf_scale;
@@ -2665,10 +2658,6 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         const int dir = tc / 24;
         const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
         twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
-        if (tid >= 48 && tid < 56) {
-            const int dr = (tid - 48) / 4, rr = (tid - 48) % 4;
-            twb[dr][rr] = rr == 3 ? make_double2(0.0, dr ? -1.0 : 1.0) : make_double2(1.0, 0.0);
-        }
         const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
         wrow[lr0] = c_mul(ps, make_double2(wl.x, -wl.y));
         ssc[kc] = sqrt(pnv / 2.0);
@@ -2704,7 +2693,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
         const double2 pv = dpp_c<QP_XOR2>(p);
         double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-        e = c_mulf(e, twb[0][r]);
+        e = quad_tw<1>(e, r == 3);
         const double2 qv = dpp_c<QP_XOR1>(e);
         t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
     }
@@ -2735,7 +2724,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
             const double2 rv = make_double2(r0[m].x + sc * z.x, r0[m].y + sc * z.y);
             const double2 pv = dpp_c<QP_XOR1>(rv);
             double2 g = make_double2(fma(sg2, rv.x, pv.x), fma(sg2, rv.y, pv.y));
-            g = c_mulf(g, twb[1][r]);
+            g = quad_tw<-1>(g, r == 3);
             const double2 qv = dpp_c<QP_XOR2>(g);
             f[m] = c_mulf(make_double2(fma(sg1, g.x, qv.x), fma(sg1, g.y, qv.y)), twa[1][r][m]);
         }
