@@ -2144,11 +2144,11 @@ __global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, M
 // the niter k_mic_fft launches: y, the transmitted indices and the row tables
 // are read once per symbol instead of once per stage, decisions never leave
 // the registers, Bv / Bs of both variants are staged once.
-// The tap GEMM's A rows are ordered quarter-major: tile t row 4c + k is tap
-// index 4t + k (q = idx / 6, window sample 6c + idx % 6) of time quarter c,
-// so after the GEMM the lane quad of a unit reads its quarter's 4 taps of the
-// tile from a 16-row per-wave slab (4.4 KB, reused per tile) instead of the
-// 13 KB slab of all tiles (k_mic_fft): 17 instead of 52 KB of LDS per block.
+// The tap GEMM's A rows interleave the time quarters: tile t row c + 4k is tap
+// index 4t + k (q = idx / 6, window sample 6c + idx % 6) of quarter c, so the
+// lane quad of a unit pulls its quarter's 4 taps of the tile from one lane with
+// ds_bpermute (mic_taps): no LDS slab (k_mic_fft: 52 KB per block; r03's first
+// version: a 17 KB per-wave slab with a fence pair per tile).
 // ---------------------------------------------------------------------------
 struct Mic2Args {
     const double2* __restrict__ bv;   // [var][snr][NT][N][NP]
@@ -2163,15 +2163,29 @@ struct Mic2Args {
 
 __device__ __forceinline__ int mic_var(int s, int niter) { return (s == 0 || 2 * s <= niter) ? 0 : 1; }
 
+// a complex from lane addr / 4 of the wave (ds_bpermute: the LDS crossbar, no LDS
+// allocation, no barrier)
+__device__ __forceinline__ double2 bperm_c(int addr, double2 v) {
+    return make_double2(__hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.x)),
+                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.x))),
+                        __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.y)),
+                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.y))));
+}
+
 // Estimated taps of the lane's six window samples (quad layout: lane r of a unit
 // holds samples 6 cq + m) for the 16 units of a wave: MFMA GEMM (3M) with
 // A(q, j, p) = Bv[q][klo + j][p] and B = hP (lane (g, jc): pilots 4 ks + g of
-// unit jc), D tiles through the wave's 16-row slab `sl` (17-unit stride).
+// unit jc).  Tile t's A row i is tap index 4 t + (i >> 2) of time quarter i & 3,
+// so D register k of lane (g, jc) holds tap index 4 t + k of quarter g, unit jc:
+// the lane (unit ul, quarter cq) pulls its four taps of the tile from lane
+// 16 cq + ul with one ds_bpermute per dword, the same register in every lane
+// (r02-r03's per-wave LDS slab needed 17 KB per block and a fence pair per tile).
 template <int NT, int NP, class ALoad>
-__device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A, const double2 (&hb)[NP / 4],
-                                         double2* sl, int l, int cq) {
+__device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A, const double2 (&hb)[NP / 4], int l,
+                                         int cq) {
     constexpr int NIDX = 6 * NT, NTILE = (NIDX + 3) / 4, NKS = NP / 4;
-    const int g = l >> 4, jc = l & 15, ca = jc >> 2, ka = jc & 3, ul = l >> 2;
+    const int g = l >> 4, jc = l & 15, ca = jc & 3, ka = jc >> 2, ul = l >> 2;
+    const int src = (16 * cq + ul) * 4;
     double br[NKS], bi[NKS], bsm[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -2193,21 +2207,12 @@ __device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A,
             p2 = MFMA64(ai, bi[ks], p2);
             p3 = MFMA64(ar + ai, bsm[ks], p3);
         }
-        // D row g + 4 reg = tap index 4t + g of quarter reg, unit jc
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg)
-            sl[(g + 4 * reg) * 17 + jc] = make_double2(p1[reg] - p2[reg], p3[reg] - p1[reg] - p2[reg]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int id2 = 4 * t + k;                     // compile-time
-            if (id2 < NIDX) taps[id2 % 6][id2 / 6] = sl[(4 * cq + k) * 17 + ul];
+            if (id2 < NIDX)
+                taps[id2 % 6][id2 / 6] = bperm_c(src, make_double2(p1[k] - p2[k], p3[k] - p1[k] - p2[k]));
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -2289,7 +2294,7 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
 template <int NT, int SH, int NP, bool TRACE, bool PIL, class ALoad, class BsLoad>
 __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
                                             const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
-                                            const double2* wrow, double2* sl, double2 (*shp)[NP][17],
+                                            const double2* wrow, double2 (*shp)[NP][17],
                                             const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
                                             int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
                                             int snr) {
@@ -2370,7 +2375,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = shp[(s - 1) & 1][4 * ks + (l >> 4)][l & 15];
             double2 taps[6][NT];
             mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); }, hb,
-                             sl, l, cq);
+                             l, cq);
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
@@ -2496,7 +2501,6 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __shared__ double2 rpv[4][24], wrow[4][24];
     __shared__ int rdc[4][24], rpc[4][24];
     __shared__ double2 bss[4][2][NT][NP];                   // Bs of each wave's symbol, both variants
-    __shared__ double2 sl[4][16 * 17];                      // per-wave tap slab
     __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
     __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
     __shared__ int cntl[4][PM_MAXIT + 1];
@@ -2525,7 +2529,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     const size_t vstride = (size_t)ma.nsnr * NT * ma.N * NP;
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
     auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], sl[w], shp, xpb, cntl[w], A,
+    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
                                          Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     // one atomic per (stage, edge) per block
@@ -2548,7 +2552,6 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     constexpr int BVS = NP + 1;
     __shared__ double2 sbv[2][NT][24][BVS];                 // Bv of the symbol's window, both variants
     __shared__ double2 bss[2][NT][NP];
-    __shared__ double2 sl[4][16 * 17];
     __shared__ int cntl[4][PM_MAXIT + 1];
     int ug, bi;
     band_block(ord, ma.nb, ug, bi);
@@ -2585,7 +2588,7 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __syncthreads();
     auto A = [&](int var, int q, int j, int p) { return sbv[var][q][j][p]; };
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, sl[w], nullptr, nullptr, cntl[w], A, Bs,
+    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
                                           row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
