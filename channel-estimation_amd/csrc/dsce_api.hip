@@ -1012,6 +1012,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
 // least 10 % of the samples (FBMC's overlapping Q^H blocks cover them all).
 void update_jakes_chunks(dsce_ctx* c) {
     if (c->jk.n0) free_alloc(c, const_cast<int*>(c->jk.n0));
+    if (c->jk.grp) free_alloc(c, const_cast<int2*>(c->jk.grp));
     c->jk = JakesChunks{};
     c->jk_nsch = c->schemes.size();
     const int N = c->ch.N;
@@ -1036,6 +1037,50 @@ void update_jakes_chunks(dsce_ctx* c) {
     if (n0.empty() || covered > 0.9 * N) return;
     c->jk.n0 = dupload(c, n0);
     c->jk.n = (int)n0.size();
+    c->jk.n0h = n0;
+}
+
+// k_jakes_grp's anchor groups for the channel's theta = 2 pi |fD| dt (radians per
+// sample): runs of consecutive chunks with theta (span - 1) / 2 <= JAKES_XMAX, MT
+// the fewest Taylor terms (16 / 24 / 28 / 32) whose remainder x^(MT+1) / (MT+1)!
+// is below 1e-17 at the widest run, LG lanes per anchor by the group count.
+// Used only when it at least halves the anchors of k_jakes_mom (one per chunk).
+void update_jakes_groups(dsce_ctx* c) {
+    JakesChunks& jk = c->jk;
+    const double th = 6.283185307179586 * std::fabs(c->ch.fD) * c->ch.dt;
+    if (jk.theta == th && jk.nsch_grp == jk.n) return;
+    if (jk.grp) free_alloc(c, const_cast<int2*>(jk.grp));
+    jk.grp = nullptr;
+    jk.ngrp = jk.lg = jk.mt = 0;
+    jk.theta = th;
+    jk.nsch_grp = jk.n;
+    const int L = JakesChunks::LEN;
+    const std::vector<int>& n0 = jk.n0h;
+    if (n0.empty() || !(th > 0.0) || th * 0.5 * (L - 1) > JAKES_XMAX) return;
+    std::vector<int2> g;
+    double xmax = 0.0;
+    for (size_t i = 0; i < n0.size();) {
+        size_t j = i + 1;
+        while (j < n0.size() && th * 0.5 * (n0[j] + L - 1 - n0[i]) <= JAKES_XMAX) ++j;
+        g.push_back(make_int2((int)i, (int)(j - i)));
+        xmax = std::max(xmax, th * 0.5 * (n0[j - 1] + L - 1 - n0[i]));
+        i = j;
+    }
+    if (2 * g.size() > n0.size()) return;
+    int mt = 0;
+    for (int m : {16, 24, 28, 32}) {
+        double b = 1.0;                                    // x^(m+1) / (m+1)!
+        for (int k = 1; k <= m + 1; ++k) b *= xmax / k;
+        if (b <= 1e-17) {
+            mt = m;
+            break;
+        }
+    }
+    if (!mt) return;
+    jk.grp = dupload(c, g);
+    jk.ngrp = (int)g.size();
+    jk.lg = jk.ngrp <= 2 ? 16 : jk.ngrp <= 4 ? 8 : 4;
+    jk.mt = mt;
 }
 
 // One traced unit (dsce_trace_unit_ex): realisation lane `lane` of the batch at
@@ -1068,6 +1113,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
     {
         Timed t(c, "k_jakes");
         if (c->jk_nsch != c->schemes.size()) update_jakes_chunks(c);
+        update_jakes_groups(c);
         launch_jakes(c->stream, op, c->ch, seed, rep0, R, b.ir, &c->jk);
     }
     const int chunk = snr_chunk(c);
@@ -1595,7 +1641,16 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     // position of the kernels' realisation-to-wave mapping
     const int N = ctx->ch.N, R = 64, lane = (int)(rep % 8);
     double2* ir = dalloc<double2>(ctx, (size_t)ctx->ch.ntap * N * R);
-    launch_jakes(ctx->stream, ctx->op, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
+    if (ctx->op.realise_win) {
+        // only the samples the schemes' Q^H windows read (the run's Jakes kernels),
+        // zero elsewhere
+        if (ctx->jk_nsch != ctx->schemes.size()) update_jakes_chunks(ctx);
+        update_jakes_groups(ctx);
+        DSCE_HIP_CHECK(hipMemsetAsync(ir, 0, (size_t)ctx->ch.ntap * N * R * sizeof(double2), ctx->stream));
+        launch_jakes(ctx->stream, ctx->op, ctx->ch, seed, rep - (uint64_t)lane, R, ir, &ctx->jk);
+    } else {
+        launch_jakes(ctx->stream, ctx->op, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
+    }
     std::vector<double2> h((size_t)ctx->ch.ntap * N * R);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ir, h.size() * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -1982,7 +2037,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom) X(realise_win)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

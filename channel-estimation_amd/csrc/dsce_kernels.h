@@ -3,6 +3,8 @@
 
 #include "dsce_common.h"
 
+#include <vector>
+
 namespace dsce {
 
 // Kernel-selection options of a context (dsce_set_option; defaults = the
@@ -32,7 +34,10 @@ struct Opts {
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
     int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
-    int jakes_mom = 1;        // Jakes taps of the read windows by phase moments (k_jakes_mom) where exact enough
+    int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
+    int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
+                              // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
+                              // each where its truncation is below rounding, else the next lower
     int mic2 = 1;             // FFT-form OFDM: every MMSE stage in one launch pair (k_mic_pilot + k_mic_data)
                               // and perfect-CSI stage 0 inside k_pic_fft; 0: per-stage k_stage0_fft / k_mic_fft
 };
@@ -144,7 +149,19 @@ struct JakesChunks {
     static constexpr int LEN = 24;   // samples per chunk
     const int* n0 = nullptr;         // device: first sample of each chunk
     int n = 0;
+    std::vector<int> n0h;            // host copy of n0 (the anchor grouping)
+    // k_jakes_grp anchor groups (jakes_grouping): runs of consecutive chunks whose
+    // span keeps |theta k| <= JAKES_XMAX around the group centre; grp[g] =
+    // (first chunk, chunk count); lg lanes per group, mt Taylor terms.  Rebuilt
+    // when theta = 2 pi |fD| dt changes; ngrp == 0: not usable.
+    const int2* grp = nullptr;
+    int ngrp = 0, lg = 0, mt = 0;
+    double theta = -1.0;
+    int nsch_grp = -1;               // chunk count the groups were built for
 };
+// the anchor groups' limit: |theta k| <= JAKES_XMAX (the Taylor sum's terms grow
+// to e^x / sqrt(2 pi x) before they fall: x = 3 costs ~20x the per-term rounding)
+constexpr double JAKES_XMAX = 3.0;
 // jc: form only those chunks (samples outside stay as they are: zero)
 void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
                   double2* ir, const JakesChunks* jc = nullptr);

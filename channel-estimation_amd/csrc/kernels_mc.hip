@@ -228,6 +228,20 @@ __device__ __forceinline__ double2 c_mul_fma(double2 z, double2 w) {
     return make_double2(fma(z.x, w.x, -z.y * w.y), fma(z.x, w.y, z.y * w.x));
 }
 
+// DPP move of a double / complex within each quad of lanes (quad_perm control;
+// also the row controls: 0x141 row_half_mirror, 0x128 row_ror 8)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false),
+                            __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double2 dpp_c(double2 v) { return make_double2(dpp_d<CTRL>(v.x), dpp_d<CTRL>(v.y)); }
+static constexpr int QP_XOR1 = 0xb1;    // quad_perm [1, 0, 3, 2]
+static constexpr int QP_XOR2 = 0x4e;    // quad_perm [2, 3, 0, 1]
+static constexpr int QP_PREV = 0x4b;    // quad_perm [3, 2, 0, 1]: the lane holding the previous time quarter
+
 static constexpr int JCH_MAX = 16;
 
 // a double from the neighbouring lane of the pair (DPP quad_perm [1, 0, 3, 2])
@@ -487,6 +501,116 @@ k_jakes_mom(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restric
     }
 }
 
+// Anchors over groups of chunks (r03, k_jakes_grp): the moment sum of
+// k_jakes_mom taken around the centre c of a run of consecutive chunks instead of
+// each chunk's own, with MT terms enough for |theta k| <= JAKES_XMAX (3.0) over the
+// run (jakes groups: MT = the smallest of 16 / 24 / 28 / 32 with x^(MT+1) / (MT+1)! <=
+// 1e-17; the terms peak at e^x / sqrt(2 pi x) ~ 5 before they fall, so the
+// rounding stays ~ 5 P eps).  At C2 two anchors per realisation and tap replace
+// fourteen: per path and anchor one cis and MT (multiply + 2 FMAs), LG lanes per
+// anchor split the paths and sum their moments by DPP (quad xor 1 / 2, row half
+// mirror, row rotate 8), then split the run's samples for Horner.
+template <int MT, int LG>
+__global__ void __launch_bounds__(256) k_jakes_grp(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+                                                   double2* __restrict__ ir, const int* __restrict__ chunk_n0,
+                                                   const int2* __restrict__ grp, int ngrp) {
+    static_assert(LG == 4 || LG == 8 || LG == 16, "lanes per anchor");
+    constexpr int JCH = JakesChunks::LEN, RPW = 2, LPR = WAVE / RPW, GPB = LPR / LG;
+    extern __shared__ double sm[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int sub = lane / LPR, sl = lane % LPR;
+    const int P = ch.paths;
+    double* ds = sm + (size_t)(wv * RPW + sub) * 3 * P;
+    double* ph = ds + P;
+    double* th = ph + P;
+    const int tap = blockIdx.z;
+    const int rl = (blockIdx.y * 4 + wv) * RPW + sub;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    for (int p = sl; p < P; p += LPR) {
+        const uint32_t e = (uint32_t)(tap + ch.ntap * p);       // rand([Ntap 1 Paths]) column-major
+        const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, e >> 1);
+        const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, e >> 1);
+        const double t = (e & 1) ? u53(wt.z, wt.w) : u53(wt.x, wt.y);
+        const double phi = (e & 1) ? u53(wp.z, wp.w) : u53(wp.x, wp.y);
+        const double d = (ch.model == 0) ? cos((t * 2.0) * M_PI) * ch.fD : (2.0 * (t - 0.5)) * ch.fD;
+        ds[p] = d;
+        ph[p] = phi;
+        th[p] = TWO_PI * (d * ch.dt);
+    }
+    __syncthreads();
+    const int gi = blockIdx.x * GPB + sl / LG, li = sl % LG;
+    if (gi >= ngrp) return;                                     // whole groups leave together
+    const int2 gr = grp[gi];
+    const int na = chunk_n0[gr.x], nb = chunk_n0[gr.x + gr.y - 1];
+    const double cen = 0.5 * ((double)na + (double)nb + (JCH - 1));
+    const double tc = cen * ch.dt;
+    double2 M[MT + 1];
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) M[m] = make_double2(0.0, 0.0);
+    int p = li;
+    for (; p + LG < P; p += 2 * LG) {
+        const double2 z0 = cis_turns(ph[p] + ds[p] * tc), z1 = cis_turns(ph[p + LG] + ds[p + LG] * tc);
+        const double t0 = th[p], t1 = th[p + LG];
+        M[0].x += z0.x + z1.x;
+        M[0].y += z0.y + z1.y;
+        double w0 = 1.0, w1 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            w1 *= t1;
+            M[m].x = fma(z1.x, w1, fma(z0.x, w0, M[m].x));
+            M[m].y = fma(z1.y, w1, fma(z0.y, w0, M[m].y));
+        }
+    }
+    if (p < P) {
+        const double2 z0 = cis_turns(ph[p] + ds[p] * tc);
+        const double t0 = th[p];
+        M[0].x += z0.x;
+        M[0].y += z0.y;
+        double w0 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            M[m].x = fma(z0.x, w0, M[m].x);
+            M[m].y = fma(z0.y, w0, M[m].y);
+        }
+    }
+    // the group's moments summed into every lane of the group; then M_m / m!
+    double f = 1.0;
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) {
+        double mx = M[m].x, my = M[m].y;
+        mx += dpp_d<QP_XOR1>(mx);
+        my += dpp_d<QP_XOR1>(my);
+        mx += dpp_d<QP_XOR2>(mx);
+        my += dpp_d<QP_XOR2>(my);
+        if constexpr (LG >= 8) {
+            mx += dpp_d<0x141>(mx);                             // row_half_mirror: the other quad of 8
+            my += dpp_d<0x141>(my);
+        }
+        if constexpr (LG >= 16) {
+            mx += dpp_d<0x128>(mx);                             // row_ror 8: the other half of the row
+            my += dpp_d<0x128>(my);
+        }
+        if (m >= 2) f /= (double)m;                             // constant-folded
+        M[m] = make_double2(mx * f, my * f);
+    }
+    const double gs = ch.sqrt_pdp[tap] / sqrt((double)P);
+    const int ns = gr.y * JCH;
+    for (int j = li; j < ns; j += LG) {
+        const int n = chunk_n0[gr.x + j / JCH] + j % JCH;
+        const double kp = (double)n - cen;
+        double2 acc = M[MT];
+#pragma unroll
+        for (int m = MT - 1; m >= 0; --m) {
+            const double ax = acc.x;
+            acc.x = fma(-kp, acc.y, M[m].x);
+            acc.y = fma(kp, ax, M[m].y);
+        }
+        if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(gs * acc.x, gs * acc.y);
+    }
+}
+
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
 // u2 = u53(w2,w3), (re, im) = sqrt(-2 log(1-u1)) (cos, sin)(2 pi u2).
 __device__ __forceinline__ double2 normal_pair(uint4 w) {
@@ -580,6 +704,23 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
     if (jc && jc->n0 && op.jakes_win && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024) {
         // the phase-moment form where its Taylor remainder is negligible
         // (|theta| (LEN - 1) / 2 <= 0.3), else the recurrence
+        if (op.jakes_mom == 2 && jc->ngrp > 0) {
+            constexpr int RPW = 2;
+            const int gpb = WAVE / RPW / jc->lg;
+            dim3 grid((jc->ngrp + gpb - 1) / gpb, R / (4 * RPW), ch.ntap);
+            const size_t lds = (size_t)4 * RPW * 3 * ch.paths * sizeof(double);
+#define LAUNCH_JGRP(MT_, LG_)                                                                                 \
+    if (jc->mt == MT_ && jc->lg == LG_) {                                                                    \
+        hipLaunchKernelGGL((k_jakes_grp<MT_, LG_>), grid, dim3(256), lds, s, ch, seed, rep0, R, ir, jc->n0,  \
+                           jc->grp, jc->ngrp);                                                               \
+        return;                                                                                              \
+    }
+            LAUNCH_JGRP(16, 4) LAUNCH_JGRP(16, 8) LAUNCH_JGRP(16, 16)
+            LAUNCH_JGRP(24, 4) LAUNCH_JGRP(24, 8) LAUNCH_JGRP(24, 16)
+            LAUNCH_JGRP(28, 4) LAUNCH_JGRP(28, 8) LAUNCH_JGRP(28, 16)
+            LAUNCH_JGRP(32, 4) LAUNCH_JGRP(32, 8) LAUNCH_JGRP(32, 16)
+#undef LAUNCH_JGRP
+        }
         if (op.jakes_mom && JakesChunks::LEN == 24 && TWO_PI * fabs(ch.fD) * ch.dt * 11.5 <= 0.3) {
             constexpr int RPW = 2, CPW = WAVE / RPW / 2;
             dim3 grid((jc->n + CPW - 1) / CPW, R / (4 * RPW), ch.ntap);
@@ -1233,18 +1374,6 @@ __device__ __forceinline__ double2 quad_tw(double2 e, bool r3) {
     return make_double2(r3 ? nx : e.x, r3 ? ny : e.y);
 }
 
-// DPP move of a double / complex within each quad of lanes (quad_perm control)
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-    const int lo = __double2loint(v), hi = __double2hiint(v);
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, false),
-                            __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ double2 dpp_c(double2 v) { return make_double2(dpp_d<CTRL>(v.x), dpp_d<CTRL>(v.y)); }
-static constexpr int QP_XOR1 = 0xb1;    // quad_perm [1, 0, 3, 2]
-static constexpr int QP_XOR2 = 0x4e;    // quad_perm [2, 3, 0, 1]
-static constexpr int QP_PREV = 0x4b;    // quad_perm [3, 2, 0, 1]: the lane holding the previous time quarter
 
 // position of output k of dft6 in the array (k = k1 + 3 k2 lands at k2 + 2 k1)
 __host__ __device__ constexpr int p6(int k) { return k / 3 + 2 * (k % 3); }

@@ -300,7 +300,11 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  * at dsce_build_mmse), 0: the W contraction everywhere), qidx, stage0_fft,
  * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic, pilot_fuse (the OFDM fast-path pieces,
  * 1 = on), mic2 (1 = every MMSE stage of FFT-form OFDM in k_mic_pilot + k_mic_data and the
- * perfect-CSI stage 0 in k_pic_fft; 0 = the per-stage kernels), snr_base (0..255: the noise of SNR index k is sub-stream
+ * perfect-CSI stage 0 in k_pic_fft; 0 = the per-stage kernels), jakes_mom (the Jakes taps of the
+ * read windows: 2 = Taylor anchors over runs of windows, 1 = one anchor per window, 0 = the
+ * recurrence; each only where its truncation stays below rounding), realise_win (1:
+ * dsce_channel_realise forms only the samples the schemes' windows read, zero elsewhere,
+ * with the run's Jakes kernels), snr_base (0..255: the noise of SNR index k is sub-stream
  * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
  * one-rank run's noise).  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);

@@ -36,6 +36,29 @@ def test_jakes_ir_matches_oracle(ofdm):
         np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("mom", [2, 1, 0])
+def test_jakes_window_kernels_match_oracle(ofdm, mom):
+    """The run's Jakes kernels (only the samples the Q^H windows read):
+    k_jakes_grp (Taylor anchors over runs of windows), k_jakes_mom (one anchor
+    per window) and the recurrence, each against the oracle's per-sample sum of
+    sinusoids at the window samples, 1e-12."""
+    S, eng, _ = ofdm
+    ch = S.chan
+    eng.set_option("realise_win", 1)
+    eng.set_option("jakes_mom", mom)
+    try:
+        for rep in (0, 1, 6, 77, 1 << 33):
+            ir_g = eng.channel_impulse_response(SEED, rep)
+            ir_o = refsim.jakes_ir(SEED, rep, S.N, ch["dt"], ch["pdp_norm"], ch["idx_taps"], ch["fD"], ch["paths"])
+            mask = ir_g != 0
+            # every tap's window samples: C2 reads 14 windows of 24
+            assert mask.sum() >= 14 * 24 * len(ch["idx_taps"]), mask.sum()
+            np.testing.assert_allclose(ir_g[mask], ir_o[mask], rtol=0, atol=1e-12, err_msg=str((mom, rep)))
+    finally:
+        eng.set_option("realise_win", 0)
+        eng.set_option("jakes_mom", 2)
+
+
 def test_correlation_matrices_match_oracle(ofdm):
     S, eng, mm = ofdm
     rhp, rest, rnoi = eng.correlation(0)
@@ -376,7 +399,7 @@ def test_stage_variants_agree(name):
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
                 {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
-                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0})
+                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0}, {"jakes_mom": 1}, {"jakes_mom": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
