@@ -1042,7 +1042,7 @@ void update_jakes_chunks(dsce_ctx* c) {
 
 // k_jakes_grp's anchor groups for the channel's theta = 2 pi |fD| dt (radians per
 // sample): runs of consecutive chunks with theta (span - 1) / 2 <= JAKES_XMAX, MT
-// the fewest Taylor terms (16 / 24 / 28 / 32) whose remainder x^(MT+1) / (MT+1)!
+// the fewest Taylor terms (16 / 24 / 28) whose remainder x^(MT+1) / (MT+1)!
 // is below 1e-17 at the widest run, LG lanes per anchor by the group count.
 // Used only when it at least halves the anchors of k_jakes_mom (one per chunk).
 void update_jakes_groups(dsce_ctx* c) {
@@ -1068,7 +1068,7 @@ void update_jakes_groups(dsce_ctx* c) {
     }
     if (2 * g.size() > n0.size()) return;
     int mt = 0;
-    for (int m : {16, 24, 28, 32}) {
+    for (int m : {16, 24, 28}) {                           // 28 covers x <= 3 (7.7e-18)
         double b = 1.0;                                    // x^(m+1) / (m+1)!
         for (int k = 1; k <= m + 1; ++k) b *= xmax / k;
         if (b <= 1e-17) {

@@ -504,14 +504,14 @@ k_jakes_mom(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restric
 // Anchors over groups of chunks (r03, k_jakes_grp): the moment sum of
 // k_jakes_mom taken around the centre c of a run of consecutive chunks instead of
 // each chunk's own, with MT terms enough for |theta k| <= JAKES_XMAX (3.0) over the
-// run (jakes groups: MT = the smallest of 16 / 24 / 28 / 32 with x^(MT+1) / (MT+1)! <=
+// run (jakes groups: MT = the smallest of 16 / 24 / 28 with x^(MT+1) / (MT+1)! <=
 // 1e-17; the terms peak at e^x / sqrt(2 pi x) ~ 5 before they fall, so the
 // rounding stays ~ 5 P eps).  At C2 two anchors per realisation and tap replace
 // fourteen: per path and anchor one cis and MT (multiply + 2 FMAs), LG lanes per
 // anchor split the paths and sum their moments by DPP (quad xor 1 / 2, row half
 // mirror, row rotate 8), then split the run's samples for Horner.
 template <int MT, int LG>
-__global__ void __launch_bounds__(256) k_jakes_grp(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_jakes_grp(ChannelK ch, uint64_t seed, uint64_t rep0, int R,
                                                    double2* __restrict__ ir, const int* __restrict__ chunk_n0,
                                                    const int2* __restrict__ grp, int ngrp) {
     static_assert(LG == 4 || LG == 8 || LG == 16, "lanes per anchor");
@@ -718,7 +718,6 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
             LAUNCH_JGRP(16, 4) LAUNCH_JGRP(16, 8) LAUNCH_JGRP(16, 16)
             LAUNCH_JGRP(24, 4) LAUNCH_JGRP(24, 8) LAUNCH_JGRP(24, 16)
             LAUNCH_JGRP(28, 4) LAUNCH_JGRP(28, 8) LAUNCH_JGRP(28, 16)
-            LAUNCH_JGRP(32, 4) LAUNCH_JGRP(32, 8) LAUNCH_JGRP(32, 16)
 #undef LAUNCH_JGRP
         }
         if (op.jakes_mom && JakesChunks::LEN == 24 && TWO_PI * fabs(ch.fD) * ch.dt * 11.5 <= 0.3) {
@@ -2656,6 +2655,8 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __syncthreads();
     const double2* __restrict__ bvb = ma.bv + ((size_t)snr * NT * ma.N + klo) * NP;
     const size_t vstride = (size_t)ma.nsnr * NT * ma.N * NP;
+    // the tap GEMM operand straight from L2 (staging each wave's window in LDS,
+    // reloaded at the W -> W0 switch: 40 more VGPRs, 1.97 -> 2.28 ms per step)
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
     auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
     mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
