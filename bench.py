@@ -425,6 +425,8 @@ def main():
         # complex product in the 3M form, 4 in the 4M form
         executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and not mic_l else 1.0)
     paths = [sorted(p) for p in paths]
+    work = {name: {"cmac_per_rep": eng.work_model(sid)[0], "mmse_kernel": mmse_kernel(set(paths[sid]))}
+            for sid, name in enumerate(schemes)}
     achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
     peak_meas = eng.fp64_mfma_peak()
@@ -519,6 +521,7 @@ def main():
         "cpu_baseline": cpu,
         "setup_s": setup_s,
         "kernels_ms": kernels,
+        "work_per_scheme": work,
         "ber_last_snr": ber,
     }
     print(json.dumps(line))
