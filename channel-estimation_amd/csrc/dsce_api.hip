@@ -519,6 +519,14 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
         s.k.row_pcol = dupload(c, row_pcol);
         s.k.row_pval = dupload(c, row_pval);
         s.k.p_diag = diag ? 1 : 0;
+        {
+            std::vector<int> seen((size_t)NP + s.d.n_data, 0);
+            for (int r = 0; r < LK; ++r)
+                if (row_pcol[r] >= 0 && row_pcol[r] < NP + s.d.n_data) ++seen[row_pcol[r]];
+            bool onto = diag;
+            for (int v : seen) onto = onto && v == 1;
+            s.k.tx_rows = onto ? 1 : 0;
+        }
     }
     // bits per realisation
     s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;
@@ -1144,7 +1152,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
             Timed t(c, "tx");
             b.U = R * std::min(chunk, c->nsnr);
             launch_tx(c->stream, s.k, c->ch, s.d.bits_slot, s.d.pilot_slot, seed, rep0, b,
-                      txrx_fft_ok(op, s.k, c->ch, b));
+                      txrx_fft_ok(op, s.k, c->ch, b), op.tx_rows != 0);
         }
         const bool pfuse = perfect_fusable(op, s.k);
         for (int s0 = 0; s0 < c->nsnr; s0 += chunk) {
@@ -2037,7 +2045,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom) X(realise_win)
+    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom) X(realise_win) X(tx_rows)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

@@ -151,6 +151,9 @@ struct SchemeK {
     const int* row_pcol;          // LK
     const double2* row_pval;      // LK
     int p_diag;
+    // p_diag and every pilot / data column sits on exactly one row: the TX
+    // symbols can be drawn row by row in parallel (k_tx_rows)
+    int tx_rows;
     // block-local perfect-CSI IC (pic_ok: every Q^H block's rows are the G
     // columns of its own samples, e.g. OFDM symbols; precondition of pf_ok)
     int pic_ok;

@@ -34,6 +34,7 @@ struct Opts {
     int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
     int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
+    int tx_rows = 1;          // row-local precoders: TX symbols drawn row-parallel (k_tx_rows)
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
@@ -168,7 +169,7 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
 // txrx (txrx_fft_ok): only the symbols; k_txrx_fft forms s, r0 and diag(D) in
 // launch_rx_front
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
-               uint64_t rep0, McBuffers& b, bool txrx = false);
+               uint64_t rep0, McBuffers& b, bool txrx = false, bool rows = true);
 bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
                          uint64_t seed, uint64_t rep0, McBuffers& b);

@@ -1152,6 +1152,48 @@ __global__ void __launch_bounds__(64) k_tx_symbols(SchemeK sk, int bits_slot, in
     }
 }
 
+// k_tx_symbols for row-local precoders (SchemeK::tx_rows, e.g. OFDM's P): every
+// row carries one pilot or data column, so the rows are drawn in parallel,
+// S row slices per realisation (grid R/64 x S: 8 waves / SIMD instead of one,
+// whose 336 sequential stream draws per lane left it latency-bound at 12 %
+// VALU issue).  Same draws, same arithmetic: xp = s / |s|, the data index from
+// the bit stream, xs[r] = p_val (0 + xin), sidr[r] = the row's data index.
+template <int S>
+__global__ void __launch_bounds__(64) k_tx_rows(SchemeK sk, int bits_slot, int pilot_slot, uint64_t seed, uint64_t rep0,
+                                                int R, double2* __restrict__ xp, uint16_t* __restrict__ sidx,
+                                                double2* __restrict__ xs, uint16_t* __restrict__ sidr) {
+    __shared__ double2 sym[256];
+    for (int i = threadIdx.x; i < sk.M; i += WAVE) sym[i] = sk.symbols[i];
+    __syncthreads();
+    const int rl = blockIdx.x * WAVE + threadIdx.x;
+    const uint64_t rep = rep0 + (uint64_t)rl;
+    const uint32_t mmask = (uint32_t)(sk.M - 1);
+    for (int r = blockIdx.y; r < sk.LK; r += S) {
+        const int k = sk.row_pcol[r];                          // uniform: one row per block and step
+        double2 acc = make_double2(0.0, 0.0);
+        if (k >= 0 && k < sk.NP) {
+            const uint4 w = stream_block(seed, rep, STREAM_PILOTS, pilot_slot, (uint32_t)k >> 2);
+            const uint32_t word = (k & 3) == 0 ? w.x : (k & 3) == 1 ? w.y : (k & 3) == 2 ? w.z : w.w;
+            const double2 s = sym[word & mmask];
+            const double a = hypot(s.x, s.y);
+            const double2 pv = make_double2(s.x / a, s.y / a);
+            xp[(size_t)k * R + rl] = pv;
+            c_fma(acc, sk.row_pval[r], pv);
+        } else if (k >= sk.NP) {
+            const int i = k - sk.NP;
+            const uint32_t q = (uint32_t)(i * sk.mbits);
+            const uint4 w = stream_block(seed, rep, STREAM_BITS, bits_slot, q >> 7);
+            const uint32_t wi = (q >> 5) & 3;
+            const uint32_t word = wi == 0 ? w.x : wi == 1 ? w.y : wi == 2 ? w.z : w.w;
+            const uint16_t si = (uint16_t)((word >> (q & 31)) & mmask);
+            sidx[(size_t)i * R + rl] = si;
+            sidr[(size_t)r * R + rl] = si;
+            c_fma(acc, sk.row_pval[r], sym[si]);
+        }
+        xs[(size_t)r * R + rl] = acc;
+    }
+}
+
 // r0 = H s (script:383-385), lane = realisation, grid (R/64, ceil(N/64)).
 __global__ void __launch_bounds__(64) k_channel_apply(ChannelK ch, int R, const double2* __restrict__ ir,
                                                       const double2* __restrict__ ss, double2* __restrict__ r0) {
@@ -1168,10 +1210,14 @@ __global__ void __launch_bounds__(64) k_channel_apply(ChannelK ch, int R, const 
 }
 
 void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_slot, int pilot_slot, uint64_t seed,
-               uint64_t rep0, McBuffers& b, bool txrx) {
+               uint64_t rep0, McBuffers& b, bool txrx, bool rows) {
     const int R = b.R;
-    hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
-                       b.xp, b.sidx, b.xs, b.sidr);
+    if (sk.tx_rows && rows)
+        hipLaunchKernelGGL((k_tx_rows<8>), dim3(R / WAVE, 8), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0,
+                           R, b.xp, b.sidx, b.xs, b.sidr);
+    else
+        hipLaunchKernelGGL(k_tx_symbols, dim3(R / WAVE), dim3(WAVE), 0, s, sk, bits_slot, pilot_slot, seed, rep0, R,
+                           b.xp, b.sidx, b.xs, b.sidr);
     if (txrx) return;      // s, r0 and diag(D) come from k_txrx_fft with the receiver front
     // s = G x (script:376-378)
     launch_band(s, sk.G, R, nullptr, LoadSoA{b.xs, R}, StoreSoA{b.ss, R});

@@ -304,7 +304,8 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  * read windows: 2 = Taylor anchors over runs of windows, 1 = one anchor per window, 0 = the
  * recurrence; each only where its truncation stays below rounding), realise_win (1:
  * dsce_channel_realise forms only the samples the schemes' windows read, zero elsewhere,
- * with the run's Jakes kernels), snr_base (0..255: the noise of SNR index k is sub-stream
+ * with the run's Jakes kernels), tx_rows (1: TX symbols of a row-local precoder drawn
+ * row-parallel), snr_base (0..255: the noise of SNR index k is sub-stream
  * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
  * one-rank run's noise).  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);

@@ -399,7 +399,8 @@ def test_stage_variants_agree(name):
                 {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
                 {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
-                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0}, {"jakes_mom": 1}, {"jakes_mom": 0})
+                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0}, {"jakes_mom": 1}, {"jakes_mom": 0},
+                {"tx_rows": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
