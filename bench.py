@@ -317,8 +317,8 @@ def launch_ranks(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--reps-per-step", type=int, default=0, help="realisations per step per GPU (0: workload default)")
     ap.add_argument("--batch", type=int, default=0, help="realisations per device batch (0: = reps per step)")
