@@ -317,8 +317,10 @@ def launch_ranks(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    # defaults: C2 100 timed steps after 10 warm-up (about 1 s timed: steady
+    # state), the slower configurations 10 after 2
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--reps-per-step", type=int, default=0, help="realisations per step per GPU (0: workload default)")
     ap.add_argument("--batch", type=int, default=0, help="realisations per device batch (0: = reps per step)")
@@ -328,6 +330,10 @@ def main():
     ap.add_argument("--cpu-baseline-leg", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--leg-index", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 100 if args.config == "c2" else 10
+    if args.warmup is None:
+        args.warmup = 10 if args.config == "c2" else 2
     if args.cpu_baseline_leg:
         cpu_baseline_leg(args.cpu_seconds, args.config, args.leg_index)
         return 0
