@@ -12,6 +12,7 @@ __global__ void __launch_bounds__(256) k_op(double* out, int n) {
     double a0 = threadIdx.x * 1e-3, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
            a7 = a0 + 7;
     const double b = 1.0000001, c = 1e-9;
+    double x0 = a0 * 2, x1 = a1 * 2, x2 = a2 * 2, x3 = a3 * 2, x4 = a4 * 2, x5 = a5 * 2, x6 = a6 * 2, x7 = a7 * 2;
     int i0 = threadIdx.x, i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3, i4 = i0 + 4, i5 = i0 + 5, i6 = i0 + 6, i7 = i0 + 7;
     const unsigned long long m = (blockIdx.x & 1) ? 0x5555555555555555ull : 0xaaaaaaaaaaaaaaaaull;
     for (int it = 0; it < n; ++it) {
@@ -57,6 +58,25 @@ __global__ void __launch_bounds__(256) k_op(double* out, int n) {
                 REP8(F)
 #undef F
                 asm volatile("s_waitcnt lgkmcnt(0)");
+            } else if constexpr (OP == 10) {
+                // v_mfma_f64_4x4x4f64, 8 independent accumulators
+#define F(k) a##k = __builtin_amdgcn_mfma_f64_4x4x4f64(b, c, a##k, 0, 0, 0);
+                REP8(F)
+#undef F
+            } else if constexpr (OP == 11) {
+                // v_mfma_f64_16x16x4f64 (4 accumulator registers each; 8 chains)
+                typedef double d4v __attribute__((ext_vector_type(4)));
+                d4v q0 = {a0, a1, a2, a3}, q1 = {a4, a5, a6, a7};
+#define F(k) q##k = __builtin_amdgcn_mfma_f64_16x16x4f64(b, c, q##k, 0, 0, 0);
+                F(0) F(1) F(0) F(1) F(0) F(1) F(0) F(1)
+#undef F
+                a0 = q0[0]; a1 = q0[1]; a2 = q0[2]; a3 = q0[3]; a4 = q1[0]; a5 = q1[1]; a6 = q1[2]; a7 = q1[3];
+            } else if constexpr (OP == 12) {
+                // a 4x4x4 MFMA beside 4 independent f64 FMAs
+#define F(k) a##k = __builtin_amdgcn_mfma_f64_4x4x4f64(b, c, a##k, 0, 0, 0); \
+             asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x##k) : "v"(b), "v"(c));
+                REP8(F)
+#undef F
             } else if constexpr (OP == 7) {
                 // f64 FMA and DPP alternating (the chain network's mix)
 #define F(k) asm volatile("v_fma_f64 %0, %0, %2, %3\n v_mov_b32_dpp %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##k), "+v"(i##k) : "v"(b), "v"(c));
@@ -65,7 +85,7 @@ __global__ void __launch_bounds__(256) k_op(double* out, int n) {
             }
         }
     }
-    out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + i0 + i1 + i2 + i3 + i4 + i5 + i6 + i7;
+    out[blockIdx.x * 256 + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7 + i0 + i1 + i2 + i3 + i4 + i5 + i6 + i7;
 }
 
 template <int OP>
@@ -92,11 +112,12 @@ int main() {
     hipMalloc(&d, (size_t)cus * 8 * 256 * sizeof(double));
     const char* names[] = {"v_fma_f64", "v_add_f64", "v_mul_f64", "v_mov_b32_dpp", "v_cndmask_b32", "v_add_u32",
                            "v_fma_f32", "fma_f64+dpp (per pair)", "ds_swizzle_b32 (8, wait)",
-                           "fma_f64+swizzle (per pair)"};
+                           "fma_f64+swizzle (per pair)", "mfma_f64_4x4x4", "mfma_f64_16x16x4 (2 chains)",
+                           "mfma4x4x4+fma_f64 (per pair)"};
     const int n = 2000;
     printf("CUs %d clock %.2f GHz; cycles per wave-instruction per SIMD (8 chains per wave)\n", cus, ghz);
     printf("%-24s %8s %8s %8s %8s\n", "op", "1 w/SIMD", "2", "3", "4");
-    for (int op = 0; op < 10; ++op) {
+    for (int op = 0; op < 13; ++op) {
         printf("%-24s", names[op]);
         for (int w = 1; w <= 4; ++w) {
             const int blocks = cus * w;          // 256 threads = one wave per SIMD per block
@@ -112,6 +133,9 @@ int main() {
                 case 7: ms = run<7>(d, blocks, n); break;
                 case 8: ms = run<8>(d, blocks, n); break;
                 case 9: ms = run<9>(d, blocks, n); break;
+                case 10: ms = run<10>(d, blocks, n); break;
+                case 11: ms = run<11>(d, blocks, n); break;
+                case 12: ms = run<12>(d, blocks, n); break;
             }
             const double instr_per_simd = (double)w * n * 32;      // per wave: n x 4 x 8
             printf(" %8.2f", ms * 1e-3 * ghz * 1e9 / instr_per_simd);
