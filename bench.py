@@ -407,14 +407,12 @@ def main():
     total_reps = B * args.steps * world
     value = total_reps / el
 
-    # roofline of the dominant kernel (the MMSE IC: k_mic_fft where the scheme is
-    # FFT-form OFDM, else the W contraction k_wcontract; HIP events on the
-    # engine's stream)
-    # each scheme's MMSE kernel: k_mic_data (every stage in one launch pair), k_mic_fft
-    # (per-iteration FFT form) or the W contraction; the dominant one by measured time
-    # carries the roofline, with the work model of the schemes it runs
+    # roofline of the dominant kernel (HIP events on the engine's stream): each
+    # scheme's MMSE kernel is k_mic_data (FFT-form OFDM: every stage in one launch
+    # pair with k_mic_pilot) or the W contraction k_wcontract; the dominant one by
+    # measured time carries the roofline, with the work model of the schemes it runs
     def mmse_kernel(p):
-        return "k_mic_data" if "mic_stages" in p else "k_mic_fft" if "mic_fft" in p else "k_wcontract"
+        return "k_mic_data" if "mic_stages" in p else "k_wcontract"
     paths = [eng.path_info(sid) for sid in range(len(schemes))]
     kname = max({mmse_kernel(p) for p in paths}, key=lambda k: eng.kernel_time(k)[1])
     mic_l = kname != "k_wcontract"
@@ -428,7 +426,7 @@ def main():
         f = cmac_per_rep * 8.0 * B * args.steps
         flops += f
         # matrix-core flops actually executed per counted flop: 3 real MFMAs per
-        # complex product in the 3M form, 4 in the 4M form
+        # complex product in the 3M form
         executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and not mic_l else 1.0)
     paths = [sorted(p) for p in paths]
     work = {name: {"cmac_per_rep": eng.work_model(sid)[0], "mmse_kernel": mmse_kernel(set(paths[sid]))}
@@ -445,7 +443,7 @@ def main():
     hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
     bound = "hbm" if hbm_frac is not None and achieved_tf and hbm_frac > achieved_tf / FP64_PEAK_TFLOPS else "mfma"
     kernels = {}
-    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_fft", "k_mic_pilot", "k_mic_data",
+    for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_pilot", "k_mic_data",
               "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
         kernels[k] = {"launches": n, "ms": round(ms, 3)}
@@ -489,11 +487,7 @@ def main():
                                 "pilots, decisions in registers: per stage H_hat = Bv hP on the matrix cores (3M), "
                                 "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain, one-tap + detection on the "
                                 "VALU; FP64 roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both "
-                                "peaks 78.6 TF)") if kname == "k_mic_data" else
-                               ("k_mic_fft: MMSE IC iteration as y - Q'(H_hat (G v)) + diag(D_hat) v; H_hat = Bv hP "
-                                "on the matrix cores (3M), DFT-24 chain + one-tap + detection on the VALU; FP64 "
-                                "roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both peaks "
-                                "78.6 TF)") if mic_l else
+                                "peaks 78.6 TF)") if mic_l else
                                ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
                                 "diag(D_hat) + detection in its epilogue)"),
                      "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -501,7 +495,7 @@ def main():
                      "peak_measured": peak_meas,
                      "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas else None,
                      # executed matrix-core flops / measured peak from the work model (W contraction), or the
-                     # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (k_mic_fft: only its tap GEMM
+                     # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (k_mic_data: only its tap GEMM
                      # runs on the matrix cores)
                      "mfma_busy": (lim or {}).get("mfma_busy") if mic_l else
                      ((exec_tf / peak_meas) if exec_tf and peak_meas else None),
@@ -512,11 +506,7 @@ def main():
                      "work_model": ("per unit and data symbol: stage 0 window sums ntap x NP + 24; per IC stage the "
                                     "estimated taps ntap x 24 x NP CMACs, their window sums ntap x 24, the channel "
                                     "ntap x 24, diag(D_hat_prev) v 24, this stage's window sums ntap x NP and diag 24 "
-                                    "(8 flops per CMAC) + two DFT-24 at 5 n log2 n flops") if kname == "k_mic_data" else
-                                   ("per unit and OFDM symbol: estimated taps ntap x 24 x NP CMACs, window sums "
-                                    "ntap x NP, channel ntap x 24, diag(D_hat) 2 x 24 CMACs (8 flops each) + two DFT-24 "
-                                    "at 5 n log2 n flops; with pilot_fuse (iterations 1..niter-1) also the next iteration's pilot-symbol "
-                                    "chains (taps, channel, diag(D_hat) u, two DFT-24); peak = FP64 matrix spec (= FP64 vector spec)") if mic_l else
+                                    "(8 flops per CMAC) + two DFT-24 at 5 n log2 n flops") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
                                     "fused diag(D_hat)), 8 real flops per CMAC; the 3M form executes 6 of the 8 counted "
                                     "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "

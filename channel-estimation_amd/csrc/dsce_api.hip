@@ -98,14 +98,13 @@ struct Scheme {
     long long w_elems = 0, w_struct = 0;
     double2* W = nullptr;
     double2* Wd = nullptr;
-    double2* Wp = nullptr;          // pair-tile copy of W for k_wpair (null: not eligible)
-    double* Wp3 = nullptr;          // its Re / Im / Re+Im planes (3M complex products)
+    double* Wp3 = nullptr;          // pair-tile copy of W as Re / Im / Re+Im planes (k_wpair3; null: not eligible)
     double2* Wpil = nullptr;        // fused MMSE stage operands (null: not eligible)
     double2* WdA = nullptr;
     int* pil_c0 = nullptr;
-    double2* Bv = nullptr;          // structured MMSE IC operator (k_mic_fft; null: not eligible)
+    double2* Bv = nullptr;          // structured MMSE IC operator (k_mic_pilot / k_mic_data; null: not eligible)
     double2* Bs = nullptr;
-    int* pblk = nullptr;            // QH blocks with pilot rows (k_pilot_fft, k_mic_pilot)
+    int* pblk = nullptr;            // QH blocks with pilot rows (k_mic_pilot)
     int* pmask = nullptr;           // [QH blk] 1 = holds pilot rows
     int npb = 0;
     int* dblk = nullptr;            // QH blocks without pilot rows (k_mic_data)
@@ -134,8 +133,6 @@ using namespace dsce;
 struct dsce_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;        // perfect-CSI branch of the IC iterations
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool chan_set = false;
     ChannelK ch{};
@@ -591,7 +588,7 @@ void trim_w_band(dsce_ctx* c, Scheme& s, std::vector<void*>& tmp) {
 
 // ---------------------------------------------------------------------------
 // setup pipeline: R_hP, R_est, R_noI, R_Dij, W, W0 (script:208-313)
-// Pair-tile copy of the trimmed W band for k_wpair (NP a multiple of 4 with
+// Pair-tile copy of the trimmed W band for k_wpair3 (NP a multiple of 4 with
 // NP/4 in {2, 4, 8}; 24-row pair blocks when every block has <= 24 rows, else 32).
 void build_wpair(dsce_ctx* c, Scheme& s) {
     const int NP = s.d.n_pilots, nblk = (int)s.wband.row0.size();
@@ -625,10 +622,13 @@ void build_wpair(dsce_ctx* c, Scheme& s) {
     s.wp_elems = std::max<long long>(o, 1);
     s.wp_exec = exec;
     const int nsl = 2 * c->nsnr;
-    s.Wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
+    // the complex pair tiles are only the packer's intermediate: freed once the
+    // 3M planes exist
+    double2* wp = dalloc<double2>(c, (size_t)nsl * s.wp_elems);
     // W's 3M planes, two k-steps per 16-byte lane load
     s.Wp3 = dalloc<double>(c, (size_t)nsl * 3 * s.wp_elems);
-    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, s.Wp, s.wp_elems, nsl, s.Wp3);
+    setup_wpair(c->stream, s.Wb, NP, s.W, s.w_elems, s.Pb, wp, s.wp_elems, nsl, s.Wp3);
+    free_alloc(c, wp);
     // fused MMSE stage: block-diagonal W (every block's columns are its own 24
     // rows, OFDM), row-local precoder, select-mode detection, NP = 16
     bool fuse = rbp == 24 && NP == 16 && s.k.p_diag && !s.d.despread;
@@ -675,7 +675,7 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 }
 
 // ---------------------------------------------------------------------------
-// Operator of the structured MMSE IC (k_mic_fft): D_hat = Q' H_hat G with the
+// Operator of the structured MMSE IC (k_mic_pilot / k_mic_data): D_hat = Q' H_hat G with the
 // estimated taps H_hat = Bv hP (setup_bv).  Eligible: FFT-form OFDM blocks
 // (SchemeK::pf_ok), the fused stage's pilot pre-pass (Wpil), NP = 16, at most two
 // taps with delays <= 1.  Kept only if Q' H_hat G reproduces EVERY entry of the
@@ -824,7 +824,6 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
     if (s.W) {                     // rebuild (e.g. new SNR list): back to the structural band
         free_alloc(c, s.W);
         free_alloc(c, s.Wd);
-        if (s.Wp) free_alloc(c, s.Wp);
         if (s.Wp3) free_alloc(c, s.Wp3);
         if (s.Wpil) free_alloc(c, s.Wpil);
         if (s.WdA) free_alloc(c, s.WdA);
@@ -837,7 +836,7 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         s.Bv = s.Bs = nullptr;
         s.pblk = s.pmask = s.dblk = nullptr;
         s.npb = s.ndb = 0;
-        s.W = s.Wd = s.Wp = nullptr;
+        s.W = s.Wd = nullptr;
         s.Wp3 = nullptr;
         s.Wpil = s.WdA = nullptr;
         s.pil_c0 = nullptr;
@@ -994,7 +993,6 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.yperf = dalloc<double2>(c, LK * U, L);
     b.hp = dalloc<double2>(c, NP * U, L);
     b.hp2 = dalloc<double2>(c, NP * U, L);
-    b.hp3 = dalloc<double2>(c, NP * U, L);
     b.hest = dalloc<double2>(c, LK * U, L);
     b.v = dalloc<double2>(c, LK * U, L);
     b.u = dalloc<double2>(c, LK * U, L);
@@ -1004,8 +1002,6 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.qe = dalloc<uint16_t>(c, ND * U, L);
     b.qp = dalloc<uint16_t>(c, ND * U, L);
     b.sidr = dalloc<uint16_t>(c, (LK + 32) * R, L);
-    b.qre = dalloc<uint16_t>(c, LK * U, L);
-    b.qrp = dalloc<uint16_t>(c, LK * U, L);
     // LS pilot estimates of every stage (k_mic_pilot -> k_mic_data)
     b.hpa_stages = c->niter + 1;
     b.hpa = dalloc<double2>(c, (size_t)b.hpa_stages * NP * U, L);
@@ -1134,7 +1130,6 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
         mm.w_elems = s.w_elems;
         mm.nsnr = c->nsnr;
         mm.Wb = s.Wb;
-        mm.Wp = s.Wp;
         mm.Wp3 = s.Wp3;
         mm.wp_elems = s.wp_elems;
         mm.Pb = s.Pb;
@@ -1173,13 +1168,13 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
             }
             if (to && to->y) copy_col(c, to->y, b.y, LK, b.U, tunit);
             if (to && to->h_perfect) copy_col(c, to->h_perfect, b.h, LK, R, tr->lane);
-            // FFT-form OFDM (mic2): the perfect-CSI branch is one k_pic_fft with its
+            // FFT-form OFDM: the perfect-CSI branch is one k_pic_fft with its
             // stage 0, the MMSE branch k_mic_pilot + k_mic_data, every stage each
             if (pfuse && mmse_stages_ok(op, s.k, mm, c->ch, b, c->niter)) {
                 PerfectDetectArgs pd{c->d_counters, (int)si, 0, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
                 {
                     Timed t(c, "perfect_ic");
-                    s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, false, true);
+                    s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, true);
                 }
                 {
                     Timed t(c, "k_mic_pilot");
@@ -1195,90 +1190,23 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 b.tr = nullptr;
                 continue;
             }
-            // With the perfect-CSI branch fused into perfect_ic, the IC iterations
-            // are two independent chains after stage 0: MMSE (contraction ->
-            // stage, MFMA-bound) on the main stream and perfect CSI on stream2
-            // (Opts::streams = 2), joined before the next chunk.
-            const bool two = pfuse && op.streams == 2 && !tracing;
-            // FFT-form OFDM: the whole perfect-CSI chain is one kernel (k_pic_fft,
-            // u in registers across the iterations)
+            // Otherwise one launch group per stage.  With the perfect-CSI branch
+            // fused into perfect_ic, the IC iterations are two independent chains
+            // after stage 0: MMSE (contraction -> stage) and perfect CSI.
+            // FFT-form OFDM with the W contraction (mmse_ic 0): the whole
+            // perfect-CSI chain is one kernel (k_pic_fft, u in registers)
             const bool chain = pfuse && perfect_chain_ok(op, s.k, c->ch, b, c->niter);
             // block-diagonal W + row-local P (OFDM): the MMSE stage of every IC
             // iteration rides in the contraction's epilogue (k_pilot_pre +
             // k_wpair3<..., true>); hP alternates between hp and hp2
             const bool mfuse = pfuse && mmse_fused_ok(op, s.k, mm, b);
-            // OFDM: the MMSE IC as Q' H_hat G by FFT (k_pilot_pre + k_mic_fft)
-            const bool mic = pfuse && mmse_fft_ok(op, s.k, mm, c->ch, b);
-            // the pilot pass hands y_ic of the pilot symbols to k_mic_fft
-            const bool yic = mic && op.pilot_fft && op.mic_yic && mm.npb > 0;
-            // both IC chains index-based (k_mic_fft + k_pic_fft): the stage and the
-            // chains pass decisions as symbol indices (qe / qp), not as v / u
-            const bool qidx = mic && chain && s.k.M <= 65536 && op.qidx &&
-                              perfect_chain_fft(op, s.k, c->ch, b, c->niter);
             double2* hp_prev = b.hp;
             double2* hp_cur = b.hp2;
-            double2* hp_next = b.hp3;
-            // pilot_fuse: iteration it's k_mic_fft also runs iteration it + 1's
-            // pilot pass in its pilot-symbol blocks (hP of it + 1 into hp_next)
-            const bool pfz = yic && op.pilot_fuse && op.mic_mfma;
-            bool have_next = false;
             for (int it = 0; it <= c->niter; ++it) {
-                if (it == 1 && (two || chain)) {
-                    hipStream_t ps = two ? c->stream2 : c->stream;
-                    if (two) {
-                        DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
-                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
-                    }
-                    if (chain) {
-                        Timed t(c, "perfect_ic", ps);
-                        PerfectDetectArgs pd{c->d_counters, (int)si, 1, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
-                        s.path |= launch_perfect_chain(ps, op, s.k, c->ch, b, &pd, c->niter, qidx);
-                    } else {
-                        for (int jt = 1; jt <= c->niter; ++jt) {
-                            Timed t(c, "perfect_ic", ps);
-                            PerfectDetectArgs pd{c->d_counters, (int)si, jt, c->niter + 1, c->nsnr, jt == c->niter,
-                                                 s.k.slI, s.k.slQ};
-                            s.path |= launch_perfect_ic(ps, op, s.k, c->ch, b, &pd);
-                        }
-                    }
-                    if (two) DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
-                }
-                if (it > 0 && mic) {
-                    if (!have_next) {
-                        Timed t(c, "k_pilot_pre");
-                        if (op.pilot_fft && mm.npb > 0)
-                            launch_pilot_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter), b, hp_prev,
-                                             hp_cur, op.xcd, qidx, yic);
-                        else
-                            launch_pilot_pre(c->stream, s.k, mm, var_of_stage(it - 1, c->niter), b, hp_prev, hp_cur,
-                                             qidx);
-                    }
-                    if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, hp_cur, NP, b.U, tunit);
-                    {
-                        Timed t(c, "k_mic_fft");
-                        PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
-                                             s.k.slI, s.k.slQ};
-                        s.path |= launch_mmse_fft(c->stream, s.k, mm, c->ch, var_of_stage(it - 1, c->niter),
-                                                  var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
-                                                  hp_prev, hp_cur, &pd, op.xcd, qidx, op.mic_mfma != 0, yic,
-                                                  pfz ? hp_next : nullptr);
-                    }
-                    have_next = pfz && it < c->niter;
-                    if (have_next) {
-                        double2* const t = hp_prev;
-                        hp_prev = hp_cur;
-                        hp_cur = hp_next;
-                        hp_next = t;
-                    } else {
-                        std::swap(hp_prev, hp_cur);
-                    }
-                    if (!two && !chain) {
-                        Timed t(c, "perfect_ic");
-                        PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
-                                             s.k.slI, s.k.slQ};
-                        s.path |= launch_perfect_ic(c->stream, op, s.k, c->ch, b, pfuse ? &pd : nullptr);
-                    }
-                    continue;
+                if (it == 1 && chain) {
+                    Timed t(c, "perfect_ic");
+                    PerfectDetectArgs pd{c->d_counters, (int)si, 1, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
+                    s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter);
                 }
                 if (it > 0 && mfuse) {
                     {
@@ -1287,14 +1215,14 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                     }
                     if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, hp_cur, NP, b.U, tunit);
                     {
-                        // the contraction with the stage in its epilogue (bench's roofline kernel)
+                        // the contraction with the stage in its epilogue
                         Timed t(c, "k_wcontract");
                         s.path |= launch_mmse_fused(c->stream, op, s.k, mm, var_of_stage(it - 1, c->niter),
                                                     var_of_stage(it, c->niter), it, c->niter, it == c->niter, b,
                                                     hp_prev, hp_cur, c->d_counters, (int)si);
                     }
                     std::swap(hp_prev, hp_cur);
-                    if (!two && !chain) {
+                    if (!chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
                                              s.k.slI, s.k.slQ};
@@ -1308,7 +1236,7 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                         s.path |= launch_wcontract(c->stream, op, s.k, mm, var_of_stage(it - 1, c->niter), b);
                     }
                     if (to && to->yest_stages) copy_col(c, to->yest_stages + (size_t)2 * it * LK, b.yest, LK, b.U, tunit);
-                    if (!two && !chain) {
+                    if (!chain) {
                         Timed t(c, "perfect_ic");
                         PerfectDetectArgs pd{c->d_counters, (int)si, it, c->niter + 1, c->nsnr, it == c->niter,
                                              s.k.slI, s.k.slQ};
@@ -1319,18 +1247,11 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 }
                 {
                     Timed t(c, "k_stage");
-                    if (it == 0 && qidx && op.stage0_fft) {
-                        PerfectDetectArgs pd{c->d_counters, (int)si, 0, c->niter + 1, c->nsnr, c->niter == 0,
-                                             s.k.slI, s.k.slQ};
-                        s.path |= launch_stage0_fft(c->stream, s.k, mm, c->ch, c->niter, c->niter == 0, b, &pd, op.xcd);
-                    } else {
-                        s.path |= launch_stage(c->stream, op, s.k, mm, it, var_of_stage(it, c->niter), c->niter,
-                                               it == c->niter, b, c->d_counters, (int)si, !(pfuse && it > 0), qidx);
-                    }
+                    s.path |= launch_stage(c->stream, op, s.k, mm, it, var_of_stage(it, c->niter), c->niter,
+                                           it == c->niter, b, c->d_counters, (int)si, !(pfuse && it > 0));
                 }
                 if (to && to->hp_stages) copy_col(c, to->hp_stages + (size_t)2 * it * NP, b.hp, NP, b.U, tunit);
             }
-            if (two && c->niter > 0) DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
             b.tr = nullptr;
         }
     }
@@ -1389,9 +1310,6 @@ int dsce_create(int hip_device, dsce_ctx** out) {
     try {
         DSCE_HIP_CHECK(hipSetDevice(hip_device));
         DSCE_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        DSCE_HIP_CHECK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-        DSCE_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-        DSCE_HIP_CHECK(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
     } catch (const std::exception& e) {
         delete ctx;
         return DSCE_EHIP;
@@ -1412,9 +1330,6 @@ void dsce_destroy(dsce_ctx* ctx) {
     }
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     delete ctx;
 }
 
@@ -1926,9 +1841,7 @@ int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
         free_alloc(ctx, s.W);
         s.W = nullptr;
     }
-    if (s.Wp) free_alloc(ctx, s.Wp);
     if (s.Wp3) free_alloc(ctx, s.Wp3);
-    s.Wp = nullptr;
     s.Wp3 = nullptr;
     s.interp = true;
     upload_interp(ctx, s);
@@ -1984,10 +1897,6 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
     // stage (LK x NP CMACs per unit)
     const double fused = (s.path & PATH_WPAIR3_FUSED) ? (double)s.LK * s.d.n_pilots : 0.0;
     if (cmac) *cmac = ((double)(s.w_struct - s.w_diag) + fused) * ctx->nsnr * ctx->niter;
-    // structured MMSE IC (k_mic_fft), per unit and FFT block: the estimated taps
-    // (ntap x 24 x NP), this stage's window sums (ntap x NP), the channel (ntap x
-    // 24), both diag(D_hat) terms (2 x 24) and two DFT-24 at 5 n log2 n flops
-    // (counted as flops / 8 CMACs)
     if (cmac && (s.path & PATH_MIC_STAGES)) {
         // k_mic_data (the bench's roofline kernel), per unit and data symbol:
         // stage 0 window sums (ntap x NP) + diag(D_hat) / one-tap (24); every
@@ -1999,16 +1908,6 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
         const double st0 = nt * NP + 24;
         const double sti = nt * 24 * NP + nt * 24 + nt * 24 + 24 + nt * NP + 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
         *cmac = (st0 + it * sti) * s.ndb * ctx->nsnr;
-    } else if (cmac && (s.path & PATH_MIC_FFT)) {
-        const double nt = ctx->ch.ntap, NP = s.d.n_pilots;
-        const double blk = nt * 24 * NP + nt * NP + nt * 24 + 2 * 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
-        *cmac = blk * s.k.QH.nblk * ctx->nsnr * ctx->niter;
-        // pilot_fuse: iterations 1..niter-1 also form the next iteration's y_ic of
-        // the pilot symbols (taps, channel, diag(D_hat) u, two DFT-24)
-        if (s.path & PATH_PILOT_FUSED) {
-            const double pil = nt * 24 * NP + nt * 24 + 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
-            *cmac += pil * s.npb * ctx->nsnr * (ctx->niter - 1);
-        }
     }
     if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
     API_END
@@ -2044,8 +1943,8 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
-    X(xcd) X(fuse_stage) X(wpair_3m) X(wda_3m) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(streams) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(qidx) X(stage0_fft) X(mic_mfma) X(pilot_fft) X(jakes_win) X(txrx_fft) X(mic_yic) X(pilot_fuse) X(snr_base) X(mic2) X(jakes_mom) X(realise_win) X(tx_rows)
+    X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN
@@ -2062,7 +1961,6 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     if (n == "pic_chain" && value != 0 && value != 3)
         throw ApiError(DSCE_EINVAL, "pic_chain: 0 (per-iteration passes) | 3 (k_pic_fft); the r01 chains 1 / 2 "
                                     "(k_pic_chain, k_pic_mfma) were retired in r03");
-    if (n == "streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "streams: 1 | 2");
     if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
     if (n == "snr_base") check_noise_streams(ctx, value, ctx->nsnr, max_noise_slot(ctx));
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");

@@ -12,35 +12,24 @@ namespace dsce {
 struct Opts {
     int xcd = 1;              // XCD-aware work order (each XCD walks a contiguous range)
     int fuse_stage = 1;       // MMSE stage of the IC iterations fused into the contraction
-    int wpair_3m = -1;        // 3M complex products in k_wpair3: -1 / 1 on (default), 0 off (4 MFMAs)
-    int wda_3m = 1;           // fused epilogue's diag(D_hat) in 3M form
     int pic_chain = 3;        // perfect-CSI IC: 0 per-iteration passes, 1 VALU chain, 2 MFMA chain, 3 FFT chain
     int pfuse = 1;            // perfect-CSI detection fused into the second banded pass
     int stage_split = 0;      // 1: 3-kernel stage (k_ls_hest, k_detect, k_precode) for every scheme
     int stage_rb = 8;         // rows per wave of k_stage_fused: 4 | 8 | 16
     int noise_fuse = 1;       // AWGN drawn inside the Q^H pass (disjoint Q^H blocks)
     int snr_chunk = 0;        // SNR points per receiver chunk (0: all)
-    int streams = 1;          // 2: perfect-CSI chain on a second stream
     int jakes_rpw = 2;        // realisations per Jakes wave (1 | 2)
     int wtrim = 1;            // trim W to its non-zero column extent (read by dsce_build_mmse)
     int wcontract_valu = 0;   // 1: VALU contraction instead of the MFMA pair tiles
-    int mmse_ic = 1;          // MMSE IC of OFDM as Q' H_hat G by FFT (k_mic_fft) where eligible; 0: W contraction
-    int qidx = 1;             // k_mic_fft + k_pic_fft: decisions between stages as symbol indices, not v / u
-    int stage0_fft = 1;       // with qidx: stage 0 as k_stage0_fft (symbol blocks, structured diag(D_hat))
-    int mic_mfma = 1;         // k_mic_fft's estimated taps as an MFMA GEMM (3M) instead of VALU dot products
-    int pilot_fft = 1;        // structured pilot pre-pass (k_mic_fft PILOT mode) instead of k_pilot_pre's W rows
+    int mmse_ic = 1;          // MMSE branch of FFT-form OFDM as Q' H_hat G (k_mic_pilot + k_mic_data); 0: W contraction
     int jakes_win = 1;        // Jakes taps only at the samples some Q^H row reads (JakesChunks)
     int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
-    int mic_yic = 1;          // k_mic_fft's pilot-symbol blocks reuse the pilot pass's y_ic
-    int pilot_fuse = 1;       // with mic_yic: the next iteration's pilot pass rides in k_mic_fft's pilot-symbol blocks
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
     int tx_rows = 1;          // row-local precoders: TX symbols drawn row-parallel (k_tx_rows)
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower
-    int mic2 = 1;             // FFT-form OFDM: every MMSE stage in one launch pair (k_mic_pilot + k_mic_data)
-                              // and perfect-CSI stage 0 inside k_pic_fft; 0: per-stage k_stage0_fft / k_mic_fft
 };
 
 // Kernels a scheme's last dsce_run / dsce_trace_unit_ex went through
@@ -48,7 +37,7 @@ struct Opts {
 enum : unsigned {
     PATH_WPAIR3_FUSED = 1u << 0,   // k_pilot_pre + k_wpair3<.., FUSE> (stage in the contraction epilogue)
     PATH_WPAIR3 = 1u << 1,         // k_wpair3 (3M, unfused)
-    PATH_WPAIR4M = 1u << 2,        // k_wpair (4 real MFMAs per complex product)
+    PATH_WPAIR4M = 1u << 2,        // retired (r01-r02 k_wpair, 4 real MFMAs per complex product)
     PATH_WCONTRACT_VALU = 1u << 3, // k_wcontract_valu
     PATH_PIC_MFMA = 1u << 4,       // k_pic_mfma (perfect-CSI chain on the matrix cores)
     PATH_PIC_CHAIN = 1u << 5,      // k_pic_chain (VALU chain)
@@ -57,10 +46,10 @@ enum : unsigned {
     PATH_STAGE_SPLIT = 1u << 8,    // k_ls_hest + k_detect + k_precode
     PATH_NOISE_FUSED = 1u << 9,    // noise drawn inside the Q^H pass
     PATH_PIC_FFT = 1u << 10,       // k_pic_fft (perfect-CSI chain by FFT, OFDM)
-    PATH_MIC_FFT = 1u << 11,       // k_pilot_pre + k_mic_fft (MMSE IC as Q' H_hat G by FFT, OFDM)
+    PATH_MIC_FFT = 1u << 11,       // MMSE IC as Q' H_hat G by FFT (OFDM; k_mic_pilot + k_mic_data)
     PATH_TXRX_FFT = 1u << 12,      // k_txrx_fft (TX + channel + noisy receiver front by FFT, OFDM)
-    PATH_PILOT_FUSED = 1u << 13,   // k_mic_fft also runs the next iteration's pilot pass (pilot_fuse)
-    PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair (mic2)
+    PATH_PILOT_FUSED = 1u << 13,   // retired (r02 k_mic_fft's fused pilot pass)
+    PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -99,7 +88,6 @@ struct McBuffers {
     double2* yperf;   // [LK][U]
     double2* hp;      // [NP][U]   LS pilot estimates of the current stage
     double2* hp2;     // [NP][U]   second buffer (fused MMSE stage: previous / current stage)
-    double2* hp3;     // [NP][U]   third buffer (k_mic_fft with the next iteration's pilot pass)
     double2* hest;    // [LK][U]   diag(D_hat) of the current stage
     double2* v;       // [LK][U]   P [xP; Q(x_est)]
     double2* u;       // [LK][U]   P [xP; Q(x_perfect)]
@@ -109,8 +97,6 @@ struct McBuffers {
     uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
     uint16_t* sidr;   // [LK][R]   transmitted symbol index per data row (row-indexed sidx)
-    uint16_t* qre;    // [LK][U]   QIDX chains: MMSE decisions per data row
-    uint16_t* qrp;    // [LK][U]   QIDX chains: perfect-CSI decisions per data row
     double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (mic2), or null
     int hpa_stages;   // stages hpa holds
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
@@ -124,7 +110,6 @@ struct MmseK {
     long long w_elems;
     int nsnr;
     Band Wb;              // block geometry (vals unused; per-(var,snr) base added)
-    const double2* Wp;    // [var][snr][wp_elems] pair-tile layout (k_wpair), or null
     const double* Wp3;    // [var][snr][3 wp_elems] Re / Im / Re+Im planes (3M form), or null
     long long wp_elems;
     PairBand Pb;
@@ -173,12 +158,9 @@ void launch_tx(hipStream_t s, const SchemeK& sk, const ChannelK& ch, int bits_sl
 bool txrx_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b);
 unsigned launch_rx_front(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, const double* pn,
                          uint64_t seed, uint64_t rep0, McBuffers& b);
-// qidx: a row-local (p_diag) scheme's decisions leave the stage as symbol
-// indices qe / qp ([ND][U]) for the index-based chains (k_pilot_pre / k_mic_fft /
-// k_pic_fft), pilot rows implicit (P xP), instead of the re-precoded v / u
 unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
                       int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
-                      bool perfect, bool qidx = false);
+                      bool perfect);
 // true when launch_stage uses the fused select-mode pass and the precoder is
 // row-local, so the perfect-CSI branch of IC iterations can ride on perfect_ic
 bool perfect_fusable(const Opts& op, const SchemeK& sk);
@@ -188,7 +170,7 @@ unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, cons
 // stage's detection in its epilogue (no y_est, no separate stage kernel).
 bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b);
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
-                      const double2* hp_prev, double2* hp_new, bool qidx = false);
+                      const double2* hp_prev, double2* hp_new);
 unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
                            int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
                            double2* hp_new, unsigned long long* counters, int scheme_index);
@@ -198,39 +180,22 @@ struct PerfectDetectArgs {
     int scheme, stage, nstage, nsnr, last;
     double sI, sQ;   // 1 / slicer step (I, Q)
 };
-// MMSE IC iteration `stage` of an OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v
-// by FFT with the stage in its epilogue (after k_pilot_pre formed hp_new)
-bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b);
-// the pilot pre-pass of that path: y_ic of the stage at the pilot rows -> hp_new
-// yic: also store y_ic of the pilot symbols (for k_mic_fft's pilot-symbol blocks)
-void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx, bool yic = false);
-// stage 0 (one-tap + detection of both branches) of such a scheme when both IC
-// chains are index-based: k_ls + k_stage0_fft, decisions into qe / qp
-unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
-                           bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd);
-// every MMSE stage (0..n_iter) of such a scheme: k_mic_pilot + k_mic_data (mic2);
+// Every MMSE stage (0..n_iter) of an FFT-form OFDM scheme: k_mic_pilot +
+// k_mic_data, y_ic = y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain;
 // the perfect-CSI branch then runs k_pic_fft with its stage 0
 bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
                     int niter);
 // part: 1 = k_mic_pilot, 2 = k_mic_data (the data kernel reads the pilot kernel's hpa)
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
                             const PerfectDetectArgs* pd, int niter, int xcd, int part);
-unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                         int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx = false,
-                         bool tapm = true, bool yic = false, double2* hp_next = nullptr);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in
 // registers (pic_ok schemes); perfect_chain_ok tells when it applies.
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
-// true when the chain is k_pic_fft (the only chain with index-based decisions)
-bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
-// qidx: u from the stage's decision indices (StageArgs::qidx; k_pic_fft only)
 // stage0: k_pic_fft also runs the perfect-CSI stage 0 (one-tap y ./ h) first
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter, bool qidx = false, bool stage0 = false);
+                              const PerfectDetectArgs* pd, int niter, bool stage0 = false);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);
 
 // setup (correlation matrices and MMSE estimator)

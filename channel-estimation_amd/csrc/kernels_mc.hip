@@ -971,9 +971,8 @@ struct StorePerfectDetect {
     // the chains' folded slicer (nearest_lin): f = z scale + offset, top = n - 1
     double scI, ofI, topI, scQ, ofQ, topQ;
     double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
-    uint16_t* qd;                      // QIDX chains: the branch's decisions, row-indexed [LK][U] (qre / qrp)
-    const double2* xp;                 // pilots [NP][R] (k_mic_fft PILOT mode: the LS division)
-    const double2* xs;                 // precoded symbols P [xP; xD] [LK][R] (QIDX: the pilot rows of v / u)
+    const double2* xp;                 // pilots [NP][R] (k_mic_pilot: the LS division)
+    const double2* xs;                 // precoded symbols P [xP; xD] [LK][R] (the constant rows of v / u)
     const uint16_t* sidr;              // transmitted symbol index per data row [LK][R]
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
@@ -1319,22 +1318,6 @@ __device__ __forceinline__ int nearest_lin(double x, double scale, double offset
     return (int)c;
 }
 
-// Index-based decisions (QIDX chains, StageArgs::qidx): the decisions live
-// row-indexed, qd[row][U] = symbol index of a data row, so a chain reads them
-// with no table lookup in front (row r of v = P [xP; Q(x)] is row_pval[r] *
-// symbols[qd[r]] for a data row of a row-local precoder); pilot rows are the
-// realisation's constant precoded pilots xs[row][R].  Transmitted indices come
-// row-indexed too (sidr, written by k_tx_symbols).
-__device__ __forceinline__ double2 qidx_value(bool data, unsigned q, double2 pv, const double2* sym,
-                                              const double2* __restrict__ xs, size_t xs_i) {
-    if (data) {
-        double2 v = make_double2(0.0, 0.0);
-        c_fma(v, pv, sym[q]);
-        return v;
-    }
-    return xs[xs_i];
-}
-
 // Error counts of a 256-thread block, one atomic per counter per block: every
 // wave packs its totals (errors | no-edge errors << 16, per CSI branch) and
 // wave 0 sums the four waves' words from LDS.  `words` = 1 or 2 branches.
@@ -1455,7 +1438,7 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // perfect-CSI branch, the one-tap x = y ./ h (script:450-466), so no stage
 // kernel runs in front: u starts as P [xP; 0] (xs of the pilot rows) and the
 // data rows get the stage-0 decisions in registers.
-template <int NT, int SH, bool TRACE, bool QIDX, bool S0 = false>
+template <int NT, int SH, bool TRACE, bool S0 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     int ug, blk;
@@ -1475,7 +1458,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
     // and the channel taps of the lane's samples (registers for all iterations)
     double2 u[6], yh[6], hc[6];
-    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
+    unsigned txp[2] = {0u, 0u};
     double2 taps[6][NT];
     const __amdgpu_buffer_rsrc_t trs =
         buf_rsrc(ir + (size_t)klo * R, ((size_t)(NT - 1) * N + (N - klo)) * R * sizeof(double2));
@@ -1496,7 +1479,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         for (int b = 0; b < 6; ++b) {
             const int row = row0 + 4 * b + r;
             if (S0) u[b] = o.xs[(size_t)row * R + rl];
-            else if (QIDX) qv[b] = o.qd[(size_t)row * U + unit];
             else u[b] = o.u[(size_t)row * U + unit];
             txp[b >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (b & 3));
             yh[b] = o.y[(size_t)row * U + unit];
@@ -1529,11 +1511,6 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
-    if (QIDX && !S0)
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-            u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
-                              (size_t)(row0 + 4 * a + r) * R + rl);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     int ncnt = 0;
     if (S0) {
@@ -1694,7 +1671,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
 }
 
 // ---------------------------------------------------------------------------
-// The MMSE IC iteration of OFDM in structured form (k_mic_fft, rows a13-a16).
+// The MMSE IC iteration of OFDM in structured form (rows a13-a16; k_mic_pilot / k_mic_data below).
 // The estimate D_hat = reshape(W hP), W = R_Dij,hP pinv(R) (script:259-313,
 // :493-511), is Q' H_hat G: column p of R_Dij,hP is vec(Q' M_p G) with
 // M_p = reshape(R_vecH x_p) (script:260), so D_hat = Q' (sum_p M_p z_p) G with
@@ -1711,591 +1688,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
 // window: the previous stage's from its taps, this stage's from Bs (window sums
 // of Bv) and hP_new.  Per unit and symbol: NT x 24 x NP CMACs for the taps
 // instead of the contraction's 24 x 23 x NP.
-// Lane quad = unit (k_pic_fft's layout): lane r forms the estimated taps of its
-// six window samples from the symbol's Bv rows (staged in LDS once per block,
-// broadcast to the 16 quads of a wave) and the unit's hP (registers), then
-// one iteration of the DFT-24 chain, one-tap with diag(D_hat_new), slicer,
-// counts, decisions written over v.  (A first version formed the taps lane =
-// unit with Bv through scalar loads and parked them in LDS: 3.8 ms per launch,
-// 65 % of wave time waiting on the serial s_load chain.)
-// Block = 256 threads = 64 units of one symbol; SNR-fastest XCD-aware order.
 // ---------------------------------------------------------------------------
-struct MicArgs {
-    const double2* __restrict__ bv;       // [var][snr][NT][N][NP]
-    const double2* __restrict__ bs;       // [var][snr][nblk][NT][NP]
-    const double2* __restrict__ hp_prev;  // [NP][U]: the previous stage's LS pilots (its D_hat)
-    const double2* __restrict__ hp_new;   // [NP][U]: this stage's (k_pilot_pre)
-    double2* v;                           // [LK][U]: P [xP; Q(x_est)], in / out
-    double* mse_err;
-    double* mse_pow;
-    int var_prev, var_cur, nsnr, N, nblk, stage, nstage, last, scheme;
-    // PILOT mode (k_pilot_fft): the symbol blocks holding pilots, and this
-    // stage's LS pilot estimates y_ic(pilots) ./ xP / sqrt(kappa) out
-    const int* pblk;
-    int npb;
-    double2* hp_out;
-    // y_ic of the pilot symbols handed from the pilot pass to k_mic_fft (yic):
-    // the pass stores it, the main pass's pilot-symbol blocks load it instead
-    // of forming it again (same taps, same decisions, same chain)
-    double2* yest;                        // [LK][U]
-    const int* pmask;                     // [nblk]: 1 = the block holds pilot rows
-    int yic;
-    // the next iteration's pilot pass fused into the main pass (fuse, yic blocks
-    // only): once a pilot-symbol block has its decisions, it forms the next
-    // iteration's y_ic of the symbol with the taps Bv(var_cur) hp_new, stores it
-    // over yest and the LS pilots into hp_next (a third buffer: other blocks of
-    // this launch still read hp_prev)
-    double2* hp_next;                     // [NP][U]
-    int fuse;
-};
-
-template <int NT, int SH, int NP, bool TRACE, bool QIDX, bool TAPM, bool PILOT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-k_mic_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o) {
-    int ug, blk;
-    band_block(ord, PILOT ? ma.npb : sk.QH.nblk, ug, blk);
-    if (PILOT) blk = ma.pblk[blk];
-    // block-uniform: this pilot-symbol block's y_ic comes from the pilot pass
-    const bool yic = !PILOT && ma.yic && ma.pmask[blk];
-    // block-uniform: this pilot-symbol block also runs the next iteration's
-    // pilot pass (its sbv / hhs then hold Bv(var_cur) and the taps of hp_new:
-    // the y_ic epilogue of this iteration reads neither)
-    const bool fz = TAPM && !PILOT && yic && ma.fuse;
-    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int U = o.U, R = o.R;
-    const int snr = o.snr0 + (ug * WAVE) / R;
-    const int ul = w * 16 + (l >> 2);                           // phase-B unit of this lane quad
-    const int unit = ug * WAVE + ul;
-    const int rl = unit % R;
-    const int cq = (r >> 1) + 2 * (r & 1);                     // time quarter of this lane
-    const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
-    constexpr int BVS = NP + 1;                                 // padded sample stride: the quad's 4 rows in distinct banks
-    __shared__ double2 sbv[NT][24][BVS];                        // Bv of the symbol's window samples (previous stage's var)
-    __shared__ double2 sbs[NT][NP];                             // Bs of the symbol (this stage's var)
-    __shared__ int rpc[PILOT ? 1 : 24];                         // pilot column of the block's rows (fz)
-    __shared__ double2 sym[256];
-    __shared__ int sgrid[256];
-    __shared__ double2 rpv[24];
-    __shared__ int rdc[24];
-    __shared__ double2 wrow[24];                                // qs gs w^(-l): diag(D_hat) weight of a delayed tap
-    __shared__ double2 twa[2][4][6];
-    // per-unit operands (the rows' v and y, the previous stage's pilots, all NP,
-    // shared by the quad, and a quarter of this stage's: lane r holds pilots
-    // 4r..4r+3 of the window sums), requested after the table / operator loads
-    // and before the first LDS write: the LDS writes then wait only for the
-    // tables (vmcnt retires in order; the flat pointers keep the compiler from
-    // moving these loads above the LDS stores itself)
-    double2 u[6], yv[6], hq[TAPM ? 1 : NP], hn4[NP / 4];
-    unsigned qv[QIDX ? 6 : 1], txp[2] = {0u, 0u};
-    // TAPM: the taps as an MFMA GEMM, A = Bv rows (tap row R = q 24 + j, 16 per
-    // tile), B = hP_prev (k = pilot, column = the wave's 16 units), 3M complex
-    // products; lane (g = l >> 4, jc = l & 15) holds B[4 ks + g][unit jc]
-    constexpr int NTILE = (NT * 24 + 15) / 16, NKS = NP / 4;
-    double br[TAPM ? NKS : 1], bi[TAPM ? NKS : 1], bsm[TAPM ? NKS : 1];
-    double2 hb[TAPM ? NKS : 1];
-    // PILOT: pilot column of the lane's rows (prologue) and the transmitted
-    // pilot of each (requested with y, clamped, unconditional): the LS
-    // division in the epilogue then waits on no dependent load
-    int pcv[PILOT ? 6 : 1];
-    double2 xpv[PILOT ? 6 : 1];
-    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    {
-        // every global load of the prologue before the first LDS write (clamped)
-        const double2 sa = o.symbols[min(tid, o.M - 1)];
-        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
-        const int rt = min(tid, 23);
-        const double2 pv = o.row_pval[row0 + rt];
-        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
-        const int pcr = PILOT ? 0 : sk.row_pcol[row0 + rt];
-        // twiddles (a lane-varying index into the constant table is a vector
-        // load: issued here, with the tables, not behind the per-unit loads)
-        const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);
-        const double2 tw = kW24[e % 12];
-        const int lr0 = min(max(tid - 64, 0), 23);
-        const double2 t0 = kW24[lr0 % 12];
-        // the operator slices: Bv rows klo..klo+23 of every tap (NT x 24 x NP,
-        // contiguous per tap) and Bs of the block (loaded unconditionally: a
-        // branch around the array loads sent it through scratch)
-        constexpr int NBV = NT * 24 * NP, PER = (NBV + 255) / 256;
-        const double2* __restrict__ bvb =
-            ma.bv + ((size_t)((fz ? ma.var_cur : ma.var_prev) * ma.nsnr + snr) * NT * ma.N + klo) * NP;
-        double2 bvr[PER];
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int i = min(tid + 256 * k, NBV - 1), q = i / (24 * NP), rem = i % (24 * NP);
-                bvr[k] = bvb[(size_t)q * ma.N * NP + rem];
-            }
-        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
-        if (TAPM && (!yic || fz)) {
-            const double2* __restrict__ hpb = fz ? ma.hp_new : ma.hp_prev;
-    #pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                hb[ks] = hpb[(size_t)(4 * ks + (l >> 4)) * U + ug * WAVE + w * 16 + (l & 15)];
-            }
-        }
-    #pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            if (!yic) {
-                if (QIDX) qv[a] = o.qd[(size_t)row * U + unit];
-                else u[a] = ma.v[(size_t)row * U + unit];
-            }
-            if (PILOT) pcv[a] = sk.row_pcol[row];
-        }
-        if (!TAPM && !yic)
-    #pragma unroll
-            for (int p = 0; p < NP; ++p) hq[p] = ma.hp_prev[(size_t)p * U + unit];
-        if (!PILOT)
-    #pragma unroll
-            for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
-        sym[tid] = make_double2(tid < o.M ? sa.x : 0.0, tid < o.M ? sa.y : 0.0);
-        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
-        rpv[rt] = pv;                                           // unconditional, clamped (see k_pic_fft)
-        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
-        if (!PILOT) rpc[rt] = pcr;
-        // unconditional (yic blocks do not read sbv): under `if (!yic)` the
-        // compiler sinks the bvr loads next to these writes, behind a vmcnt(0)
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = min(tid + 256 * k, NBV - 1);
-            sbv[i / (24 * NP)][(i / NP) % 24][i % NP] = bvr[k];
-        }
-        {
-            const int ib = min(tid, NT * NP - 1);
-            sbs[ib / NP][ib % NP] = bsv;
-            const int tc = min(tid, 47), dir = tc / 24;
-            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-            twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-            const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            wrow[lr0] = c_mul(scale, make_double2(wl.x, -wl.y));
-        }
-    }
-    __syncthreads();
-    // data / no-edge masks of the lane's rows
-    unsigned dmask = 0u, emask = 0u;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int dc = rdc[4 * a + r];
-        dmask |= dc >= 0 ? 1u << a : 0u;
-        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
-    }
-    if (QIDX && !yic)
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-            u[a] = qidx_value((dmask >> a) & 1, qv[a], rpv[4 * a + r], sym, o.xs,
-                              (size_t)(row0 + 4 * a + r) * R + rl);
-    // the estimated taps of the lane's samples 6 cq + m and the window sums S_q
-    // of both stages.  TAPM: the MFMA GEMM's D tiles (row 16 t + g + 4 reg, unit
-    // jc) go through the wave's own LDS slab into the quad layout; otherwise
-    // each lane forms its 12 taps on the VALU (Bv rows broadcast from LDS)
-    __shared__ double2 hhs[TAPM ? 4 : 1][TAPM ? NTILE * 16 : 1][17];
-    if (TAPM && (!yic || fz)) {
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            br[ks] = hb[ks].x;
-            bi[ks] = hb[ks].y;
-            bsm[ks] = hb[ks].x + hb[ks].y;
-        }
-        const int g = l >> 4, jc = l & 15;
-        const int R = jc;                                   // A row of this lane within a tile
-#pragma unroll
-        for (int t = 0; t < NTILE; ++t) {
-            const int Rt = 16 * t + R;
-            const bool okr = Rt < NT * 24;
-            const int q = okr ? Rt / 24 : 0, jj = okr ? Rt % 24 : 0;
-            d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-                const double2 a = sbv[q][jj][4 * ks + g];
-                const double ar = okr ? a.x : 0.0, ai = okr ? a.y : 0.0;
-                p1 = MFMA64(ar, br[ks], p1);
-                p2 = MFMA64(ai, bi[ks], p2);
-                p3 = MFMA64(ar + ai, bsm[ks], p3);
-            }
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg)
-                hhs[w][16 * t + g + 4 * reg][jc] = make_double2(p1[reg] - p2[reg], p3[reg] - p1[reg] - p2[reg]);
-        }
-        // the slab is the wave's own: a wave-level fence, no block barrier
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    // y (or y_ic) and the transmitted indices are first needed in the epilogue:
-    // requested here, their latency runs under the tap assembly and the DFT
-    // chain (in the prologue they held 26 more registers at its peak)
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int row = row0 + 4 * a + r;
-        if (!PILOT) txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        yv[a] = (yic ? ma.yest : o.y)[(size_t)row * U + unit];   // yic: y_ic itself
-        if (PILOT) xpv[a] = o.xp[(size_t)min(max(pcv[a], 0), NP - 1) * R + rl];
-    }
-    double2 taps[6][NT];
-    double2 sp0 = make_double2(0.0, 0.0), sp1 = sp0, sn0 = sp0, sn1 = sp0;
-#pragma unroll
-    for (int q = 0; q < NT; ++q) {
-        double2 s = make_double2(0.0, 0.0);
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-            if (TAPM) {
-                taps[m][q] = hhs[w][q * 24 + 6 * cq + m][l >> 2];
-            } else {
-                const double2* bq = sbv[q][6 * cq + m];
-                double2 acc0 = make_double2(0.0, 0.0), acc1 = acc0;
-#pragma unroll
-                for (int p = 0; p < NP; p += 2) {
-                    c_fma(acc0, bq[p], hq[p]);
-                    c_fma(acc1, bq[p + 1], hq[p + 1]);
-                }
-                taps[m][q] = c_add(acc0, acc1);
-            }
-            s = c_add(s, taps[m][q]);
-        }
-        double2 sq = make_double2(0.0, 0.0);
-        if (!PILOT)
-#pragma unroll
-            for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
-        s = c_add(s, dpp_c<QP_XOR1>(s));
-        s = c_add(s, dpp_c<QP_XOR2>(s));
-        sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-        sq = c_add(sq, dpp_c<QP_XOR2>(sq));
-        if ((SH >> q) & 1) {
-            sp1 = c_add(sp1, s);
-            sn1 = c_add(sn1, sq);
-        } else {
-            sp0 = c_add(sp0, s);
-            sn0 = c_add(sn0, sq);
-        }
-    }
-    sp0 = c_mul(scale, sp0);
-    sn0 = c_mul(scale, sn0);
-    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
-    // ---- phase B: acc = Q' H_hat G u for the symbol (k_pic_fft's chain); a yic
-    // block has y_ic already
-    // x <- Q' (H_hat (G x)) of the symbol for the taps tp (k_pic_fft's chain)
-    auto chain = [&](double2 (&xx)[6], const double2 (&tp)[6][NT]) {
-        dft6<1>(xx);
-        double2 t[6];
-    #pragma unroll
-        for (int m = 0; m < 6; ++m) {
-            const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
-            const double2 pv = dpp_c<QP_XOR2>(p);
-            double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-            e = quad_tw<1>(e, r == 3);
-            const double2 qv = dpp_c<QP_XOR1>(e);
-            t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
-        }
-        const double2 tprev = dpp_c<QP_PREV>(t[5]);
-    #pragma unroll
-        for (int m = 5; m >= 0; --m) {
-            const double2 tq = m ? t[m - 1] : tprev;
-            double2 acc = make_double2(0.0, 0.0);
-    #pragma unroll
-            for (int q = 0; q < NT; ++q) c_fma(acc, tp[m][q], ((SH >> q) & 1) ? tq : t[m]);
-            t[m] = acc;
-        }
-    #pragma unroll
-        for (int m = 0; m < 6; ++m) {
-            const double2 pv = dpp_c<QP_XOR1>(t[m]);
-            double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-            f = quad_tw<-1>(f, r == 3);
-            const double2 qv = dpp_c<QP_XOR2>(f);
-            xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
-        }
-        dft6<-1>(xx);
-    };
-    double2 x[6];
-    if (!yic) {
-    #pragma unroll
-        for (int a = 0; a < 6; ++a) x[a] = u[a];
-        chain(x, taps);
-    }
-    if constexpr (PILOT) {
-        // the next stage's LS pilot estimates (script:487-489) at the block's pilot rows
-        // (and, for k_mic_fft's yic blocks, y_ic of every row of the symbol)
-        const double sqk = 1.0 / sk.inv_sqrt_kappa;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            const int pc = pcv[a];
-            double2 ye = c_sub(yv[a], x[p6(a)]);
-            double2 hpv = sp0;
-            c_fma(hpv, wrow[4 * a + r], sp1);
-            c_fma(ye, hpv, u[a]);
-            if (ma.yic) ma.yest[(size_t)row * U + unit] = ye;
-            if (pc >= 0 && pc < NP) {
-                const double2 q = c_div(ye, xpv[a]);
-                ma.hp_out[(size_t)pc * U + unit] = make_double2(q.x / sqk, q.y / sqk);
-            }
-        }
-        return;
-    }
-    // ---- epilogue per row 4a + r: y_ic = y - acc + diag(D_hat_prev) u, one-tap
-    // with diag(D_hat_new), slicer, counts, re-precoded decision into v
-    int code[6], dp[6];
-    int anytie = 0;
-    double me = 0.0;
-    double2 hn[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int lr = 4 * a + r;
-        const double2 wl = wrow[lr];
-        double2 hpv = sp0, hnv = sn0;
-        c_fma(hpv, wl, sp1);
-        c_fma(hnv, wl, sn1);
-        hn[a] = hnv;
-        double2 ye = yv[a];
-        if (!yic) {
-            ye = c_sub(yv[a], x[p6(a)]);
-            c_fma(ye, hpv, u[a]);
-        }
-        const double2 z = c_div1(ye, hnv);
-        int tI, tQ;
-        const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
-        const int iQ = nearest_lin(z.y, o.scQ, o.ofQ, o.topQ, tQ);
-        code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
-        anytie |= tI | tQ;
-        dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
-        if (TRACE && unit == o.tr->unit) {
-            const int row = row0 + lr;
-            o.tr->yest[(size_t)ma.stage * o.tr->LK + row] = ye;
-            o.tr->hest[(size_t)ma.stage * o.tr->LK + row] = hnv;
-        }
-    }
-    // fz: y as received and the transmitted pilots of the next iteration's
-    // pilot pass, requested as soon as y_ic is consumed (their latency runs
-    // under the tie handling, the counts and the decision stores)
-    double2 xq[6];
-    int pc[6];
-    if (fz) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            pc[a] = rpc[4 * a + r];
-            yv[a] = o.y[(size_t)row * U + unit];
-            xq[a] = o.xp[(size_t)min(max(pc[a], 0), NP - 1) * R + rl];
-        }
-    }
-    if (ma.mse_err) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const double2 hv = o.h[(size_t)(row0 + 4 * a + r) * R + rl];
-            const double dx = hn[a].x - hv.x, dy = hn[a].y - hv.y;
-            me += dx * dx + dy * dy;
-        }
-    }
-    if (__ballot(anytie)) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
-            const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
-            dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
-                        min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
-        }
-    }
-    int ncnt = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const bool data = (dmask >> a) & 1;
-        const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
-        ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
-        if (TRACE && data && unit == o.tr->unit) o.tr->dec_e[(size_t)ma.stage * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
-        if (!ma.last && data) {
-            if (QIDX) {
-                o.qd[(size_t)(row0 + 4 * a + r) * U + unit] = (uint16_t)dp[a];
-            } else {
-                double2 nv = make_double2(0.0, 0.0);
-                c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
-                ma.v[(size_t)(row0 + 4 * a + r) * U + unit] = nv;
-            }
-        }
-    }
-    {
-        __shared__ int bcnt[8];
-        const int pk[2] = {ncnt, 0};
-        block_counts(pk, 1, bcnt, o.counters, o.cidx0 + (size_t)ma.stage + (size_t)snr * o.cstride_snr,
-                     (size_t)o.cstride_edge, 0, rl < o.rvalid);
-    }
-    if (ma.mse_err)
-        flush_mse(me, 0.0, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, ma.stage, rl < o.rvalid);
-    if (fz) {
-        // the next iteration's pilot pass (PILOT mode above) on this symbol:
-        // u = this iteration's decisions, taps Bv(var_cur) hp_new from the
-        // wave's slab, sp0 / sp1 their window sums (formed above), y as received
-        const double sqk = 1.0 / sk.inv_sqrt_kappa;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            u[a] = qidx_value((dmask >> a) & 1, (unsigned)dp[a], rpv[4 * a + r], sym, o.xs, (size_t)row * R + rl);
-        }
-#pragma unroll
-        for (int q = 0; q < NT; ++q)
-#pragma unroll
-            for (int m = 0; m < 6; ++m) taps[m][q] = hhs[w][q * 24 + 6 * cq + m][l >> 2];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) x[a] = u[a];
-        chain(x, taps);
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            double2 ye = c_sub(yv[a], x[p6(a)]);
-            double2 hpv = sp0;
-            c_fma(hpv, wrow[4 * a + r], sp1);
-            c_fma(ye, hpv, u[a]);
-            ma.yest[(size_t)row * U + unit] = ye;
-            if (pc[a] >= 0 && pc[a] < NP) {
-                const double2 qq = c_div(ye, xq[a]);
-                ma.hp_next[(size_t)pc[a] * U + unit] = make_double2(qq.x / sqk, qq.y / sqk);
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Stage 0 of an FFT-form OFDM scheme on the index-based chains (k_stage0_fft):
-// one-tap + detection of both branches (script:428-466) for 64 units x one
-// symbol in k_mic_fft's layout.  diag(D_hat_0) = qs gs sum_q w^(-l d_q) S_q with
-// S_q = Bs hP_0 (the structured diagonal, equal to Wd hP_0 to rounding, checked
-// by build_mic), so the stage reads y, h and a quarter of hP per lane and
-// writes the decision indices qe / qp (pilot rows stay implicit).  MSE sums
-// |h_hat - h|^2 and |h|^2 at stage 0 when enabled.
-// ---------------------------------------------------------------------------
-template <int NT, int SH, int NP, bool TRACE>
-__global__ void __launch_bounds__(256) k_stage0_fft(SchemeK sk, BandOrder ord, MicArgs ma, StorePerfectDetect o,
-                                                    uint16_t* __restrict__ qp, unsigned long long* __restrict__ counters) {
-    int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
-    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int U = o.U, R = o.R;
-    const int snr = o.snr0 + (ug * WAVE) / R;
-    const int unit = ug * WAVE + w * 16 + (l >> 2);
-    const int rl = unit % R;
-    const int row0 = sk.QH.row0[blk];
-    __shared__ double2 sbs[NT][NP];
-    __shared__ int sgrid[256];
-    __shared__ int rdc[24];
-    __shared__ double2 wrow[24];
-    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    double2 yv[6], hv[6], hn4[NP / 4];
-    unsigned txp[2] = {0u, 0u};
-    {
-        // table loads, then the per-unit loads, then the LDS writes: the writes
-        // wait only for the tables (vmcnt retires in order)
-        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
-        const int rt = min(tid, 23);
-        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
-        const double2 bsv = ma.bs[(((size_t)(ma.var_cur * ma.nsnr + snr) * ma.nblk + blk) * NT) * NP + min(tid, NT * NP - 1)];
-        const int lr0 = min(max(tid - 64, 0), 23);
-        const double2 t0 = kW24[lr0 % 12];
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int row = row0 + 4 * a + r;
-            yv[a] = o.y[(size_t)row * U + unit];
-            hv[a] = o.h[(size_t)row * R + rl];
-            txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
-        }
-#pragma unroll
-        for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hp_new[(size_t)(r * (NP / 4) + k) * U + unit];
-        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
-        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;     // unconditional, clamped (see k_pic_fft)
-        {
-            const int ib = min(tid, NT * NP - 1);
-            sbs[ib / NP][ib % NP] = bsv;
-            const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            wrow[lr0] = c_mul(scale, make_double2(wl.x, -wl.y));
-        }
-    }
-    __syncthreads();
-    unsigned dmask = 0u, emask = 0u;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int dc = rdc[4 * a + r];
-        dmask |= dc >= 0 ? 1u << a : 0u;
-        emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
-    }
-    double2 sn0 = make_double2(0.0, 0.0), sn1 = sn0;
-#pragma unroll
-    for (int q = 0; q < NT; ++q) {
-        double2 sq = make_double2(0.0, 0.0);
-#pragma unroll
-        for (int k = 0; k < NP / 4; ++k) c_fma(sq, sbs[q][r * (NP / 4) + k], hn4[k]);
-        sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-        sq = c_add(sq, dpp_c<QP_XOR2>(sq));
-        if ((SH >> q) & 1) sn1 = c_add(sn1, sq);
-        else sn0 = c_add(sn0, sq);
-    }
-    sn0 = c_mul(scale, sn0);
-    // both branches: code = iI | iQ << 8 | tie flags << 16 (MMSE), << 18 (perfect)
-    int ce[6], cp[6], de[6], dq[6];
-    int anytie = 0;
-    double me = 0.0, mp = 0.0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const int lr = 4 * a + r;
-        double2 hd = sn0;
-        c_fma(hd, wrow[lr], sn1);
-        const double2 ze = c_div1(yv[a], hd), zp = c_div1(yv[a], hv[a]);
-        int t0, t1, t2, t3;
-        const int iI = nearest_lin(ze.x, o.scI, o.ofI, o.topI, t0), iQ = nearest_lin(ze.y, o.scQ, o.ofQ, o.topQ, t1);
-        const int jI = nearest_lin(zp.x, o.scI, o.ofI, o.topI, t2), jQ = nearest_lin(zp.y, o.scQ, o.ofQ, o.topQ, t3);
-        ce[a] = iI | (iQ << 8) | (t0 << 16) | (t1 << 17);
-        cp[a] = jI | (jQ << 8) | (t2 << 16) | (t3 << 17);
-        anytie |= t0 | t1 | t2 | t3;
-        de[a] = sgrid[__umul24(iI, o.nQ) + iQ];
-        dq[a] = sgrid[__umul24(jI, o.nQ) + jQ];
-        if (ma.mse_err) {
-            const double dx = hd.x - hv[a].x, dy = hd.y - hv[a].y;
-            me += dx * dx + dy * dy;
-            mp += hv[a].x * hv[a].x + hv[a].y * hv[a].y;
-        }
-        if (TRACE && unit == o.tr->unit) o.tr->hest[row0 + lr] = hd;
-    }
-    if (__ballot(anytie)) {
-        auto tie = [&](int code) {
-            const int iI = code & 0xff, iQ = (code >> 8) & 0xff;
-            const int jI = max(iI - ((code >> 16) & 1), 0), jQ = max(iQ - ((code >> 17) & 1), 0);
-            return min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
-                       min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
-        };
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            de[a] = tie(ce[a]);
-            dq[a] = tie(cp[a]);
-        }
-    }
-    int cnt[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const bool data = (dmask >> a) & 1, ne = (emask >> a) & 1;
-        const int tx = (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu);
-        const int ee = data ? __popc((unsigned)(de[a] ^ tx)) : 0, ep = data ? __popc((unsigned)(dq[a] ^ tx)) : 0;
-        cnt[0] += ee;
-        cnt[1] += ne ? ee : 0;
-        cnt[2] += ep;
-        cnt[3] += ne ? ep : 0;
-        const int d = rdc[4 * a + r] >> 1;
-        if (TRACE && data && unit == o.tr->unit) {
-            o.tr->dec_e[d] = de[a];
-            o.tr->dec_p[d] = dq[a];
-        }
-        if (!ma.last && data) {
-            const size_t qi = (size_t)(row0 + 4 * a + r) * U + unit;
-            o.qd[qi] = (uint16_t)de[a];
-            qp[qi] = (uint16_t)dq[a];
-        }
-    }
-    {
-        __shared__ int bcnt[8];
-        const int pk[2] = {cnt[0] | (cnt[1] << 16), cnt[2] | (cnt[3] << 16)};
-        block_counts(pk, 2, bcnt, counters, (((size_t)ma.scheme * 4) * ma.nsnr + snr) * ma.nstage,
-                     (size_t)ma.nsnr * ma.nstage, 2 * (size_t)ma.nsnr * ma.nstage, rl < o.rvalid);
-    }
-    if (ma.mse_err) flush_mse(me, mp, ma.mse_err, ma.mse_pow, ma.scheme, ma.nsnr, snr, ma.nstage, 0, rl < o.rvalid);
-}
-
 
 // ---------------------------------------------------------------------------
 // The MMSE branch of an FFT-form OFDM scheme with EVERY stage in one launch
@@ -2994,16 +2387,12 @@ static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, co
     return sk.pf_ok && op.pic_chain == 3 && pic_fft_shift(ch) >= 0 && fits && niter >= 1 && niter <= PM_MAXIT;
 }
 
-bool perfect_chain_fft(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
-    return pic_fft_ok(op, sk, ch, b, niter);
-}
-
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
     return pic_fft_ok(op, sk, ch, b, niter);
 }
 
-// Detection operands of the chain kernels (k_pic_fft / k_mic_fft /
-// k_stage0_fft): tables, slicer folded for nearest_lin, counters of branch `csi`
+// Detection operands of the chain kernels (k_pic_fft / k_mic_pilot /
+// k_mic_data): tables, slicer folded for nearest_lin, counters of branch `csi`
 // (0 MMSE, 1 perfect CSI; the stage is added per iteration).
 static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, const PerfectDetectArgs* pd, int csi) {
     StorePerfectDetect o{};
@@ -3034,7 +2423,6 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.idd = 1.0 / sk.data_div;
     o.sI = pd->sI;
     o.sQ = pd->sQ;
-    o.qd = csi ? b.qrp : b.qre;
     o.xp = b.xp;
     o.xs = b.xs;
     o.sidr = b.sidr;
@@ -3049,72 +2437,13 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     return o;
 }
 
-bool mmse_fft_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b) {
-    const bool fits = (long long)ch.ntap * ch.N * 16 < (1ll << 31) && (long long)sk.LK * b.U < (1ll << 62);
-    return op.mmse_ic == 1 && mm.Bv && mm.Bs && mm.Wpil && sk.pf_ok && sk.NP == 16 && pic_fft_shift(ch) >= 0 &&
-           (b.U % 64) == 0 && (b.R % 64) == 0 && fits;
-}
-
-unsigned launch_mmse_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                         int var_cur, int stage, int n_iter, bool last, McBuffers& b, const double2* hp_prev,
-                         const double2* hp_new, const PerfectDetectArgs* pd, int xcd, bool qidx, bool tapm,
-                         bool yic, double2* hp_next) {
-    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
-    MicArgs ma{};
-    ma.bv = mm.Bv;
-    ma.bs = mm.Bs;
-    ma.hp_prev = hp_prev;
-    ma.hp_new = hp_new;
-    ma.v = b.v;
-    ma.mse_err = b.mse_err;
-    ma.mse_pow = b.mse_pow;
-    ma.var_prev = var_prev;
-    ma.var_cur = var_cur;
-    ma.nsnr = mm.nsnr;
-    ma.N = ch.N;
-    ma.nblk = sk.QH.nblk;
-    ma.stage = stage;
-    ma.nstage = n_iter + 1;
-    ma.last = last ? 1 : 0;
-    ma.scheme = pd->scheme;
-    ma.yest = b.yest;
-    ma.pmask = mm.pmask;
-    ma.yic = yic && mm.pmask ? 1 : 0;
-    ma.hp_next = hp_next;
-    ma.fuse = hp_next && ma.yic && tapm && !last ? 1 : 0;
-    const unsigned pf = ma.fuse ? PATH_PILOT_FUSED : 0u;
-    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
-    const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_MIC3(NTV, SHV, TM)                                                                                     \
-    do {                                                                                                              \
-        if (b.tr && qidx)                                                                                             \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, true, TM, false>), grid, blk, 0, s, sk, om, ma, o);     \
-        else if (b.tr)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, true, false, TM, false>), grid, blk, 0, s, sk, om, ma, o);    \
-        else if (qidx)                                                                                                \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, TM, false>), grid, blk, 0, s, sk, om, ma, o);    \
-        else                                                                                                          \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, TM, false>), grid, blk, 0, s, sk, om, ma, o);   \
-    } while (0)
-#define LAUNCH_MIC(NTV, SHV)                                                                                          \
-    do {                                                                                                              \
-        if (tapm) LAUNCH_MIC3(NTV, SHV, true);                                                                        \
-        else LAUNCH_MIC3(NTV, SHV, false);                                                                            \
-    } while (0)
-    const int sh = pic_fft_shift(ch);
-    if (ch.ntap == 1) LAUNCH_MIC(1, 0);
-    else if (sh == 1) LAUNCH_MIC(2, 1);
-    else LAUNCH_MIC(2, 2);
-#undef LAUNCH_MIC
-#undef LAUNCH_MIC3
-    return PATH_MIC_FFT | pf;
-}
-
 // Every stage of the MMSE branch of an FFT-form OFDM scheme (k_mic_pilot over the
 // pilot symbols, then k_mic_data over the others; see Mic2Args).
 bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
                     int niter) {
-    return op.mic2 && mmse_fft_ok(op, sk, mm, ch, b) && mm.npb >= 1 && mm.npb <= 4 && mm.ndb >= 1 && b.hpa &&
+    const bool fits = (long long)ch.ntap * ch.N * 16 < (1ll << 31) && (long long)sk.LK * b.U < (1ll << 62);
+    return op.mmse_ic == 1 && mm.Bv && mm.Bs && sk.pf_ok && sk.NP == 16 && pic_fft_shift(ch) >= 0 &&
+           (b.U % 64) == 0 && (b.R % 64) == 0 && fits && mm.npb >= 1 && mm.npb <= 4 && mm.ndb >= 1 && b.hpa &&
            niter >= 1 && niter <= PM_MAXIT && b.hpa_stages >= niter + 1 && op.pic_chain == 3 &&
            pic_fft_ok(op, sk, ch, b, niter) && (long long)(niter + 1) * sk.NP * b.U < (1ll << 40);
 }
@@ -3167,91 +2496,34 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     return PATH_MIC_FFT | PATH_MIC_STAGES;
 }
 
-// The pilot pre-pass of the structured MMSE IC (k_mic_fft in PILOT mode): y_ic of
-// IC iteration `stage` at the pilot rows only (script:482-489) -> hp_new, over
-// the symbol blocks that hold pilots (4 of 14 at C2); MFMA taps, no detection.
-void launch_pilot_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int var_prev,
-                      McBuffers& b, const double2* hp_prev, double2* hp_new, int xcd, bool qidx, bool yic) {
-    PerfectDetectArgs pd{};
-    StorePerfectDetect o = chain_detect(sk, b, &pd, 0);
-    MicArgs ma{};
-    ma.bv = mm.Bv;
-    ma.bs = mm.Bs;
-    ma.hp_prev = hp_prev;
-    ma.hp_out = hp_new;
-    ma.v = b.v;
-    ma.var_prev = var_prev;
-    ma.nsnr = mm.nsnr;
-    ma.N = ch.N;
-    ma.nblk = sk.QH.nblk;
-    ma.pblk = mm.pblk;
-    ma.npb = mm.npb;
-    ma.yest = b.yest;
-    ma.yic = yic ? 1 : 0;
-    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
-    const dim3 grid((b.U / WAVE) * mm.npb), blk(256);
-#define LAUNCH_PIL(NTV, SHV)                                                                                          \
-    do {                                                                                                              \
-        if (qidx)                                                                                                     \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, true, true, true>), grid, blk, 0, s, sk, om, ma, o);   \
-        else                                                                                                          \
-            hipLaunchKernelGGL((k_mic_fft<NTV, SHV, 16, false, false, true, true>), grid, blk, 0, s, sk, om, ma, o);  \
+unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
+                              const PerfectDetectArgs* pd, int niter, bool stage0) {
+    if (!pic_fft_ok(op, sk, ch, b, niter))
+        throw std::logic_error("launch_perfect_chain: no chain kernel for this scheme (perfect_chain_ok is false)");
+    StorePerfectDetect o = chain_detect(sk, b, pd, 1);
+    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
+    const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
+    // stage0: the chain also runs stage 0 of the branch (with k_mic_pilot /
+    // k_mic_data); otherwise stage 0 came from the stage kernel (u in HBM)
+#define LAUNCH_PF(NTV, SHV, S0V)                                                                                  \
+    do {                                                                                                          \
+        if (b.tr)                                                                                                 \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);  \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+    } while (0)
+#define LAUNCH_PF2(NTV, SHV)                \
+    do {                                    \
+        if (stage0) LAUNCH_PF(NTV, SHV, true); \
+        else LAUNCH_PF(NTV, SHV, false);       \
     } while (0)
     const int sh = pic_fft_shift(ch);
-    if (ch.ntap == 1) LAUNCH_PIL(1, 0);
-    else if (sh == 1) LAUNCH_PIL(2, 1);
-    else LAUNCH_PIL(2, 2);
-#undef LAUNCH_PIL
-}
-
-unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
-                              const PerfectDetectArgs* pd, int niter, bool qidx, bool stage0) {
-    StorePerfectDetect o = chain_detect(sk, b, pd, 1);
-    qidx = qidx && pic_fft_ok(op, sk, ch, b, niter);
-    if (stage0) {
-        if (!pic_fft_ok(op, sk, ch, b, niter)) throw std::logic_error("launch_perfect_chain: stage 0 needs k_pic_fft");
-        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
-        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_PF0(NTV, SHV)                                                                                           \
-    do {                                                                                                               \
-        if (b.tr)                                                                                                      \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
-        else                                                                                                           \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o,      \
-                               niter);                                                                                 \
-    } while (0)
-        const int sh = pic_fft_shift(ch);
-        if (ch.ntap == 1) LAUNCH_PF0(1, 0);
-        else if (sh == 1) LAUNCH_PF0(2, 1);
-        else LAUNCH_PF0(2, 2);
-#undef LAUNCH_PF0
-        return PATH_PIC_FFT;
-    }
-    if (pic_fft_ok(op, sk, ch, b, niter)) {
-        o.pf_scale_re = sk.pf_scale.x;
-        o.pf_scale_im = sk.pf_scale.y;
-        const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
-        const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_PF(NTV, SHV)                                                                                      \
-    do {                                                                                                         \
-        if (b.tr && qidx)                                                                                        \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
-        else if (b.tr)                                                                                           \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);\
-        else if (qidx)                                                                                           \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, true>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);\
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, false>), grid, blk, 0, s, sk, om, b.ir, ch.N, o,      \
-                               niter);                                                                           \
-    } while (0)
-        const int sh = pic_fft_shift(ch);
-        if (ch.ntap == 1) LAUNCH_PF(1, 0);
-        else if (sh == 1) LAUNCH_PF(2, 1);
-        else LAUNCH_PF(2, 2);
+    if (ch.ntap == 1) LAUNCH_PF2(1, 0);
+    else if (sh == 1) LAUNCH_PF2(2, 1);
+    else LAUNCH_PF2(2, 2);
+#undef LAUNCH_PF2
 #undef LAUNCH_PF
-        return PATH_PIC_FFT;
-    }
-    throw std::logic_error("launch_perfect_chain: no chain kernel for this scheme (perfect_chain_ok is false)");
+    return PATH_PIC_FFT;
 }
 
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
@@ -3343,7 +2615,7 @@ __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* _
     }
 }
 
-// k_wpair: the same contraction regrouped so no MFMA row is padding.  With
+// The W contraction on the matrix cores (k_wpair3), regrouped so no MFMA row is padding.  With
 // D_hat[r,c] = sum_p W[(r,c),p] hP_p,  y_est[r] = y[r] - sum_c D_hat[r,c] v_c.
 // The first product is a GEMM with M = (row, column) pairs of the block (q = c*RBP
 // + r; 24 x 24 pairs of an OFDM symbol tile exactly into 16-pair tiles), K = NP
@@ -3354,98 +2626,9 @@ __global__ void __launch_bounds__(64) k_wcontract_valu(Band Wb, const double2* _
 // periods (RBP 24: 3 tiles = 2 columns, RBP 32: 2 tiles = 1 column) so pair ->
 // (column, row) is compile-time.  Wave = 16 units, block = 4 waves = 64 units of
 // one SNR point; grid (U/64, nblk).
-template <int RBP, int NKS>
-__global__ void __launch_bounds__(256) k_wpair(PairBand P, const double2* __restrict__ Wall, long long wp_elems,
-                                               int var, int nsnr, int snr0, int R, int U,
-                                               const double2* __restrict__ hp, const double2* __restrict__ v,
-                                               const double2* __restrict__ y, double2* __restrict__ yest) {
-    constexpr int PER = RBP == 24 ? 3 : 2;           // tiles per period
-    constexpr int CPP = RBP == 24 ? 2 : 1;           // columns per period
-    constexpr int NACC = RBP / 4;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
-    const int unit = blockIdx.x * 64 + wv * 16 + j;
-    const int snr = snr0 + (blockIdx.x * 64) / R;
-    const int blk = blockIdx.y;
-    double2 hb[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) hb[ks] = hp[(size_t)(4 * ks + g) * U + unit];
-    const int clo = P.clo[blk], ntile = P.ntile[blk];
-    const double2* __restrict__ w = Wall + ((size_t)var * nsnr + snr) * (size_t)wp_elems + P.off[blk] + lane;
-    double2 acc[NACC];
-#pragma unroll
-    for (int k = 0; k < NACC; ++k) acc[k] = make_double2(0.0, 0.0);
-    const double2* __restrict__ vb = v + (size_t)clo * U + unit;
-    // one 16-pair tile: 4*NKS MFMAs, then the v epilogue of its 4 D rows (tile tt
-    // of a period; which column / accumulator each row feeds is compile-time)
-    auto tile = [&](const double2 (&aa)[NKS], const double2 (&vvv)[CPP], auto ttc) {
-        constexpr int tt = decltype(ttc)::value;
-        d4 re = {0, 0, 0, 0}, im = {0, 0, 0, 0};
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            re = MFMA64(aa[ks].x, hb[ks].x, re);
-            im = MFMA64(aa[ks].x, hb[ks].y, im);
-            re = MFMA64(-aa[ks].y, hb[ks].y, re);
-            im = MFMA64(aa[ks].y, hb[ks].x, im);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            constexpr int dummy = 0;
-            (void)dummy;
-            const int q0 = 16 * tt + 4 * i;                // pair offset in the period, less g
-            const int cc = q0 / RBP, rho = (q0 % RBP) / 4;
-            c_fma(acc[rho], make_double2(re[i], im[i]), vvv[cc]);
-        }
-    };
-    auto ldt = [&](int t, double2 (&aa)[NKS]) {
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) aa[ks] = w[((size_t)t * NKS + ks) * 64];
-    };
-    auto ldv = [&](int t0, double2 (&vvv)[CPP]) {
-#pragma unroll
-        for (int cc = 0; cc < CPP; ++cc) vvv[cc] = vb[(size_t)((t0 / PER) * CPP + cc) * U];
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    double2 A0[NKS], A1[NKS], vv[CPP];
-    // tile-level ping-pong: tile t+1's W loads are in flight during tile t's MFMAs
-    if (ntile > 0) ldt(0, A0);
-    for (int t0 = 0; t0 < ntile; t0 += PER) {
-        ldv(t0, vv);
-        const int tn = t0 + PER < ntile ? t0 + PER : t0;          // clamp: harmless reload at the end
-        if (PER == 3) {
-            // period of 3 tiles: A0 A1 A0, and the next period's first tile lands in A1 ->
-            // swap roles by reloading it into A0 after the last tile (one register copy)
-            ldt(t0 + 1, A1);
-            tile(A0, vv, I0{});
-            ldt(t0 + 2, A0);
-            tile(A1, vv, I1{});
-            ldt(tn, A1);
-            tile(A0, vv, I2{});
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) A0[ks] = A1[ks];
-        } else {
-            ldt(t0 + 1, A1);
-            tile(A0, vv, I0{});
-            ldt(tn, A0);
-            tile(A1, vv, I1{});
-        }
-    }
-    const int row0 = P.row0[blk], nrows = P.nrows[blk];
-#pragma unroll
-    for (int k = 0; k < NACC; ++k) {
-        const int r = g + 4 * k;
-        if (r < nrows) {
-            const size_t i = (size_t)(row0 + r) * U + unit;
-            yest[i] = c_sub(y[i], acc[k]);
-        }
-    }
-}
-
-// 3M (Gauss / Karatsuba) form of k_wpair: per k-step three real MFMAs
+// Complex products in 3M (Gauss / Karatsuba) form: per k-step three real MFMAs
 //   P1 += Wr hr,  P2 += Wi hi,  P3 += (Wr + Wi)(hr + hi);  Re = P1 - P2, Im = P3 - P1 - P2
-// instead of four (-25 % matrix-core work); W arrives as three 64-double planes
+// instead of four (-25 % matrix-core work; the r01 4-MFMA k_wpair was retired in r03); W arrives as three 64-double planes
 // per (tile, k-step) (k_wpair_pack3), hP as Re / Im / Re+Im registers.
 // Fused MMSE stage (FUSE, block-diagonal W, row-local P): after the
 // contraction the tile's rows go straight through the stage of IC iteration
@@ -3469,7 +2652,7 @@ struct FuseArgs {
     int rvalid;                    // realisations of the batch that count (McBuffers::rvalid)
 };
 
-template <int RBP, int NKS, bool FUSE, bool WDA_3M>
+template <int RBP, int NKS, bool FUSE>
 __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __restrict__ W3, long long wp_elems,
                                             int var, int nsnr, int snr0, int R, int U,
                                             const double2* __restrict__ hp, const double2* v,
@@ -3654,35 +2837,19 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
             hs[ks] = hv.x + hv.y;
         }
         const double2* __restrict__ wa = fa.WdA + (((size_t)fa.var * nsnr + snr) * P.nblk + blk) * 2 * NKS * 64 + lane;
-        if (WDA_3M) {
-            // 3M like the contraction: three real MFMAs per k-step instead of four
+        // 3M like the contraction: three real MFMAs per k-step instead of four
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
+        for (int t = 0; t < 2; ++t) {
+            d4 p1 = d4{0.0, 0.0, 0.0, 0.0}, p2 = p1, p3 = p1;
 #pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    const double2 a = wa[(t * NKS + ks) * 64];
-                    p1 = MFMA64(a.x, hr[ks], p1);
-                    p2 = MFMA64(a.y, hi[ks], p2);
-                    p3 = MFMA64(a.x + a.y, hs[ks], p3);
-                }
-                er[t] = p1 - p2;
-                ei[t] = p3 - p1 - p2;
+            for (int ks = 0; ks < NKS; ++ks) {
+                const double2 a = wa[(t * NKS + ks) * 64];
+                p1 = MFMA64(a.x, hr[ks], p1);
+                p2 = MFMA64(a.y, hi[ks], p2);
+                p3 = MFMA64(a.x + a.y, hs[ks], p3);
             }
-        } else {
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                er[t] = d4{0.0, 0.0, 0.0, 0.0};
-                ei[t] = er[t];
-#pragma unroll
-                for (int ks = 0; ks < NKS; ++ks) {
-                    const double2 a = wa[(t * NKS + ks) * 64];
-                    er[t] = MFMA64(a.x, hr[ks], er[t]);
-                    er[t] = MFMA64(-a.y, hi[ks], er[t]);
-                    ei[t] = MFMA64(a.x, hi[ks], ei[t]);
-                    ei[t] = MFMA64(a.y, hr[ks], ei[t]);
-                }
-            }
+            er[t] = p1 - p2;
+            ei[t] = p3 - p1 - p2;
         }
     }
     const int rl = unit % R;
@@ -3735,12 +2902,12 @@ __device__ __forceinline__ void wpair3_body(const PairBand& P, const double* __r
     if (fa.mse_err) flush_mse(me, mp, fa.mse_err, fa.mse_pow, fa.scheme, nsnr, snr, fa.nstage, fa.stage, rl < fa.rvalid);
 }
 
-template <int RBP, int NKS, bool FUSE, bool WDA_3M = false>
+template <int RBP, int NKS, bool FUSE>
 __global__ void __launch_bounds__(256)
     k_wpair3(PairBand P, const double* __restrict__ W3, long long wp_elems, int var, int nsnr, int snr0, int R, int U,
              const double2* __restrict__ hp, const double2* v, const double2* __restrict__ y,
              double2* __restrict__ yest, SchemeK sk, FuseArgs fa) {
-    wpair3_body<RBP, NKS, FUSE, WDA_3M>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
+    wpair3_body<RBP, NKS, FUSE>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
 }
 
 // Pre-pass of the fused MMSE stage of IC iteration `stage` (script:482-489):
@@ -3750,37 +2917,18 @@ __global__ void __launch_bounds__(256)
 // before any row can be detected.  Lane = unit; the pilot rows of W stream
 // with wave-uniform (scalar) loads.  NP x 24 x (NP + 1) CMACs per unit, 5 % of
 // the contraction.
-template <int NP, bool QIDX>
+template <int NP>
 __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __restrict__ Wpil,
                                                   const int* __restrict__ pil_c0, int var_prev, int nsnr, int snr0,
                                                   int R, int U, const double2* __restrict__ hp_prev,
-                                                  const double2* __restrict__ v, const uint16_t* __restrict__ qd,
-                                                  const double2* __restrict__ xs, const double2* __restrict__ y,
+                                                  const double2* __restrict__ v, const double2* __restrict__ y,
                                                   const double2* __restrict__ xp, double2* __restrict__ hp_new) {
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int rl = unit % R;
     const int snr = snr0 + (blockIdx.x * WAVE) / R;
-    __shared__ double2 sym[QIDX ? 256 : 1];
-    if (QIDX) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + 64 * k;
-            const double2 a = sk.symbols[min(i, sk.M - 1)];
-            sym[i] = make_double2(i < sk.M ? a.x : 0.0, i < sk.M ? a.y : 0.0);
-        }
-        __syncthreads();
-    }
-    // column c of v = P [xP; Q(x_est)]: the stored vector, or (QIDX) rebuilt
-    // from the decision indices; c is wave-uniform, so the row tables are
-    // scalar loads and the pilot / data branch is uniform
-    auto vcol = [&](int c) -> double2 {
-        if (!QIDX) return v[(size_t)c * U + unit];
-        const int pc = sk.row_pcol[c];
-        if (pc < NP) return xs[(size_t)c * R + rl];          // pilot (or empty) row: P xP
-        double2 r = make_double2(0.0, 0.0);
-        c_fma(r, sk.row_pval[c], sym[qd[(size_t)c * U + unit]]);
-        return r;
-    };
+    // column c of v = P [xP; Q(x_est)] (c is wave-uniform: the row tables are
+    // scalar loads)
+    auto vcol = [&](int c) -> double2 { return v[(size_t)c * U + unit]; };
     double2 hq[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) hq[p] = hp_prev[(size_t)p * U + unit];
@@ -3812,25 +2960,15 @@ __global__ void __launch_bounds__(64) k_pilot_pre(SchemeK sk, const double2* __r
     }
 }
 
-static bool wpair_3m(const Opts& op, const MmseK& mm) {
-    // 3M by default (NP = 32 too: its extra registers cost occupancy, but the
-    // contraction still drops 286 -> 225 ms per launch at C5, r02)
-    return mm.Wp3 && op.wpair_3m != 0;
-}
-
 bool mmse_fused_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b) {
     return mm.Wpil && mm.WdA && mm.Pb.rbp == 24 && mm.Pb.nks == 4 && sk.NP == 16 && op.fuse_stage &&
-           !op.wcontract_valu && wpair_3m(op, mm) && (b.U % 64) == 0 && (b.R % 64) == 0;
+           !op.wcontract_valu && mm.Wp3 && (b.U % 64) == 0 && (b.R % 64) == 0;
 }
 
 void launch_pilot_pre(hipStream_t s, const SchemeK& sk, const MmseK& mm, int var_prev, McBuffers& b,
-                      const double2* hp_prev, double2* hp_new, bool qidx) {
-    if (qidx)
-        hipLaunchKernelGGL((k_pilot_pre<16, true>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev,
-                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qre, b.xs, b.y, b.xp, hp_new);
-    else
-        hipLaunchKernelGGL((k_pilot_pre<16, false>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0,
-                           var_prev, mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.qre, b.xs, b.y, b.xp, hp_new);
+                      const double2* hp_prev, double2* hp_new) {
+    hipLaunchKernelGGL((k_pilot_pre<16>), dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, mm.Wpil, mm.pil_c0, var_prev, mm.nsnr,
+                       b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.xp, hp_new);
 }
 
 unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var_prev,
@@ -3853,50 +2991,32 @@ unsigned launch_mmse_fused(hipStream_t s, const Opts& op, const SchemeK& sk, con
     fa.scheme = scheme_index;
     fa.rvalid = b.rvalid;
     const dim3 grid(b.U / 64, mm.Pb.nblk);
-    // Opts::wda_3m = 0: diag(D_hat) of the epilogue with four real MFMAs per k-step
-    if (op.wda_3m)
-        hipLaunchKernelGGL((k_wpair3<24, 4, true, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var_prev,
-                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
-    else
-        hipLaunchKernelGGL((k_wpair3<24, 4, true, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var_prev,
-                           mm.nsnr, b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
+    hipLaunchKernelGGL((k_wpair3<24, 4, true>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var_prev, mm.nsnr,
+                       b.snr0, b.R, b.U, hp_prev, b.v, b.y, b.yest, sk, fa);
     return PATH_WPAIR3_FUSED;
 }
 
 unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int var, McBuffers& b) {
-    const bool pair_ok = mm.Wp && (b.U % 64) == 0 && (b.R % 64) == 0 && !op.wcontract_valu;
+    // the pair-tile contraction (k_wpair3), or the VALU contraction over the
+    // packed band where no pair tiles exist (a block wider than 32 rows) or on
+    // request (Opts::wcontract_valu)
+    const bool pair_ok = mm.Wp3 && (b.U % 64) == 0 && (b.R % 64) == 0 && !op.wcontract_valu;
     if (pair_ok) {
         const dim3 grid(b.U / 64, mm.Pb.nblk);
-        if (wpair_3m(op, mm)) {
 #define LAUNCH_W3(RBPV, NKSV)                                                                                  \
     hipLaunchKernelGGL((k_wpair3<RBPV, NKSV, false>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var,    \
                        mm.nsnr, b.snr0, b.R, b.U, b.hp, b.v, b.y, b.yest, sk, FuseArgs{})
-            if (mm.Pb.rbp == 24) {
-                if (mm.Pb.nks == 2) LAUNCH_W3(24, 2);
-                else if (mm.Pb.nks == 4) LAUNCH_W3(24, 4);
-                else LAUNCH_W3(24, 8);
-            } else {
-                if (mm.Pb.nks == 2) LAUNCH_W3(32, 2);
-                else if (mm.Pb.nks == 4) LAUNCH_W3(32, 4);
-                else LAUNCH_W3(32, 8);
-            }
-#undef LAUNCH_W3
-            return PATH_WPAIR3;
-        }
-#define LAUNCH_WP(RBPV, NKSV)                                                                                    \
-    hipLaunchKernelGGL((k_wpair<RBPV, NKSV>), grid, dim3(256), 0, s, mm.Pb, mm.Wp, mm.wp_elems, var, mm.nsnr, b.snr0, \
-                       b.R, b.U, b.hp, b.v, b.y, b.yest)
         if (mm.Pb.rbp == 24) {
-            if (mm.Pb.nks == 2) LAUNCH_WP(24, 2);
-            else if (mm.Pb.nks == 4) LAUNCH_WP(24, 4);
-            else LAUNCH_WP(24, 8);
+            if (mm.Pb.nks == 2) LAUNCH_W3(24, 2);
+            else if (mm.Pb.nks == 4) LAUNCH_W3(24, 4);
+            else LAUNCH_W3(24, 8);
         } else {
-            if (mm.Pb.nks == 2) LAUNCH_WP(32, 2);
-            else if (mm.Pb.nks == 4) LAUNCH_WP(32, 4);
-            else LAUNCH_WP(32, 8);
+            if (mm.Pb.nks == 2) LAUNCH_W3(32, 2);
+            else if (mm.Pb.nks == 4) LAUNCH_W3(32, 4);
+            else LAUNCH_W3(32, 8);
         }
-#undef LAUNCH_WP
-        return PATH_WPAIR4M;
+#undef LAUNCH_W3
+        return PATH_WPAIR3;
     }
     hipLaunchKernelGGL(k_wcontract_valu, dim3(b.U / WAVE, mm.Wb.nblk), dim3(WAVE), sk.NP * WAVE * sizeof(double2), s,
                        mm.Wb, mm.W, mm.w_elems, var, mm.nsnr, b.snr0, sk.NP, b.R, b.U, b.hp, b.v, b.y, b.yest);
@@ -3937,7 +3057,6 @@ __device__ __forceinline__ int slice(const SchemeK& sk, double2 z) {
 struct StageArgs {
     int stage, var, nsnr, nstage, scheme, last, perfect, R, U, snr0, xcd_order;
     int rvalid;                // realisations of the batch that count (McBuffers::rvalid)
-    int qidx;                  // p_diag schemes: decisions as symbol indices (qe / qp) instead of v / u
     const TraceK* tr;          // null unless tracing (dsce_trace_unit_ex)
     const double2* ysrc_e;     // y (stage 0) or y_est
     const double2* ysrc_p;     // y (stage 0) or y_perf
@@ -4231,7 +3350,7 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                     if (PERF) st.tr->dec_p[(size_t)st.stage * st.tr->ND + i] = dp;
                 }
                 if (!st.last) {
-                    if (sk.p_diag && !st.qidx) {
+                    if (sk.p_diag) {
                         const double2 pv = rpval[r];
                         double2 av = make_double2(0.0, 0.0), au = av;
                         if (rpcol[r] >= 0) {
@@ -4241,13 +3360,12 @@ __global__ void __launch_bounds__(256) k_stage_fused(SchemeK sk, StageArgs st, i
                         v[ix] = av;
                         if (PERF) u[ix] = au;
                     } else {
-                        // qidx: row-indexed decisions for the index-based chains
-                        const size_t qi = (size_t)(st.qidx ? row : i) * U + unit;
+                        const size_t qi = (size_t)i * U + unit;
                         qe[qi] = (uint16_t)de;
                         qp[qi] = (uint16_t)dp;
                     }
                 }
-            } else if (!st.last && sk.p_diag && st.stage == 0 && !st.qidx) {   // pilot / empty row: constant P xP
+            } else if (!st.last && sk.p_diag && st.stage == 0) {   // pilot / empty row: constant P xP
                 const int kc = rpcol[r];
                 double2 av = make_double2(0.0, 0.0);
                 if (kc >= 0) c_fma(av, rpval[r], xp[(size_t)kc * R + rl]);
@@ -4264,8 +3382,8 @@ template <int NPT>
 static void launch_stage_fused_np(hipStream_t s, const SchemeK& sk, const StageArgs& st, const MmseK& mm, McBuffers& b,
                                   unsigned long long* counters, int rb) {
     const int ug = b.U / 64;
-    uint16_t* qe_ = st.qidx ? b.qre : b.qe;            // qidx: row-indexed decisions
-    uint16_t* qp_ = st.qidx ? b.qrp : b.qp;
+    uint16_t* qe_ = b.qe;
+    uint16_t* qp_ = b.qp;
 #define LAUNCH_SF(RBV)                                                                                          \
     {                                                                                                           \
         const int nrb = (sk.LK + 4 * (RBV) - 1) / (4 * (RBV));                                                  \
@@ -4300,10 +3418,9 @@ bool perfect_fusable(const Opts& op, const SchemeK& sk) { return stage_fused_ok(
 
 unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, int stage, int var,
                       int n_iter, bool last, McBuffers& b, unsigned long long* counters, int scheme_index,
-                      bool perfect, bool qidx) {
+                      bool perfect) {
     StageArgs st;
     st.perfect = perfect ? 1 : 0;
-    st.qidx = qidx && sk.p_diag && stage_fused_ok(op, sk) ? 1 : 0;
     st.stage = stage;
     st.var = var;
     st.nsnr = mm.nsnr;
@@ -4340,48 +3457,6 @@ unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const Mm
     if (!last)
         hipLaunchKernelGGL(k_precode, dim3(b.U / WAVE, rblk), dim3(WAVE), 0, s, sk, st, b.xp, b.qe, b.qp, b.v, b.u);
     return PATH_STAGE_SPLIT;
-}
-
-// Stage 0 of the index-based OFDM chains (k_ls + k_stage0_fft)
-unsigned launch_stage0_fft(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, int n_iter,
-                           bool last, McBuffers& b, const PerfectDetectArgs* pd, int xcd) {
-    // LS pilot estimates of stage 0 into b.hp (k_ls), then the symbol-block stage
-    StageArgs st{};
-    st.R = b.R;
-    st.rvalid = b.rvalid;
-    st.U = b.U;
-    st.ysrc_e = b.y;
-    hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);
-    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
-    MicArgs ma{};
-    ma.bs = mm.Bs;
-    ma.hp_new = b.hp;
-    ma.mse_err = b.mse_err;
-    ma.mse_pow = b.mse_pow;
-    ma.var_cur = 0;
-    ma.nsnr = mm.nsnr;
-    ma.N = ch.N;
-    ma.nblk = sk.QH.nblk;
-    ma.stage = 0;
-    ma.nstage = n_iter + 1;
-    ma.last = last ? 1 : 0;
-    ma.scheme = pd->scheme;
-    const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
-    const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
-#define LAUNCH_S0(NTV, SHV)                                                                                           \
-    do {                                                                                                              \
-        if (b.tr)                                                                                                     \
-            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o, b.qrp, pd->counters); \
-        else                                                                                                          \
-            hipLaunchKernelGGL((k_stage0_fft<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o, b.qrp,           \
-                               pd->counters);                                                                         \
-    } while (0)
-    const int sh = pic_fft_shift(ch);
-    if (ch.ntap == 1) LAUNCH_S0(1, 0);
-    else if (sh == 1) LAUNCH_S0(2, 1);
-    else LAUNCH_S0(2, 2);
-#undef LAUNCH_S0
-    return PATH_STAGE_FUSED;
 }
 
 // MMSE one-tap channel h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p for n LS

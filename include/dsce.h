@@ -184,7 +184,7 @@ typedef struct {
 /* Kernel paths (dsce_path_info) */
 #define DSCE_PATH_WPAIR3_FUSED    (1u << 0)   /* k_pilot_pre + k_wpair3 with the MMSE stage in its epilogue */
 #define DSCE_PATH_WPAIR3          (1u << 1)   /* k_wpair3: MFMA pair-tile contraction, 3M products        */
-#define DSCE_PATH_WPAIR4M         (1u << 2)   /* k_wpair: pair tiles, 4 real MFMAs per complex product     */
+#define DSCE_PATH_WPAIR4M         (1u << 2)   /* retired in r03 (k_wpair, 4M products); never set          */
 #define DSCE_PATH_WCONTRACT_VALU  (1u << 3)   /* k_wcontract_valu                                         */
 #define DSCE_PATH_PIC_MFMA        (1u << 4)   /* retired in ABI 4 (k_pic_mfma); never set                  */
 #define DSCE_PATH_PIC_CHAIN       (1u << 5)   /* retired in ABI 4 (k_pic_chain); never set                 */
@@ -193,9 +193,9 @@ typedef struct {
 #define DSCE_PATH_STAGE_SPLIT     (1u << 8)   /* k_ls_hest + k_detect + k_precode                          */
 #define DSCE_PATH_NOISE_FUSED     (1u << 9)   /* AWGN drawn inside the Q^H pass                            */
 #define DSCE_PATH_PIC_FFT         (1u << 10)  /* k_pic_fft: perfect-CSI IC chain by FFT (OFDM, VALU)       */
-#define DSCE_PATH_MIC_FFT         (1u << 11)  /* k_pilot_pre + k_mic_fft: MMSE IC as Q' H_hat G by FFT (OFDM) */
+#define DSCE_PATH_MIC_FFT         (1u << 11)  /* MMSE IC as Q' H_hat G by FFT (OFDM; with DSCE_PATH_MIC_STAGES) */
 #define DSCE_PATH_TXRX_FFT        (1u << 12)  /* k_txrx_fft: TX + channel + noisy receiver front by FFT (OFDM) */
-#define DSCE_PATH_PILOT_FUSED     (1u << 13)  /* k_mic_fft also runs the next IC iteration's pilot pass       */
+#define DSCE_PATH_PILOT_FUSED     (1u << 13)  /* retired in r03 (k_mic_fft's fused pilot pass); never set     */
 #define DSCE_PATH_MIC_STAGES      (1u << 14)  /* k_mic_pilot + k_mic_data: every MMSE stage of an FFT-form OFDM
                                                  scheme in one launch pair; k_pic_fft with the perfect-CSI stage 0 */
 
@@ -290,24 +290,28 @@ int dsce_trace_unit_ex(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t
 int dsce_scheme_dims(dsce_ctx* ctx, int32_t scheme_id, dsce_dims* dims);
 /* Which kernels a scheme's last dsce_run / trace used: DSCE_PATH_* bits. */
 int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
-/* Kernel-selection options (defaults = the measured-best path; for A/B runs and
- * tests): xcd, fuse_stage, wpair_3m (-1 auto), wda_3m, pic_chain (0 passes,
- * 3 FFT chain where the scheme's G / Q allow it, else passes), pfuse, stage_split, stage_rb (4|8|16), noise_fuse,
- * snr_chunk (0 all), streams (1|2), jakes_rpw (1|2), wtrim (read by
- * dsce_build_mmse), wcontract_valu, mmse_ic (1: the MMSE IC iterations of an FFT-form
- * OFDM scheme as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}
- * (k_mic_fft; equal to the W contraction of script:482-511 to rounding, checked
- * at dsce_build_mmse), 0: the W contraction everywhere), qidx, stage0_fft,
- * mic_mfma, pilot_fft, jakes_win, txrx_fft, mic_yic, pilot_fuse (the OFDM fast-path pieces,
- * 1 = on), mic2 (1 = every MMSE stage of FFT-form OFDM in k_mic_pilot + k_mic_data and the
- * perfect-CSI stage 0 in k_pic_fft; 0 = the per-stage kernels), jakes_mom (the Jakes taps of the
- * read windows: 2 = Taylor anchors over runs of windows, 1 = one anchor per window, 0 = the
- * recurrence; each only where its truncation stays below rounding), realise_win (1:
- * dsce_channel_realise forms only the samples the schemes' windows read, zero elsewhere,
- * with the run's Jakes kernels), tx_rows (1: TX symbols of a row-local precoder drawn
- * row-parallel), snr_base (0..255: the noise of SNR index k is sub-stream
- * snr_base + k, so a rank serving SNR points [b, ...) of a sweep draws the
- * one-rank run's noise).  Unknown names return DSCE_EINVAL. */
+/* Kernel-selection options (defaults = the measured-best path; each other value
+ * selects a real fallback, reached by the parity tests):
+ *   xcd (XCD-aware work order), fuse_stage (MMSE stage in the contraction's
+ *   epilogue), pic_chain (3: perfect-CSI IC chain by FFT where the scheme's G / Q
+ *   allow it, 0: two banded passes per iteration), pfuse, stage_split, stage_rb
+ *   (4|8|16), noise_fuse, snr_chunk (0 all), jakes_rpw (1|2), wtrim (read by
+ *   dsce_build_mmse), wcontract_valu (the VALU contraction, also the fallback
+ *   without pair tiles), mmse_ic (1: the MMSE branch of an FFT-form OFDM scheme
+ *   as y - Q'(H_hat (G v)) + diag(D_hat) v with H_hat = E{H | hP}, every stage in
+ *   k_mic_pilot + k_mic_data and the perfect-CSI stage 0 in k_pic_fft; equal to
+ *   the W contraction of script:482-511 to rounding, checked at dsce_build_mmse;
+ *   0: the W contraction everywhere), jakes_win, txrx_fft, jakes_mom (the Jakes
+ *   taps of the read windows: 2 = Taylor anchors over runs of windows, 1 = one
+ *   anchor per window, 0 = the recurrence; each only where its truncation stays
+ *   below rounding), realise_win (1: dsce_channel_realise forms only the samples
+ *   the schemes' windows read, zero elsewhere, with the run's Jakes kernels),
+ *   tx_rows (1: TX symbols of a row-local precoder drawn row-parallel), snr_base
+ *   (0..255: the noise of SNR index k is sub-stream snr_base + k, so a rank
+ *   serving SNR points [b, ...) of a sweep draws the one-rank run's noise).
+ * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
+ * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
+ * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value);
 int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 

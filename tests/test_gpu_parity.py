@@ -94,13 +94,11 @@ def test_mmse_estimator_matches_oracle(ofdm):
 # The benchmarked kernels under direct oracle parity (bench path = C2 OFDM:
 # k_txrx_fft for TX / channel / noisy receiver front, k_pic_fft for the whole
 # perfect-CSI branch (stage 0 + IC chain), k_mic_pilot + k_mic_data for every
-# stage of the MMSE branch (Q' H_hat G by FFT)); the r02 per-stage path
-# (k_stage0_fft + k_mic_fft with the fused pilot pass, mic2 0) and the W
-# contraction (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
+# stage of the MMSE branch (Q' H_hat G by FFT)), and the W contraction
+# (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
 BENCH_PATH = {"mic_fft", "mic_stages", "pic_fft", "noise_fused", "txrx_fft"}
-STAGE_PATH = {"mic_fft", "pilot_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
-W_PATH = STAGE_PATH - {"mic_fft", "pilot_fused"} | {"wpair3_fused"}
+W_PATH = {"wpair3_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
 
 
 def _check_trace(g, u, name, tol=1e-9):
@@ -123,14 +121,14 @@ def _check_trace(g, u, name, tol=1e-9):
 def test_bench_kernels_trace_matches_oracle(ofdm):
     """dsce_trace_unit_ex runs the same kernels as dsce_run (asserted through
     dsce_path_info) and every intermediate of every stage of a unit matches the
-    oracle (literal W of script:493-511): k_mic_fft's y_est and diag(D_hat),
-    k_pilot_pre's LS pilots, k_pic_fft's y_perf (data rows: the chain forms
-    only those) and both branches' decisions; the same for the fused W
-    contraction (mmse_ic 0)."""
+    oracle (literal W of script:493-511): k_mic_pilot / k_mic_data's y_est,
+    LS pilots and diag(D_hat) of every stage, k_pic_fft's y_perf (data rows:
+    the chain forms only those) and both branches' decisions; the same for the
+    fused W contraction (mmse_ic 0: k_pilot_pre + k_wpair3 epilogue, stage 0
+    from k_stage_fused, k_pic_fft without its stage 0)."""
     S, eng, mm = ofdm
     rows = S.schemes["ofdm"]["data_pos"]
-    for mic2, mic, path in ((1, 1, BENCH_PATH), (0, 1, STAGE_PATH), (1, 0, W_PATH)):
-        eng.set_option("mic2", mic2)
+    for mic, path in ((1, BENCH_PATH), (0, W_PATH)):
         eng.set_option("mmse_ic", mic)
         for rep in (5, 70):
             tr = {}
@@ -139,10 +137,9 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
                 g = eng.trace_unit(0, SEED, rep, k)
                 assert path <= eng.path_info(0), eng.path_info(0)
                 u = tr["units"][k]
-                ns = _check_trace(g, u, "mic2 %d mmse_ic %d rep %d snr %d" % (mic2, mic, rep, k))
+                ns = _check_trace(g, u, "mmse_ic %d rep %d snr %d" % (mic, rep, k))
                 for st in range(1, ns):
                     np.testing.assert_allclose(g["yperf"][st][rows], u["yperf"][st][rows], rtol=0, atol=1e-9)
-    eng.set_option("mic2", 1)
     eng.set_option("mmse_ic", 1)
 
 
@@ -175,18 +172,18 @@ def test_error_counts_match_oracle(ofdm):
 @pytest.mark.parametrize("n_iter", [1, 2, 3, 6])
 def test_ic_iteration_counts_match_oracle(n_iter):
     """Other IC iteration counts (script:479 `NrIterations`): the estimator
-    variant switch (W0 up to niter / 2, script:497-501) and the fused pilot pass
-    (iteration i's k_mic_fft forms iteration i + 1's pilots; none for niter 1)
-    against the oracle, counts of every stage, and one unit traced per element."""
+    variant switch (W0 up to niter / 2, script:497-501) against the oracle
+    through the bench kernels and the W contraction, counts of every stage, and
+    one unit traced per element."""
     S = harness.setup("default", schemes=("ofdm",), snr_db=[15.0, 35.0], n_iter=n_iter)
     eng = harness.engine(S, batch=64)
     cg = eng.run(SEED, 0, 64)
     path = eng.path_info(0)
     assert BENCH_PATH <= path, path
-    eng.set_option("mic2", 0)                   # the per-stage path: the pilot pass fuses from niter 2 on
+    eng.set_option("mmse_ic", 0)                # the W contraction, per-stage launches
     assert np.array_equal(eng.run(SEED, 0, 64), cg)
-    assert ("pilot_fused" in eng.path_info(0)) == (n_iter >= 2), eng.path_info(0)
-    eng.set_option("mic2", 1)
+    assert W_PATH <= eng.path_info(0), eng.path_info(0)
+    eng.set_option("mmse_ic", 1)
     res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
     assert cg.shape == res["err"].shape
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
@@ -370,20 +367,15 @@ def test_stage_variants_agree(name):
     """Every kernel option (dsce_set_option) gives identical counts on 1024
     realisations: the fused select-mode stage vs the 3-kernel split path (any
     row-block size), perfect-CSI detection fused into the second pass or not,
-    XCD-aware work order on/off, SNR-chunked receiver, two streams, 4-MFMA
-    instead of 3M complex products, the VALU contraction, the MMSE stage as its
-    own kernels instead of fused into the contraction, the perfect-CSI chain as
-    per-iteration passes instead of k_pic_fft, the fused
-    epilogue's diag(D_hat) with 4 real MFMAs, one realisation per Jakes wave,
-    the W contraction instead of the structured MMSE IC (k_mic_fft), decisions
-    passed between the stages as v / u instead of symbol indices, k_mic_fft's
-    taps on the VALU instead of the matrix cores, the pilot pre-pass from W's
-    pilot rows (k_pilot_pre) instead of the structured chain, the Jakes taps at
-    every sample instead of only where a Q^H row reads them, TX / channel /
-    noisy Q^H as banded passes instead of k_txrx_fft, the pilot symbols' y_ic
-    formed again in k_mic_fft instead of handed over by the pilot pass, the
-    pilot pass as its own launch instead of riding in the previous iteration's
-    k_mic_fft."""
+    XCD-aware work order on/off, SNR-chunked receiver, the VALU contraction
+    (the fallback without pair tiles), the MMSE stage as its own kernels
+    instead of fused into the contraction, the perfect-CSI chain as
+    per-iteration passes instead of k_pic_fft, one realisation per Jakes wave,
+    the W contraction instead of the structured MMSE IC (k_mic_pilot /
+    k_mic_data), the Jakes taps at every sample instead of only where a Q^H row
+    reads them (and the anchor / moment fallbacks), TX / channel / noisy Q^H as
+    banded passes instead of k_txrx_fft, the TX symbols one realisation per
+    lane (k_tx_symbols, the fallback for non-row-local precoders)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -394,13 +386,11 @@ def test_stage_variants_agree(name):
         eng.set_option("stage_rb", rb)
         np.testing.assert_array_equal(eng.run(SEED, 0, 1024), ref, err_msg=str(rb))
     eng.set_option("stage_rb", 8)
-    variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2}, {"streams": 2}, {"wpair_3m": 0},
+    variants = ({"pfuse": 0}, {"xcd": 0}, {"snr_chunk": 2},
                 {"wcontract_valu": 1}, {"fuse_stage": 0}, {"pic_chain": 0},
-                {"streams": 2, "fuse_stage": 0}, {"noise_fuse": 0}, {"wda_3m": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
-                {"qidx": 0}, {"stage0_fft": 0}, {"mic_mfma": 0},
-                {"pilot_fft": 0}, {"jakes_win": 0}, {"txrx_fft": 0},
-                {"mic_yic": 0}, {"pilot_fuse": 0}, {"mic2": 0}, {"jakes_mom": 1}, {"jakes_mom": 0},
-                {"tx_rows": 0})
+                {"noise_fuse": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
+                {"jakes_win": 0}, {"txrx_fft": 0}, {"mmse_ic": 0, "fuse_stage": 0, "pic_chain": 0},
+                {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
@@ -421,6 +411,12 @@ def test_options_are_validated():
     for retired in (1, 2):                      # k_pic_chain / k_pic_mfma, retired in r03
         with pytest.raises(DsceError):
             eng.set_option("pic_chain", retired)
+    # the r01-r02 variants pruned in r03 (4M k_wpair, the per-stage k_mic_fft
+    # path, the second stream): their options are gone
+    for name in ("wpair_3m", "wda_3m", "streams", "qidx", "stage0_fft", "mic_mfma", "pilot_fft", "mic_yic",
+                 "pilot_fuse", "mic2"):
+        with pytest.raises(DsceError):
+            eng.set_option(name, 0)
     assert eng.get_option("fuse_stage") == 1
     eng.close()
 
