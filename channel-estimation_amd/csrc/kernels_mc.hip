@@ -2063,7 +2063,7 @@ __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, doub
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
 template <int NT, int SH, int NP, bool TRACE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
+__global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[4][24], wrow[4][24];
     __shared__ int rdc[4][24], rpc[4][24];
