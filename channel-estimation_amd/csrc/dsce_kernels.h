@@ -26,6 +26,7 @@ struct Opts {
     int txrx_fft = 1;         // TX + channel + receiver front of FFT-form OFDM in one pass (k_txrx_fft)
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
     int tx_rows = 1;          // row-local precoders: TX symbols drawn row-parallel (k_tx_rows)
+    int pic_net = 1;          // k_pic_fft's 4-point network: 1 = v_mfma_f64_4x4x4 (quarters on 16-lane rows), 0 = DPP
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;

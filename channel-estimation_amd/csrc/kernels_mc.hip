@@ -1403,6 +1403,26 @@ __device__ __forceinline__ double2 quad_tw(double2 e, bool r3) {
 }
 
 
+// D = A B of the four 4 x 4 blocks of v_mfma_f64_4x4x4f64 with complex A and B
+// (this lane's entries a, b): re = Ar Br - Ai Bi, im = Ar Bi + Ai Br, two
+// accumulating MFMAs each
+__device__ __forceinline__ double2 mfma4_cmul(double2 a, double2 b) {
+    double re = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b.x, 0.0, 0, 0, 0);
+    re = __builtin_amdgcn_mfma_f64_4x4x4f64(-a.y, b.y, re, 0, 0, 0);
+    double im = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b.y, 0.0, 0, 0, 0);
+    im = __builtin_amdgcn_mfma_f64_4x4x4f64(a.y, b.x, im, 0, 0, 0);
+    return make_double2(re, im);
+}
+
+// a complex from lane addr / 4 of the wave (ds_bpermute: the LDS crossbar, no LDS
+// allocation, no barrier)
+__device__ __forceinline__ double2 bperm_c(int addr, double2 v) {
+    return make_double2(__hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.x)),
+                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.x))),
+                        __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.y)),
+                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.y))));
+}
+
 // position of output k of dft6 in the array (k = k1 + 3 k2 lands at k2 + 2 k1)
 __host__ __device__ constexpr int p6(int k) { return k / 3 + 2 * (k % 3); }
 
@@ -1438,22 +1458,33 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // perfect-CSI branch, the one-tap x = y ./ h (script:450-466), so no stage
 // kernel runs in front: u starts as P [xP; 0] (xs of the pilot rows) and the
 // data rows get the stage-0 decisions in registers.
-template <int NT, int SH, bool TRACE, bool S0 = false>
+// NM (r03k): the 4-point network on the matrix cores instead.  A unit's four
+// quarters sit on the four 16-lane rows (lane = 16 r + unit), which is the K
+// index of v_mfma_f64_4x4x4f64 (4 blocks of 4 units: B[k][n] in lane 16 k +
+// 4 c + n, D[i][n] in lane 16 i + 4 c + n, A[i][k] in lane 16 k + 4 c + i), so
+// per sample m the whole network including the lane twiddle is one complex
+// 4 x 4 product, A_m[i][k] = i^(i k) w24^(k m) (inverse) or qs gs i^(-i k)
+// w24^(-i m) (forward; outputs in natural order): four MFMAs (re / im x the
+// two real K halves, 72 cycles per m per wave on the box) instead of the lane
+// twiddle, 8 DPP moves, 4 FMAs and the +-i selects (100 cycles,
+// tools/ubench/net.hip).  The previous quarter's sample 5 comes by ds_bpermute.
+template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     int ug, blk;
     band_block(ord, sk.QH.nblk, ug, blk);
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = l & 3;
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = NM ? l >> 4 : l & 3;
     const int U = o.U, R = o.R;
-    const int unit = ug * WAVE + w * 16 + (l >> 2);
+    const int unit = ug * WAVE + w * 16 + (NM ? (l & 15) : (l >> 2));
     const int rl = unit % R;
-    const int cq = (r >> 1) + 2 * (r & 1);                     // time quarter of this lane
+    const int cq = NM ? r : (r >> 1) + 2 * (r & 1);            // time quarter of this lane
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
     __shared__ double2 sym[256];
     __shared__ int sgrid[256];
     __shared__ double2 rpv[24];
     __shared__ int rdc[24];
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
+    __shared__ double2 amt[NM ? 2 : 1][6][16];                  // NM: A_m[i][k] at [dir][m][i + 4 k]
     __shared__ int cntl[4][PM_MAXIT + 1];                      // [wave][stage]
     // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
     // and the channel taps of the lane's samples (registers for all iterations)
@@ -1500,6 +1531,14 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             const int tc = min(tid, 47), dir = tc / 24;
             const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
             twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+        }
+        if (NM && tid < 192) {
+            // A_m[i][k]: inverse w24^(6 i k + k m), forward qs gs w24^-(6 i k + i m)
+            const int dir = tid / 96, m = (tid / 16) % 6, ii = tid & 3, kk = (tid >> 2) & 3;
+            const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
+            const double2 t0 = kW24[ea % 12];
+            const double2 v = ea >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+            amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
         }
     }
     __syncthreads();
@@ -1567,19 +1606,25 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         for (int a = 0; a < 6; ++a) x[a] = u[a];
         dft6<1>(x);
         double2 t[6];
+        const int ai = (l & 3) + 4 * (l >> 4) + oz;             // NM: this lane's A entry
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            const double2 p = c_mulf(x[p6(m)], twa[0][ro][m]);
-            const double2 pv = dpp_c<QP_XOR2>(p);
-            double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-            e = quad_tw<1>(e, r == 3);
-            const double2 qv = dpp_c<QP_XOR1>(e);
-            t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+            if (NM) {
+                const double2 am = amt[0][m][ai], b = x[p6(m)];
+                t[m] = mfma4_cmul(am, b);
+            } else {
+                const double2 p = c_mulf(x[p6(m)], twa[0][ro][m]);
+                const double2 pv = dpp_c<QP_XOR2>(p);
+                double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+                e = quad_tw<1>(e, r == 3);
+                const double2 qv = dpp_c<QP_XOR1>(e);
+                t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+            }
         }
         // channel, in place, last sample first: x[m] = sum_q IR_q[m] t[m - d_q];
         // t[-1] of the quarter is sample 5 of the previous quarter's lane (the
         // cyclic prefix for quarter 0)
-        const double2 tprev = dpp_c<QP_PREV>(t[5]);
+        const double2 tprev = NM ? bperm_c(((l + 48) & 63) * 4, t[5]) : dpp_c<QP_PREV>(t[5]);
 #pragma unroll
         for (int m = 5; m >= 0; --m) {
             const double2 tp = m ? t[m - 1] : tprev;
@@ -1592,11 +1637,15 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         // xor 2) back to lane r = output residue, twiddle qs gs w24^-(r m'), DFT-6
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            const double2 pv = dpp_c<QP_XOR1>(t[m]);
-            double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-            f = quad_tw<-1>(f, r == 3);
-            const double2 qv = dpp_c<QP_XOR2>(f);
-            x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][ro][m]);
+            if (NM) {
+                x[m] = mfma4_cmul(amt[NM ? 1 : 0][m][ai], t[m]);
+            } else {
+                const double2 pv = dpp_c<QP_XOR1>(t[m]);
+                double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+                f = quad_tw<-1>(f, r == 3);
+                const double2 qv = dpp_c<QP_XOR2>(f);
+                x[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][ro][m]);
+            }
         }
         dft6<-1>(x);
         // y / h and 1 / h at the first epilogue (not before the loop): the
@@ -1729,15 +1778,6 @@ struct Mic2Args {
 };
 
 __device__ __forceinline__ int mic_var(int s, int niter) { return (s == 0 || 2 * s <= niter) ? 0 : 1; }
-
-// a complex from lane addr / 4 of the wave (ds_bpermute: the LDS crossbar, no LDS
-// allocation, no barrier)
-__device__ __forceinline__ double2 bperm_c(int addr, double2 v) {
-    return make_double2(__hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.x)),
-                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.x))),
-                        __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v.y)),
-                                         __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.y))));
-}
 
 // Estimated taps of the lane's six window samples (quad layout: lane r of a unit
 // holds samples 6 cq + m) for the 16 units of a wave: MFMA GEMM (3M) with
@@ -2505,17 +2545,20 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
     // stage0: the chain also runs stage 0 of the branch (with k_mic_pilot /
     // k_mic_data); otherwise stage 0 came from the stage kernel (u in HBM)
-#define LAUNCH_PF(NTV, SHV, S0V)                                                                                  \
-    do {                                                                                                          \
-        if (b.tr)                                                                                                 \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);  \
-        else                                                                                                      \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+#define LAUNCH_PF(NTV, SHV, S0V, NMV)                                                                               \
+    do {                                                                                                             \
+        if (b.tr)                                                                                                    \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);  \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
     } while (0)
-#define LAUNCH_PF2(NTV, SHV)                \
-    do {                                    \
-        if (stage0) LAUNCH_PF(NTV, SHV, true); \
-        else LAUNCH_PF(NTV, SHV, false);       \
+    // Opts::pic_net: the 4-point network on the matrix cores (1) or by DPP (0)
+#define LAUNCH_PF2(NTV, SHV)                              \
+    do {                                                  \
+        if (stage0 && op.pic_net) LAUNCH_PF(NTV, SHV, true, true);    \
+        else if (stage0) LAUNCH_PF(NTV, SHV, true, false);            \
+        else if (op.pic_net) LAUNCH_PF(NTV, SHV, false, true);        \
+        else LAUNCH_PF(NTV, SHV, false, false);                       \
     } while (0)
     const int sh = pic_fft_shift(ch);
     if (ch.ntap == 1) LAUNCH_PF2(1, 0);
