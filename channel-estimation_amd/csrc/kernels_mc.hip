@@ -1310,12 +1310,16 @@ __device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, unsigned vo
 // integral, inside the grid) flags the lower neighbour as the tie alternative
 // (first-minimum rule of SignalConstellation.m:88, resolved on the grid by the
 // caller: a flag at level 0 reads level 0 twice); NaN / inf (h == 0) clamp into
-// the grid.
+// the grid.  The clamp runs on the truncated integer (v_cvt_i32_f64 saturates
+// and maps NaN to 0; below 0 truncation and floor clamp alike): two f64 ops
+// per component fewer than floor / fmax / fmin.
 __device__ __forceinline__ int nearest_lin(double x, double scale, double offset, double top, int& tie) {
     const double f = fma(x, scale, offset);              // (x - lv0) / step + 0.5
-    const double c = fmin(fmax(floor(f), 0.0), top);
-    tie = f == c ? 1 : 0;                                // on the mid-point below level c
-    return (int)c;
+    int t, c;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(t) : "v"(f));
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(t), "v"((int)top));
+    tie = f == (double)c ? 1 : 0;                        // on the mid-point below level c
+    return c;
 }
 
 // Error counts of a 256-thread block, one atomic per counter per block: every
