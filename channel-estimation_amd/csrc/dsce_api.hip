@@ -1178,11 +1178,11 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 }
                 {
                     Timed t(c, "k_mic_pilot");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1);
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1, (op.mic_net & 2) != 0);
                 }
                 {
                     Timed t(c, "k_mic_data");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2);
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2, (op.mic_net & 1) != 0);
                 }
                 if (to && to->hp_stages)
                     for (int st = 0; st <= c->niter; ++st)
@@ -1944,7 +1944,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

@@ -27,6 +27,8 @@ struct Opts {
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
     int tx_rows = 1;          // row-local precoders: TX symbols drawn row-parallel (k_tx_rows)
     int pic_net = 1;          // k_pic_fft's 4-point network: 1 = v_mfma_f64_4x4x4 (quarters on 16-lane rows), 0 = DPP
+    int mic_net = 1;          // the same network for k_mic_data (bit 0) / k_mic_pilot (bit 1), whose tap GEMM then
+                              // needs no exchange: data 3.99 -> 3.65 ms, pilot 1.91 -> 2.00 ms (237 VGPRs): 1
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
@@ -188,7 +190,7 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
                     int niter);
 // part: 1 = k_mic_pilot, 2 = k_mic_data (the data kernel reads the pilot kernel's hpa)
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd, int part);
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm = true);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in

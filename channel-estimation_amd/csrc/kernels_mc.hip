@@ -1791,7 +1791,9 @@ __device__ __forceinline__ int mic_var(int s, int niter) { return (s == 0 || 2 *
 // the lane (unit ul, quarter cq) pulls its four taps of the tile from lane
 // 16 cq + ul with one ds_bpermute per dword, the same register in every lane
 // (r02-r03's per-wave LDS slab needed 17 KB per block and a fence pair per tile).
-template <int NT, int NP, class ALoad>
+// NM (quarters on the 16-lane rows, lane = 16 cq + unit): D register k of a
+// lane already is its tap index 4 t + k, no exchange at all.
+template <int NT, int NP, bool NM, class ALoad>
 __device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A, const double2 (&hb)[NP / 4], int l,
                                          int cq) {
     constexpr int NIDX = 6 * NT, NTILE = (NIDX + 3) / 4, NKS = NP / 4;
@@ -1821,29 +1823,37 @@ __device__ __forceinline__ void mic_taps(double2 (&taps)[6][NT], const ALoad& A,
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int id2 = 4 * t + k;                     // compile-time
-            if (id2 < NIDX)
-                taps[id2 % 6][id2 / 6] = bperm_c(src, make_double2(p1[k] - p2[k], p3[k] - p1[k] - p2[k]));
+            if (id2 < NIDX) {
+                const double2 tv = make_double2(p1[k] - p2[k], p3[k] - p1[k] - p2[k]);
+                taps[id2 % 6][id2 / 6] = NM ? tv : bperm_c(src, tv);
+            }
         }
     }
 }
 
 // x <- qs gs DFT24(sum_q taps_q .* IDFT24(x)(. - d_q)) of one symbol (k_pic_fft's
 // chain; twa: the lane twiddles staged in LDS, output scale folded in twa[1])
-template <int NT, int SH>
+// NM: k_pic_fft's matrix-core network (amt: A_m per [dir][m][i + 4 k], ai this
+// lane's entry; the previous quarter's sample by ds_bpermute)
+template <int NT, int SH, bool NM>
 __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[6][NT], const double2 (*twa)[4][6],
-                                          int r, double sg1, double sg2) {
+                                          const double2 (*amt)[6][16], int ai, int l, int r, double sg1, double sg2) {
     dft6<1>(xx);
     double2 t[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
-        const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
-        const double2 pv = dpp_c<QP_XOR2>(p);
-        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-        e = quad_tw<1>(e, r == 3);
-        const double2 qv = dpp_c<QP_XOR1>(e);
-        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+        if (NM) {
+            t[m] = mfma4_cmul(amt[0][m][ai], xx[p6(m)]);
+        } else {
+            const double2 p = c_mulf(xx[p6(m)], twa[0][r][m]);
+            const double2 pv = dpp_c<QP_XOR2>(p);
+            double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
+            e = quad_tw<1>(e, r == 3);
+            const double2 qv = dpp_c<QP_XOR1>(e);
+            t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
+        }
     }
-    const double2 tprev = dpp_c<QP_PREV>(t[5]);
+    const double2 tprev = NM ? bperm_c(((l + 48) & 63) * 4, t[5]) : dpp_c<QP_PREV>(t[5]);
 #pragma unroll
     for (int m = 5; m >= 0; --m) {
         const double2 tq = m ? t[m - 1] : tprev;
@@ -1854,11 +1864,15 @@ __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[
     }
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
-        const double2 pv = dpp_c<QP_XOR1>(t[m]);
-        double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
-        f = quad_tw<-1>(f, r == 3);
-        const double2 qv = dpp_c<QP_XOR2>(f);
-        xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+        if (NM) {
+            xx[m] = mfma4_cmul(amt[1][m][ai], t[m]);
+        } else {
+            const double2 pv = dpp_c<QP_XOR1>(t[m]);
+            double2 f = make_double2(fma(sg2, t[m].x, pv.x), fma(sg2, t[m].y, pv.y));
+            f = quad_tw<-1>(f, r == 3);
+            const double2 qv = dpp_c<QP_XOR2>(f);
+            xx[m] = c_mulf(make_double2(fma(sg1, f.x, qv.x), fma(sg1, f.y, qv.y)), twa[1][r][m]);
+        }
     }
     dft6<-1>(xx);
 }
@@ -1869,6 +1883,7 @@ struct Mic2Tables {
     double2 sym[256];
     int sgrid[256];
     double2 twa[2][4][6];
+    double2 amt[2][6][16];            // NM network: A_m[i][k] at [dir][m][i + 4 k] (k_pic_fft's)
 };
 
 // One-tap + detection of the lane's six rows with diag(D_hat) = hd[a]; returns
@@ -1902,14 +1917,14 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
 // k_mic_pilot and k_mic_data).  PIL: a pilot symbol (LS of every stage into the
 // block's LDS exchange + hpa, one barrier per stage); otherwise hP_s comes from
 // hpa.  Per-stage counters go to cntl[w][s] (one word per wave and stage).
-template <int NT, int SH, int NP, bool TRACE, bool PIL, class ALoad, class BsLoad>
+template <int NT, int SH, int NP, bool TRACE, bool PIL, bool NM, class ALoad, class BsLoad>
 __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
                                             const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
                                             const double2* wrow, double2 (*shp)[NP][17],
                                             const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
                                             int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
                                             int snr) {
-    const int cq = (r >> 1) + 2 * (r & 1);
+    const int cq = NM ? r : (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
     const double isqk = sk.inv_sqrt_kappa;
@@ -1952,8 +1967,14 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             double2 sq = c_mul(Bs(vs, q, ro * (NP / 4)), hn4[0]);
 #pragma unroll
             for (int k = 1; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
-            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            if (NM) {
+                // sum over the unit's four quarters (rows): ones(4 x 4) x B
+                sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.x, 0.0, 0, 0, 0),
+                                  __builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.y, 0.0, 0, 0, 0));
+            } else {
+                sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+                sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            }
             if ((SH >> q) & 1) {
                 sn1 = f1 ? sq : c_add(sn1, sq);
                 f1 = false;
@@ -1985,12 +2006,12 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 #pragma unroll
                 for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = shp[(s - 1) & 1][4 * ks + (l >> 4)][l & 15];
             double2 taps[6][NT];
-            mic_taps<NT, NP>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); }, hb,
-                             l, cq);
+            mic_taps<NT, NP, NM>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); },
+                                 hb, l, cq);
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
-            mic_chain<NT, SH>(x, taps, tb.twa, ro, sg1, sg2);
+            mic_chain<NT, SH, NM>(x, taps, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
             // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
@@ -2085,6 +2106,14 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
         const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
         tb.twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
     }
+    for (int i = tid; i < 192; i += nth) {
+        const int dir = i / 96, m = (i / 16) % 6, ii = i & 3, kk = (i >> 2) & 3;
+        const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
+        const double2 t0 = kW24[ea % 12];
+        const double2 v = ea >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+        tb.amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+    }
 }
 
 // Row tables of symbol block `blk` for the lanes tid < 24 of a wave-group: re-
@@ -2106,7 +2135,7 @@ __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, doub
 }
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
-template <int NT, int SH, int NP, bool TRACE>
+template <int NT, int SH, int NP, bool TRACE, bool NM = false>
 __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[4][24], wrow[4][24];
@@ -2115,11 +2144,11 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
     __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
     __shared__ int cntl[4][PM_MAXIT + 1];
-    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
     const int U = o.U, R = o.R;
     const int ug16 = xcd_remap(blockIdx.x, gridDim.x);     // 16-unit group
-    const int ul = l >> 2;
+    const int ul = NM ? l & 15 : l >> 2;
     const int unit = ug16 * 16 + ul, unit_mf = ug16 * 16 + (l & 15);
     const int rl = unit % R;
     const int snr = o.snr0 + (ug16 * 16) / R;
@@ -2142,8 +2171,8 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     // reloaded at the W -> W0 switch: 40 more VGPRs, 1.97 -> 2.28 ms per step)
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
     auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, true>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
-                                         Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    mic2_stages<NT, SH, NP, TRACE, true, NM>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
+                                             Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     // one atomic per (stage, edge) per block
     for (int i = tid; i < 2 * (ma.niter + 1); i += blockDim.x) {
@@ -2156,7 +2185,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
 }
 
 // 64 units x one data symbol per block (4 waves x 16 units)
-template <int NT, int SH, int NP, bool TRACE>
+template <int NT, int SH, int NP, bool TRACE, bool NM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __shared__ Mic2Tables tb;
@@ -2169,11 +2198,11 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     int ug, bi;
     band_block(ord, ma.nb, ug, bi);
     const int blk = ma.blks[bi];
-    const int tid = threadIdx.x, l = tid & 63, r = l & 3;
+    const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int U = o.U, R = o.R;
     const int snr = o.snr0 + (ug * WAVE) / R;
-    const int ul = l >> 2;
+    const int ul = NM ? l & 15 : l >> 2;
     const int unit = ug * WAVE + w * 16 + ul, unit_mf = ug * WAVE + w * 16 + (l & 15);
     const int rl = unit % R;
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
@@ -2201,8 +2230,8 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __syncthreads();
     auto A = [&](int var, int q, int j, int p) { return sbv[var][q][j][p]; };
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, false>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
-                                          row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    mic2_stages<NT, SH, NP, TRACE, false, NM>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
+                                              row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
     __syncthreads();
     for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
         const int s = i >> 1, edge = i & 1;
@@ -2493,7 +2522,7 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
 }
 
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd, int part) {
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     Mic2Args ma{};
     ma.bv = mm.Bv;
@@ -2514,7 +2543,9 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
         const dim3 grid(b.U / 16), blk(64 * mm.npb);
 #define LAUNCH_MP(NTV, SHV)                                                                                  \
     do {                                                                                                     \
-        if (b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true>), grid, blk, 0, s, sk, ma, o);        \
+        if (b.tr && nm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true>), grid, blk, 0, s, sk, ma, o);   \
+        else if (nm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, ma, o); \
         else hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false>), grid, blk, 0, s, sk, ma, o);            \
     } while (0)
         if (ch.ntap == 1) LAUNCH_MP(1, 0);
@@ -2529,7 +2560,9 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
         const dim3 grid((b.U / WAVE) * mm.ndb), blk(256);
 #define LAUNCH_MD(NTV, SHV)                                                                                  \
     do {                                                                                                     \
-        if (b.tr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o);     \
+        if (b.tr && nm) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, om, ma, o); \
+        else if (b.tr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o); \
+        else if (nm) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, om, ma, o); \
         else hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o);         \
     } while (0)
         if (ch.ntap == 1) LAUNCH_MD(1, 0);

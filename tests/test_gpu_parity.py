@@ -376,7 +376,8 @@ def test_stage_variants_agree(name):
     reads them (and the anchor / moment fallbacks), TX / channel / noisy Q^H as
     banded passes instead of k_txrx_fft, the TX symbols one realisation per
     lane (k_tx_symbols, the fallback for non-row-local precoders), k_pic_fft's
-    4-point network by DPP instead of on the matrix cores."""
+    4-point network by DPP instead of on the matrix cores (and k_mic_pilot /
+    k_mic_data's, with the tap GEMM's exchange by ds_bpermute)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -392,7 +393,8 @@ def test_stage_variants_agree(name):
                 {"noise_fuse": 0}, {"jakes_rpw": 1}, {"mmse_ic": 0},
                 {"jakes_win": 0}, {"txrx_fft": 0}, {"mmse_ic": 0, "fuse_stage": 0, "pic_chain": 0},
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
-                {"pic_net": 0, "mmse_ic": 0})
+                {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
+                {"mic_net": 0, "pic_net": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
