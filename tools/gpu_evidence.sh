@@ -14,7 +14,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out/smok
 tail -1 $out/smoke.log
 timeout -k 10 400 python -u bench.py > $out/bench.log 2>&1 || { echo bench_fail; tail -20 $out/bench.log; exit 1; }
 tail -1 $out/bench.log | cut -c1-400
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_stats" -- python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > $out/bench_prof.log 2>&1 || { echo prof_fail; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_stats" -- python3 bench.py --no-cpu-baseline --steps 30 --warmup 5 > $out/bench_prof.log 2>&1 || { echo prof_fail; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_fetch" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_fetch.log 2>&1 || { echo fetch_fail; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_write" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_write.log 2>&1 || { echo write_fail; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof_sq" -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $out/bench_sq.log 2>&1 || { echo sq_fail; exit 1; }
