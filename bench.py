@@ -263,8 +263,11 @@ def derive_limiter(pmc, achieved_tf, avg_ms):
       wait         = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES      (share of wave time stalled on a dependency)
       hbm          = HBM bytes per launch / launch time / 8 TB/s
       fp64         = achieved / 78.6 TF (VALU and MFMA FP64 share that peak)
-    The limiter is the largest utilisation when it reaches 0.7, else issue
-    latency."""
+      issue        = valu_issue + mfma_busy: f64 VALU and f64 MFMA instructions do
+                     not overlap on gfx950 (tools/ubench: a 4x4x4 MFMA beside f64
+                     FMAs costs the sum of both), so together they are one pipe
+    The limiter is the largest single utilisation when it reaches 0.7, else the
+    shared FP64 issue when VALU + MFMA reach 0.7, else issue latency."""
     if not pmc:
         return None
     sq = pmc.get("sq_per_launch") or {}
@@ -281,10 +284,15 @@ def derive_limiter(pmc, achieved_tf, avg_ms):
          "hbm": (pmc["hbm_bytes_per_launch"] / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9))
          if pmc.get("hbm_bytes_per_launch") and avg_ms else None,
          "fp64": achieved_tf / FP64_PEAK_TFLOPS if achieved_tf else None}
+    d["issue"] = d["valu_issue"] + d["mfma_busy"]
     util = {k: d[k] for k in ("valu_issue", "mfma_busy", "hbm") if d[k] is not None}
     top = max(util, key=util.get)
+    if util[top] < 0.7 and d["issue"] >= 0.7:
+        top, util["issue"] = "issue", d["issue"]      # neither alone, but together they fill the issue
     if util[top] >= 0.7:
-        d["limiter"] = {"valu_issue": "VALU issue", "mfma_busy": "matrix cores", "hbm": "HBM bandwidth"}[top]
+        d["limiter"] = {"issue": "FP64 issue: VALU %.2f + matrix cores %.2f of the SIMD's cycles (they share it)" % (
+                            d["valu_issue"], d["mfma_busy"]),
+                        "valu_issue": "VALU issue", "mfma_busy": "matrix cores", "hbm": "HBM bandwidth"}[top]
     else:
         d["limiter"] = "issue latency (%.1f waves/SIMD, %.0f %% of wave cycles stalled on dependencies)" % (
             d["waves_per_simd"], 100 * (d["wait_frac"] or 0))
