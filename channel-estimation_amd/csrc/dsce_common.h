@@ -92,7 +92,7 @@ struct Band {
     const double2* vals;
 };
 
-// The MMSE estimator W as pair tiles for k_wpair: per block the (row, column)
+// The MMSE estimator W as pair tiles for k_wpair3: per block the (row, column)
 // pairs q = c_local * rbp + r (r fastest, rbp = 24 or 32 rows) in tiles of 16,
 // each tile stored as [k-step][4 pilots][16 pairs] (one MFMA A operand per
 // k-step, one 16-byte load per lane).  Element of (pair q, pilot p):

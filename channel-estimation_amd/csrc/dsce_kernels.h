@@ -100,7 +100,7 @@ struct McBuffers {
     uint16_t* qe;     // [ND][U]   quantised symbol indices (estimate)
     uint16_t* qp;     // [ND][U]   quantised symbol indices (perfect CSI)
     uint16_t* sidr;   // [LK][R]   transmitted symbol index per data row (row-indexed sidx)
-    double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (mic2), or null
+    double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (k_mic_pilot -> k_mic_data), or null
     int hpa_stages;   // stages hpa holds
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
@@ -120,7 +120,7 @@ struct MmseK {
     const double2* Wpil;  // [var][snr][NP pilots][24 columns][NP]
     const double2* WdA;   // [var][snr][blk][2][NP/4][64] diag(W) rows, MFMA A layout
     const int* pil_c0;    // NP: first column of each pilot row's block
-    // structured MMSE IC (k_mic_fft): H_hat taps = Bv hP; null when not eligible
+    // structured MMSE IC (k_mic_pilot / k_mic_data): H_hat taps = Bv hP; null when not eligible
     const double2* Bv;    // [var][snr][ntap][N][NP]
     const double2* Bs;    // [var][snr][QH blk][ntap][NP]: Bv summed over each block's FFT window
     const int* pblk;      // QH blocks holding pilot rows (k_pilot_fft)

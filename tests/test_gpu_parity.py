@@ -302,7 +302,7 @@ def test_any_repetition_count(ofdm):
 
 
 def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
-    """build_mic keeps the structured MMSE IC (k_mic_fft: D_hat = Q' H_hat G)
+    """build_mic keeps the structured MMSE IC (k_mic_pilot / k_mic_data: D_hat = Q' H_hat G)
     only if Q' H_hat G reproduces EVERY entry of the thresholded W — the
     off-diagonal entries the IC subtraction uses (script:482-484), not just
     diag(D_hat).  At ZeroThreshold 1e-5 (instead of the script's 1e-8,
