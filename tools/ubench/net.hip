@@ -4,6 +4,8 @@
 //         select, DPP xor1, FMAs) with a unit on a lane quad
 //   mfma: the quarters on the four 16-lane rows, DFT-4 (twiddle folded into the
 //         per-sample A operand) as four v_mfma_f64_4x4x4f64 (re/im x two K halves)
+// build: hipcc -O3 --offload-arch=gfx950 -ffp-contract=off tools/ubench/net.hip -o tools/ubench/net
+// (on the box: tools/ubench/net > gpurun_out/net.txt; result in profiles/r03k_ubench_network.txt)
 // 8 independent chains per wave, cycles per chain-step per SIMD at 1..4 waves/SIMD.
 #include <hip/hip_runtime.h>
 #include <cstdio>
