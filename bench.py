@@ -77,12 +77,26 @@ def source_hash():
 # CPU baseline: the oracle (literal NumPy restatement of the reference's dense
 # formulation) on the GPU box's host cores, bounded sample, median of 3
 # ---------------------------------------------------------------------------
+# the oracle holds full(W) and full(W0) of every SNR point and scheme (complex,
+# LK^2 NP each): above this many bytes per process a leg times 1 and 2 SNR
+# points and extrapolates (C5: ~100 GB); C2 / C3 / C4 (0.4 / 1.9 / 1.9 GB) are
+# timed on the whole workload
+ORACLE_W_BYTES_MAX = 8e9
+
+
+def oracle_w_bytes(S, schemes):
+    return sum(2 * len(S.pn_time) * S.schemes[s]["G"].shape[1] ** 2 * len(S.schemes[s]["pilot_pos"]) * 16
+               for s in schemes)
+
+
 def cpu_baseline_leg(seconds, workload, index=0):
     """One process of the CPU baseline: oracle/refsim.simulate on single
-    realisations, 3 timed samples.  Workloads with many SNR points (C5: 16) hold
-    the oracle's full(W) of every SNR point and scheme (> 60 GB per process), so
-    there the per-realisation cost is measured at the first 1 and 2 SNR points
-    and extrapolated linearly to all of them (cost = shared + nsnr x per-SNR)."""
+    realisations of the whole workload (every SNR point, both CSI branches, all
+    IC iterations), 3 timed samples of seconds / 3 each.  Only a workload whose
+    full(W) exceeds ORACLE_W_BYTES_MAX per process (C5) times the first 1 and 2
+    SNR points and extrapolates: cost(nsnr) = c1 + (nsnr - 1) (c2 - c1) from the
+    medians, flagged invalid when the slope is not positive or the samples'
+    spread exceeds it."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import harness
     from oracle import refsim
@@ -108,10 +122,11 @@ def cpu_baseline_leg(seconds, workload, index=0):
             rates.append(n / el)
         return rates, n_total
 
-    out = {}
-    if nsnr <= 4:
+    out = {"snr_points": nsnr}
+    if oracle_w_bytes(S, schemes) <= ORACLE_W_BYTES_MAX:
         mm = [harness.oracle_mmse(S, s) for s in schemes]          # setup, untimed
         rates, reps = timed(S.pn_time, mm, seconds)
+        out["timed_snr_points"] = nsnr
     else:
         tc = refsim.time_correlation(S.N, chan["dt"], chan["fD"], chan["model"])
         R_vecH = refsim.correlation_matrix(S.N, chan["pdp_norm"], tc)
@@ -125,10 +140,21 @@ def cpu_baseline_leg(seconds, workload, index=0):
             cost[k] = [1.0 / x for x in r]
             reps += n
             del mm
-        # per sample: shared + nsnr x per-SNR cost from the 1- and 2-point samples
-        rates = [1.0 / (c1 + (nsnr - 1) * (c2 - c1)) for c1, c2 in zip(sorted(cost[1]), sorted(cost[2]))]
-        out["extrapolated"] = {"snr_points_timed": [1, 2], "snr_points": nsnr,
-                               "rates_1": [1.0 / c for c in cost[1]], "rates_2": [1.0 / c for c in cost[2]]}
+        c1, c2 = statistics.median(cost[1]), statistics.median(cost[2])
+        slope = c2 - c1
+        spread = max(max(cost[1]) - min(cost[1]), max(cost[2]) - min(cost[2]))
+        ok = slope > 0 and spread < slope
+        # one value per sample pairing around the medians' fit: the fit itself
+        # and the fits through the extreme samples (a spread, not a median of 3)
+        rates = [1.0 / (c1 + (nsnr - 1) * slope)] if ok else []
+        if ok:
+            lo, hi = min(cost[1]) + (nsnr - 1) * max(slope - spread, 0.0), max(cost[1]) + (nsnr - 1) * (slope + spread)
+            rates = [1.0 / hi, rates[0], 1.0 / lo] if lo > 0 else [1.0 / hi, rates[0]]
+        out["extrapolated"] = {"snr_points_timed": [1, 2], "snr_points": nsnr, "valid": ok,
+                               "cost_1snr_s": cost[1], "cost_2snr_s": cost[2], "slope_s_per_snr": slope,
+                               "sample_spread_s": spread,
+                               "model": "cost = c1 + (nsnr - 1) (c2 - c1), medians of 3 samples each; invalid when "
+                                        "c2 <= c1 or the spread of the samples exceeds c2 - c1"}
     import resource
     out.update({"rates": rates, "reps": reps,
                 "maxrss_bytes": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024})
@@ -183,17 +209,26 @@ def _wait_all(procs, timeout):
             progress("cpu baseline: %d of %d processes running" % (sum(p.poll() is None for p in procs), len(procs)))
 
 
+def _spread(x):
+    return {"median": statistics.median(x), "min": min(x), "max": max(x), "n": len(x)} if x else None
+
+
 def run_cpu_baseline(seconds, workload):
     """Two legs of the oracle on the host, each about seconds / 2: one process
     with single-threaded BLAS, and a pool of P such processes running at once
-    on disjoint realisations (P = the host share: OMP_NUM_THREADS on the GPU box
-    (16), else the CPUs this process may use).  Per-realisation NumPy work is
-    too small for BLAS threading (r02: 16 BLAS threads ran slower than one), so
-    the all-core baseline is the process pool: its value is the sum of the
-    processes' rates."""
+    on disjoint realisations.  P = the CPUs this job may use: the scheduler
+    affinity, capped by OMP_NUM_THREADS when it is set (the GPU box exports 16,
+    its CPU share, while the affinity mask shows the whole host) and by memory.
+    Per-realisation NumPy work is too small for BLAS threading (r02: 16 BLAS
+    threads ran slower than one), so the all-core baseline is the process pool:
+    its value is the sum of the processes' median rates.  Each leg reports the
+    median and the spread (min / max) of its 3 samples."""
     host = host_info()
-    pool = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or host.get("affinity") or host["nproc"]
-    pool = max(1, min(pool, host.get("affinity") or pool))
+    aff = host.get("affinity") or host["nproc"]
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    pool = max(1, min(aff, omp) if omp else aff)
+    reason = ("OMP_NUM_THREADS=%d (the job's CPU share) within an affinity of %d CPUs" % (omp, aff) if omp and omp < aff
+              else "the scheduler affinity (%d CPUs)" % aff)
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-leg", "--cpu-seconds", str(seconds / 2),
            "--config", workload]
     progress("cpu baseline: one process")
@@ -203,9 +238,15 @@ def run_cpu_baseline(seconds, workload):
     if one.returncode != 0:
         return None
     leg1 = json.loads(out1.strip().splitlines()[-1])
+    if not leg1["rates"]:
+        return {"value": None, "unit": "realisations/s", "kind": "port", "invalid": leg1.get("extrapolated")}
     # the pool within the host memory one command may use (the GPU box caps it at
     # ~270 GB; C5's oracle setup holds the dense W of three schemes per process)
-    pool = max(1, min(pool, int(HOST_MEM_BUDGET / max(leg1.get("maxrss_bytes", 1), 1))))
+    pmem = max(1, int(HOST_MEM_BUDGET / max(leg1.get("maxrss_bytes", 1), 1)))
+    if pmem < pool:
+        reason += ", capped to %d by memory (%.1f GB per process into %.0f GB)" % (
+            pmem, leg1.get("maxrss_bytes", 0) / 1e9, HOST_MEM_BUDGET / 1e9)
+        pool = pmem
     progress("cpu baseline: %d processes" % pool)
     procs = [subprocess.Popen(cmd + ["--leg-index", str(i + 1)], env=_leg_env(), stdout=subprocess.PIPE,
                               stderr=subprocess.DEVNULL, text=True) for i in range(pool)]
@@ -216,12 +257,23 @@ def run_cpu_baseline(seconds, workload):
         if pr.returncode != 0:
             return None
         legs.append(json.loads(out.strip().splitlines()[-1]))
+    if any(not l["rates"] for l in legs):
+        return None
     v1 = statistics.median(leg1["rates"])
     vp = sum(statistics.median(l["rates"]) for l in legs)
+    # the pool's spread: the sum over processes of each one's min / max sample
+    pool_spread = {"median": vp, "min": sum(min(l["rates"]) for l in legs),
+                   "max": sum(max(l["rates"]) for l in legs), "n": 3}
+    ext = leg1.get("extrapolated")
+    timed_all = ext is None
     return {"value": max(v1, vp), "unit": "realisations/s", "cores": pool if vp >= v1 else 1, "kind": "port",
-            "value_1t": v1, "value_pool": vp, "pool_processes": pool, "samples_1t": leg1["rates"],
-            "samples_pool": [l["rates"] for l in legs],
-            "extrapolated": leg1.get("extrapolated"),
+            "value_1t": v1, "value_pool": vp, "pool_processes": pool, "pool_reason": reason,
+            "one_process": _spread(leg1["rates"]), "pool": pool_spread,
+            "samples_1t": leg1["rates"], "samples_pool": [l["rates"] for l in legs],
+            "timed": "the whole workload (every SNR point)" if timed_all else
+                     "extrapolated from 1 and 2 SNR points (the oracle's full(W) of all %d exceeds %.0f GB per process)"
+                     % (leg1["snr_points"], ORACLE_W_BYTES_MAX / 1e9),
+            "extrapolated": ext,
             "label": "CPU restatement of reference algorithm, not MATLAB",
             "sample": "oracle/refsim.simulate (dense Q'HG zgemm, full(W) reshape-and-sum contraction, brute-force "
                       "nearest-neighbour detection, NumPy/OpenBLAS fp64, 1 BLAS thread per process) on %s: one "
@@ -247,6 +299,20 @@ def stored_pmc(kernel_tag, workload):
                 d.get("kernel", "k_wcontract") == kernel_tag:
             return d, "profiles/" + os.path.basename(f)
     return None, "no PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
+
+
+def stored_pmc_all(workload):
+    """The committed per-kernel-group PMC summary (profiles/*_pmc_all.json,
+    tools/prof_summary.py --all) of THIS source build and workload, or None."""
+    src = source_hash()
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_all.json")))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("source_hash") == src and d.get("workload") == workload:
+            return d.get("kernels"), "profiles/" + os.path.basename(f)
+    return None, "no per-kernel PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
 
 
 SIMDS = 1024                   # 256 CUs x 4 SIMDs (MI355X)
@@ -357,7 +423,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local
-    if world > 1:
+    # under a launcher (WORLD_SIZE set) the process group and the counters'
+    # all-reduce run at every world size, 1 included (the RCCL path exercised)
+    if env_world is not None:
         import torch
         import torch.distributed as dist
         # one rank per GPU; DSCE_DIST_BACKEND=gloo + more ranks than GPUs rehearses
@@ -403,12 +471,13 @@ def main():
     el = time.perf_counter() - t0
     if rank == 0:
         progress("%d timed steps: %.3f s" % (args.steps, el))
+    allreduce = None
     if dist:
         import torch
+        from dsce.parallel import allreduce_counts
         dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else "cpu"
-        ct = torch.from_numpy(counts).to(dev)
-        dist.all_reduce(ct)                 # the one exchange: BER counters (RCCL)
-        counts = ct.cpu().numpy()
+        allreduce = {}
+        counts = allreduce_counts(counts, dev, allreduce)     # the one exchange: BER counters (RCCL)
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
@@ -434,27 +503,69 @@ def main():
         f = cmac_per_rep * 8.0 * B * args.steps
         flops += f
         # matrix-core flops actually executed per counted flop: 3 real MFMAs per
-        # complex product in the 3M form
+        # complex product in the 3M form (the W contraction is that GEMM alone)
         executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and not mic_l else 1.0)
     paths = [sorted(p) for p in paths]
     work = {name: {"cmac_per_rep": eng.work_model(sid)[0], "mmse_kernel": mmse_kernel(set(paths[sid]))}
             for sid, name in enumerate(schemes)}
-    achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
-    exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None
+    achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None        # 8 flops per complex MAC
+    exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None         # what the matrix cores executed
+    # the roofline rate: the 8-flop algorithmic count for k_mic_data (a VALU /
+    # matrix-core mix, below the peak either way); for the 3M contraction the
+    # executed flops (its 8-flop equivalent rate exceeds the peak: VERDICT r03 #6)
+    roof_tf = achieved_tf if mic_l else exec_tf
     peak_meas = eng.fp64_mfma_peak()
     pmc, traffic_src = stored_pmc(kname, args.config)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     avg_ms = wc_ms / launches if launches else None
-    lim = derive_limiter(pmc, achieved_tf, avg_ms)
+    lim = derive_limiter(pmc, roof_tf, avg_ms)
     # the roof the kernel sits closer to: FP64 compute (MFMA / VALU share the
     # peak) or HBM (traffic from the stamped PMC pass)
     hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
-    bound = "hbm" if hbm_frac is not None and achieved_tf and hbm_frac > achieved_tf / FP64_PEAK_TFLOPS else "mfma"
+    bound = "hbm" if hbm_frac is not None and roof_tf and hbm_frac > roof_tf / FP64_PEAK_TFLOPS else "mfma"
+    # every timed kernel group on its own roofline (dsce_kernel_work: algorithmic
+    # flops and compulsory bytes per realisation), plus the step as a whole
+    pmc_all, pmc_all_src = stored_pmc_all(args.config)
     kernels = {}
+    step_flops = 0.0
+    modelled_ms = 0.0
     for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_pilot", "k_mic_data",
               "perfect_ic", "k_stage"):
         n, ms = eng.kernel_time(k)
-        kernels[k] = {"launches": n, "ms": round(ms, 3)}
+        if not n:
+            continue
+        fr, br = eng.kernel_work(k)
+        ent = {"launches": n, "ms_per_step": round(ms / args.steps, 4), "share": None,
+               "flops_per_rep": fr or None, "bytes_per_rep": br or None}
+        if fr and ms > 0:
+            tf = fr * B * args.steps / (ms * 1e-3) / 1e12
+            ent["tflops"] = round(tf, 3)
+            ent["frac_fp64"] = round(tf / FP64_PEAK_TFLOPS, 4)
+            step_flops += fr * B
+            modelled_ms += ms
+        if br and ms > 0:
+            gbs = br * B * args.steps / (ms * 1e-3) / 1e9
+            ent["algorithmic_gbs"] = round(gbs, 1)
+            ent["frac_hbm_algorithmic"] = round(gbs / HBM_PEAK_GBS, 4)
+        kp = (pmc_all or {}).get(k)
+        if kp and kp.get("hbm_bytes_per_launch") and ms > 0:
+            ent["traffic_per_launch"] = kp["hbm_bytes_per_launch"]
+            ent["frac_hbm_measured"] = round(kp["hbm_bytes_per_launch"] * n / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 4)
+            if kp.get("sq_per_launch"):
+                lk = derive_limiter({"sq_per_launch": kp["sq_per_launch"], "hbm_bytes_per_launch":
+                                     kp["hbm_bytes_per_launch"], "avg_duration_ns_rocprof": kp.get("avg_duration_ns_rocprof")},
+                                    ent.get("tflops"), ms / n)
+                if lk:
+                    ent["valu_issue"], ent["mfma_busy"], ent["limiter"] = lk["valu_issue"], lk["mfma_busy"], lk["limiter"]
+        kernels[k] = ent
+    tot_ms = sum(eng.kernel_time(k)[1] for k in kernels)
+    for k in kernels:
+        kernels[k]["share"] = round(eng.kernel_time(k)[1] / tot_ms, 4) if tot_ms else None
+    step_ms = el / args.steps * 1e3
+    step_roof = {"flops_per_step": step_flops, "tflops": step_flops / (step_ms * 1e-3) / 1e12 if step_ms else None,
+                 "frac_fp64": step_flops / (step_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if step_ms else None,
+                 "kernel_ms_modelled_share": modelled_ms / tot_ms if tot_ms else None,
+                 "note": "algorithmic flops of every modelled kernel group per step / wall time per step / 78.6 TF"}
     ber = {}
     for sid, name in enumerate(schemes):
         bits = eng.bits_per_rep(sid)
@@ -498,10 +609,13 @@ def main():
                                 "peaks 78.6 TF)") if mic_l else
                                ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
                                 "diag(D_hat) + detection in its epilogue)"),
-                     "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": (achieved_tf / FP64_PEAK_TFLOPS) if achieved_tf else None,
+                     "achieved": roof_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": (roof_tf / FP64_PEAK_TFLOPS) if roof_tf else None,
+                     "achieved_basis": "8 flops per complex MAC (algorithmic)" if mic_l else
+                                       "executed matrix-core flops (3M: 6 per complex MAC)",
+                     "achieved_algorithmic_8flop": achieved_tf, "achieved_executed": exec_tf,
                      "peak_measured": peak_meas,
-                     "frac_measured": (achieved_tf / peak_meas) if achieved_tf and peak_meas else None,
+                     "frac_measured": (roof_tf / peak_meas) if roof_tf and peak_meas else None,
                      # executed matrix-core flops / measured peak from the work model (W contraction), or the
                      # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (k_mic_data: only its tap GEMM
                      # runs on the matrix cores)
@@ -516,15 +630,18 @@ def main():
                                     "ntap x 24, diag(D_hat_prev) v 24, this stage's window sums ntap x NP and diag 24 "
                                     "(8 flops per CMAC) + two DFT-24 at 5 n log2 n flops") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
-                                    "fused diag(D_hat)), 8 real flops per CMAC; the 3M form executes 6 of the 8 counted "
-                                    "flops, so frac can exceed 1; mfma_busy = executed matrix-core flops / measured "
-                                    "peak"),
+                                    "fused diag(D_hat)); achieved / frac count the executed 6 flops per CMAC of the 3M "
+                                    "form, achieved_algorithmic_8flop the 8-flop equivalent; mfma_busy = executed "
+                                    "matrix-core flops / measured peak"),
                      "paths": paths,
                      "limiter": lim["limiter"] if lim else None,
                      "counters": lim},
         "cpu_baseline": cpu,
+        "allreduce": allreduce,
         "setup_s": setup_s,
-        "kernels_ms": kernels,
+        "kernels": kernels,
+        "step_roofline": step_roof,
+        "kernels_pmc_source": pmc_all_src,
         "work_per_scheme": work,
         "ber_last_snr": ber,
     }

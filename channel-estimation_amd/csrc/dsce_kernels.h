@@ -151,8 +151,11 @@ struct JakesChunks {
 // the anchor groups' limit: |theta k| <= JAKES_XMAX (the Taylor sum's terms grow
 // to e^x / sqrt(2 pi x) before they fall: x = 3 costs ~20x the per-term rounding)
 constexpr double JAKES_XMAX = 3.0;
-// jc: form only those chunks (samples outside stay as they are: zero)
-void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
+// jc: form only those chunks (samples outside stay as they are: zero).  Returns
+// which kernel ran (the work model of dsce_kernel_work): JAKES_KIND_GRP
+// k_jakes_grp, JAKES_KIND_MOM k_jakes_mom, else JAKES_KIND_OTHER.
+enum { JAKES_KIND_OTHER = 0, JAKES_KIND_MOM = 2, JAKES_KIND_GRP = 3 };
+int launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
                   double2* ir, const JakesChunks* jc = nullptr);
 // txrx (txrx_fft_ok): only the symbols; k_txrx_fft forms s, r0 and diag(D) in
 // launch_rx_front

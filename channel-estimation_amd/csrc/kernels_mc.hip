@@ -686,16 +686,16 @@ __global__ void __launch_bounds__(64) k_discrete(ChannelK ch, uint64_t seed, uin
     }
 }
 
-void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
+int launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t seed, uint64_t rep0, int R,
                   double2* ir, const JakesChunks* jc) {
     if (ch.fD == 0.0) {
         hipLaunchKernelGGL(k_static, dim3(R / WAVE, (ch.N + 63) / 64, ch.ntap), dim3(WAVE), 0, s, ch, seed, rep0, R, ir);
-        return;
+        return JAKES_KIND_OTHER;
     }
     if (ch.model >= 2) {
         hipLaunchKernelGGL(k_discrete, dim3(R / WAVE, (ch.N + DCH - 1) / DCH, ch.ntap), dim3(WAVE), 0, s, ch, seed,
                            rep0, R, ir);
-        return;
+        return JAKES_KIND_OTHER;
     }
     // only the samples some Q^H row reads (OFDM: the FFT windows): chunks of 24
     // aligned to them, two realisations per wave, a lane pair per chunk
@@ -713,7 +713,7 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
     if (jc->mt == MT_ && jc->lg == LG_) {                                                                    \
         hipLaunchKernelGGL((k_jakes_grp<MT_, LG_>), grid, dim3(256), lds, s, ch, seed, rep0, R, ir, jc->n0,  \
                            jc->grp, jc->ngrp);                                                               \
-        return;                                                                                              \
+        return JAKES_KIND_GRP;                                                                               \
     }
             LAUNCH_JGRP(16, 4) LAUNCH_JGRP(16, 8) LAUNCH_JGRP(16, 16)
             LAUNCH_JGRP(24, 4) LAUNCH_JGRP(24, 8) LAUNCH_JGRP(24, 16)
@@ -725,10 +725,10 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
             dim3 grid((jc->n + CPW - 1) / CPW, R / (4 * RPW), ch.ntap);
             hipLaunchKernelGGL((k_jakes_mom<RPW, 12>), grid, dim3(256), (size_t)4 * RPW * 3 * ch.paths * sizeof(double),
                                s, ch, seed, rep0, R, ir, jc->n0, jc->n);
-            return;
+            return JAKES_KIND_MOM;
         }
         launch_jakes_t<JakesChunks::LEN, 2, 2>(s, ch, seed, rep0, R, ir, jc->n0, jc->n);
-        return;
+        return JAKES_KIND_OTHER;
     }
     // two realisations per wave (32 lanes each) when that gives chunks of 9-20
     // samples (N 257-640) and R splits into blocks of 8; the LDS path tables
@@ -737,18 +737,18 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
     if (jch2 >= 9 && jch2 <= 20 && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024 &&
         op.jakes_rpw == 2) {
         switch (jch2) {
-            case 9: launch_jakes_t<9, 2>(s, ch, seed, rep0, R, ir); return;
-            case 10: launch_jakes_t<10, 2>(s, ch, seed, rep0, R, ir); return;
-            case 11: launch_jakes_t<11, 2>(s, ch, seed, rep0, R, ir); return;
-            case 12: launch_jakes_t<12, 2>(s, ch, seed, rep0, R, ir); return;
-            case 13: launch_jakes_t<13, 2>(s, ch, seed, rep0, R, ir); return;
-            case 14: launch_jakes_t<14, 2>(s, ch, seed, rep0, R, ir); return;
-            case 15: launch_jakes_t<15, 2>(s, ch, seed, rep0, R, ir); return;
-            case 16: launch_jakes_t<16, 2>(s, ch, seed, rep0, R, ir); return;
-            case 17: launch_jakes_t<17, 2>(s, ch, seed, rep0, R, ir); return;
-            case 18: launch_jakes_t<18, 2>(s, ch, seed, rep0, R, ir); return;
-            case 19: launch_jakes_t<19, 2>(s, ch, seed, rep0, R, ir); return;
-            default: launch_jakes_t<20, 2>(s, ch, seed, rep0, R, ir); return;
+            case 9: launch_jakes_t<9, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 10: launch_jakes_t<10, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 11: launch_jakes_t<11, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 12: launch_jakes_t<12, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 13: launch_jakes_t<13, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 14: launch_jakes_t<14, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 15: launch_jakes_t<15, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 16: launch_jakes_t<16, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 17: launch_jakes_t<17, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 18: launch_jakes_t<18, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            case 19: launch_jakes_t<19, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
+            default: launch_jakes_t<20, 2>(s, ch, seed, rep0, R, ir); return JAKES_KIND_OTHER;
         }
     }
     int jch = (ch.N + WAVE - 1) / WAVE;           // samples per lane: one wave covers N when N <= 1024
@@ -771,6 +771,7 @@ void launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t se
         case 15: launch_jakes_t<15>(s, ch, seed, rep0, R, ir); break;
         default: launch_jakes_t<16>(s, ch, seed, rep0, R, ir); break;
     }
+    return JAKES_KIND_OTHER;
 }
 
 // ---------------------------------------------------------------------------

@@ -23,9 +23,10 @@ EXPORTED = [
     "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
     "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse", "dsce_trace_unit_ex",
     "dsce_scheme_dims", "dsce_path_info", "dsce_set_option", "dsce_get_option", "dsce_fp64_mfma_peak",
+    "dsce_kernel_work", "dsce_structured_check",
 ]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # dsce_path_info bits (include/dsce.h DSCE_PATH_*)
 PATH_BITS = {
@@ -122,6 +123,8 @@ def load_library(path=None):
     lib.dsce_set_option.argtypes = [vp, C.c_char_p, C.c_int64]
     lib.dsce_get_option.argtypes = [vp, C.c_char_p, C.POINTER(C.c_int64)]
     lib.dsce_fp64_mfma_peak.argtypes = [vp, dp]
+    lib.dsce_kernel_work.argtypes = [vp, C.c_char_p, dp, dp]
+    lib.dsce_structured_check.argtypes = [vp, C.c_int32, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
         if name not in ("dsce_destroy", "dsce_last_error"):
@@ -384,6 +387,21 @@ class Engine:
         t = C.c_double()
         self._chk(self.lib.dsce_fp64_mfma_peak(self.h, C.byref(t)), "dsce_fp64_mfma_peak")
         return t.value
+
+    def kernel_work(self, name):
+        """(flops, bytes) per realisation of timed kernel group `name` (dsce_kernel_work;
+        0 = not modelled for the path that ran)."""
+        f = C.c_double()
+        b = C.c_double()
+        self._chk(self.lib.dsce_kernel_work(self.h, name.encode(), C.byref(f), C.byref(b)), "dsce_kernel_work")
+        return f.value, b.value
+
+    def structured_check(self, sid):
+        """build_mic's guard of the structured MMSE IC (dsce_structured_check): dict with
+        ratio (kept iff <= 1), dev (max |Q' H_hat G - W_thr|), wmax (max |W|), rtol."""
+        out = (C.c_double * 4)()
+        self._chk(self.lib.dsce_structured_check(self.h, int(sid), out), "dsce_structured_check")
+        return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3])
 
     def work_model(self, sid):
         cm = C.c_double()

@@ -32,14 +32,18 @@ def mround(x):
 
 # Interferer selection |D(pilot, :)| >= the (NrCanceled+1)-th largest corner
 # interference (IIC.m:72-73, :113-114) evaluated as in exact arithmetic: values
-# equal to the threshold up to TIE_RTOL count as equal.  At C4 ('Coding', 24 x 30)
-# the threshold falls inside a class of 8 interferers whose magnitudes are equal
-# in exact arithmetic; a plain floating-point >= keeps whichever of them the last
+# equal to the threshold up to TIE_RTOL count as equal.  For 'Coding' (C4 at
+# 24 x 30 and the 48 x 30 C5 geometry) the threshold falls inside a class of 8
+# interferers per pilot whose magnitudes are equal in exact arithmetic; nothing
+# else lies within 1e-6 of it, and 'Auxiliary' is unaffected
+# (tests/test_oracle_setup.py::test_tie_rtol_changes_only_the_c4_tie_class).
+# A plain floating-point >= keeps whichever of them the last
 # bits of the FFTs favour (MATLAB/FFTW's choice is unknowable offline), so every
 # restatement made a different choice.  With the tolerance all members of the
 # class are kept — deterministic, identical in the product and the oracle
 # (oracle/setup.py), and the reading of the reference's rule without rounding.
-# C4 results therefore use this precoder; against MATLAB's they are unpinned.
+# C4 / C5 'Coding' results therefore use this precoder; against MATLAB's they are
+# unpinned.
 TIE_RTOL = 1e-12
 
 

@@ -25,12 +25,17 @@ def shard_range(first_rep, n_rep, world, rank, align=64):
     return first_rep + lo, hi - lo
 
 
-def allreduce_counts(counts, device=None):
-    """Sum an int64 counter array over all ranks of the default process group."""
+def allreduce_counts(counts, device=None, info=None):
+    """Sum a counter array (int64 counts, fp64 MSE sums) over all ranks of the
+    default process group.  ``device``: where the reduction runs ('cuda' with
+    the nccl backend: RCCL over xGMI reads device tensors).  ``info`` (a dict)
+    receives the backend, the tensor's device and the world size of the call."""
     import torch
     import torch.distributed as dist
     t = torch.from_numpy(np.ascontiguousarray(counts))
     if device is not None:
         t = t.to(device)
     dist.all_reduce(t)
+    if info is not None:
+        info.update(backend=dist.get_backend(), device=str(t.device), world=dist.get_world_size())
     return t.cpu().numpy()

@@ -54,7 +54,11 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     device = 0
-    if world > 1:
+    # under a launcher (torch.distributed.run sets WORLD_SIZE) the process group
+    # and the all-reduce run at every world size, 1 included: the RCCL path of
+    # the counters is the same code with one rank or eight
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         import torch
         import torch.distributed as dist
         # DSCE_DIST_BACKEND=gloo rehearses on a one-GPU box (ranks share the device)
@@ -107,9 +111,11 @@ def main(argv=None):
             pw[:, s0:s0 + ns] = p_
         eng.close()
     extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world, "shard": a.shard}
-    if world > 1:
+    if distributed:
         dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else None
-        counts = allreduce_counts(counts, dev)                    # the one exchange
+        info = {}
+        counts = allreduce_counts(counts, dev, info)              # the one exchange
+        extra["allreduce"] = info
         if a.mse:
             err = allreduce_counts(err, dev)
             pw = allreduce_counts(pw, dev)
@@ -132,7 +138,7 @@ def main(argv=None):
     extra["realisations_per_s"] = reps / extra["seconds"]
     res = results.make(S, names, counts, bits, reps, a.seed, extra=extra)
     if rank != 0:
-        if world > 1:
+        if distributed:
             dist.destroy_process_group()
         return 0
     if a.out:
@@ -146,7 +152,7 @@ def main(argv=None):
                    "ber_ic_mmse": float(res["ber"][s]["mmse"]["all"][k][-1]),
                    "ber_onetap_mmse": float(res["ber"][s]["mmse"]["all"][k][0])} for s in names}
     print(json.dumps(summary))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0
 

@@ -39,6 +39,12 @@
  *   d      = dsce_mex('scheme_dims', id)                          % [N Ltap LK NP ND Nsym nSchemes nSNR nIter]
  *   f      = dsce_mex('path_info', id)                            % DSCE_PATH_* bits of the last run
  *   dsce_mex('set_option', name, value)
+ *   [G, Q] = dsce_mex('tx_matrices', ModObj)                       % ModObj: Modulation.OFDM or Modulation.FBMC
+ *            ('Hermite-OQAM'): G = ModObj.GetTXMatrix, Q = ModObj.GetRXMatrix' (script:191-195) computed
+ *            on the GPU from the object's Nr / PHY / Implementation / PrototypeFilter properties
+ *   dsce_mex('enable_mse', on)                                      % start (and reset) the MSE sums of 'run'
+ *   [err, pow] = dsce_mex('get_mse')                                % err [iter+1, snr, scheme], pow [snr, scheme]
+ *   c = dsce_mex('structured_check', id)                           % [ratio, max dev, max |W|, rtol] (dsce_structured_check)
  */
 #ifdef MATLAB_MEX_FILE
 #include <math.h>
@@ -389,6 +395,136 @@ static void c_set_option(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prh
     check(dsce_set_option(g_ctx, name, integer(prhs[2], 2, -1)), "dsce_set_option");
 }
 
+
+/* ---- Modulation.OFDM / Modulation.FBMC objects (tx_matrices) ------------------- */
+/* property `prop` (a struct) of the object, field `field` as a real scalar */
+static const mxArray* g_props[4];                 /* owned copies from mxGetProperty, freed by props_free */
+static int g_nprops = 0;
+static void props_free(void) {
+    int i;
+    for (i = 0; i < g_nprops; ++i) mxDestroyArray((mxArray*)g_props[i]);
+    g_nprops = 0;
+}
+static const mxArray* prop(const mxArray* obj, const char* name) {
+    mxArray* p = mxGetProperty(obj, 0, name);            /* a copy (MATLAB semantics) */
+    if (!p || !mxIsStruct(p)) {
+        if (p) mxDestroyArray(p);
+        props_free();
+        mexErrMsgIdAndTxt("dsce:args", "dsce_mex('tx_matrices'): the object has no struct property %s", name);
+    }
+    g_props[g_nprops++] = p;
+    return p;
+}
+static double field(const mxArray* st, const char* name) {
+    const mxArray* f = mxGetField(st, 0, name);
+    if (!f || !mxIsNumeric(f) || mxIsComplex(f) || mxGetNumberOfElements(f) != 1) {
+        props_free();
+        mexErrMsgIdAndTxt("dsce:args", "dsce_mex('tx_matrices'): field %s must be a real scalar", name);
+    }
+    return mxGetScalar(f);
+}
+
+static void c_tx_matrices(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* OFDM.m:184-218 / FBMC.m:318-354 on the GPU (dsce_tx_matrices, row f1) */
+    const mxArray* obj = prhs[1];
+    const mxArray *nr, *phy, *im, *pf, *td;
+    mxArray* meth;
+    dsce_tx_desc d;
+    cplx_out og, oq;
+    double *zg, *zq;
+    size_t lk;
+    int fbmc, rc;
+    (void)nrhs;
+    if (mxIsClass(obj, "Modulation.OFDM")) fbmc = 0;
+    else if (mxIsClass(obj, "Modulation.FBMC")) fbmc = 1;
+    else bad(1, "a Modulation.OFDM or Modulation.FBMC object");
+    memset(&d, 0, sizeof d);
+    nr = prop(obj, "Nr");
+    phy = prop(obj, "PHY");
+    im = prop(obj, "Implementation");
+    if (field(phy, "TransmitRealSignal") != 0.0) {
+        props_free();
+        mexErrMsgIdAndTxt("dsce:args", "dsce_mex('tx_matrices'): PHY.TransmitRealSignal must be false (OFDM.m:188-191)");
+    }
+    d.kind = fbmc;
+    d.n_subcarriers = (int32_t)field(nr, "Subcarriers");
+    d.n_symbols = (int32_t)field(nr, "MCSymbols");
+    d.n_samples = (int32_t)field(nr, "SamplesTotal");
+    d.fft_size = (int32_t)field(im, "FFTSize");
+    d.intermediate_bin = (int32_t)field(im, "IntermediateFrequency");
+    d.time_spacing = (int32_t)field(im, "TimeSpacing");
+    d.norm = field(im, "NormalizationFactor");
+    if (fbmc) {
+        char m[32];
+        meth = mxGetProperty(obj, 0, "Method");
+        if (!meth || mxGetString(meth, m, sizeof m) || strcmp(m, "Hermite-OQAM")) {
+            if (meth) mxDestroyArray(meth);
+            props_free();
+            mexErrMsgIdAndTxt("dsce:args", "dsce_mex('tx_matrices'): FBMC Method must be 'Hermite-OQAM'");
+        }
+        mxDestroyArray(meth);
+        pf = prop(obj, "PrototypeFilter");
+        td = mxGetField(pf, 0, "TimeDomain");
+        if (!td || !mxIsDouble(td) || mxIsComplex(td)) {
+            props_free();
+            mexErrMsgIdAndTxt("dsce:args", "dsce_mex('tx_matrices'): PrototypeFilter.TimeDomain must be real");
+        }
+        d.proto_len = (int32_t)mxGetNumberOfElements(td);
+        d.prototype = DSCE_DOUBLES(td);
+        d.initial_phase = field(im, "InitialPhaseShift");
+        d.rx_scale = field(nr, "Subcarriers") / (field(phy, "SamplingRate") * field(phy, "TimeSpacing"));   /* FBMC.m:352 */
+    } else {
+        d.cyclic_prefix = (int32_t)field(im, "CyclicPrefix");
+        d.zero_guard = (int32_t)field(im, "ZeroGuardSamples");
+        d.rx_scale = field(nr, "Subcarriers") * field(phy, "SubcarrierSpacing") / field(phy, "SamplingRate");  /* OFDM.m:214 */
+    }
+    lk = (size_t)d.n_subcarriers * (size_t)d.n_symbols;
+    plhs[0] = mxCreateDoubleMatrix((mwSize)d.n_samples, (mwSize)lk, mxCOMPLEX);
+    zg = out_begin(&og, plhs[0]);
+    zq = NULL;
+    if (nlhs > 1) {
+        plhs[1] = mxCreateDoubleMatrix((mwSize)d.n_samples, (mwSize)lk, mxCOMPLEX);
+        zq = out_begin(&oq, plhs[1]);
+    }
+    rc = dsce_tx_matrices(g_ctx, &d, zg, zq);
+    out_end(&og);
+    if (nlhs > 1) out_end(&oq);
+    props_free();
+    check(rc, "dsce_tx_matrices");
+}
+
+static void c_enable_mse(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    (void)nlhs; (void)plhs; (void)nrhs;
+    check(dsce_enable_mse(g_ctx, (int32_t)integer(prhs[1], 1, 0)), "dsce_enable_mse");
+}
+
+static void c_get_mse(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    /* C-ordered err [scheme][snr][stage], pow [scheme][snr]: reversed dims in MATLAB */
+    const dsce_dims d = dims_of(0);
+    mwSize de[3];
+    mxArray* pw;
+    (void)nrhs; (void)prhs;
+    de[0] = (mwSize)(d.n_iter + 1); de[1] = (mwSize)d.n_snr; de[2] = (mwSize)d.n_schemes;
+    plhs[0] = mxCreateNumericArray(3, de, mxDOUBLE_CLASS, mxREAL);
+    pw = mxCreateDoubleMatrix((mwSize)d.n_snr, (mwSize)d.n_schemes, mxREAL);
+    {
+        const int rc = dsce_get_mse(g_ctx, DSCE_DOUBLES(plhs[0]), DSCE_DOUBLES(pw));
+        if (rc != 0) mxDestroyArray(pw);
+        check(rc, "dsce_get_mse");
+    }
+    if (nlhs > 1) plhs[1] = pw;
+    else mxDestroyArray(pw);
+}
+
+static void c_structured_check(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    double c[4];
+    int k;
+    (void)nlhs; (void)nrhs;
+    check(dsce_structured_check(g_ctx, scheme_id(prhs[1], 1), c), "dsce_structured_check");
+    plhs[0] = mxCreateDoubleMatrix(1, 4, mxREAL);
+    for (k = 0; k < 4; ++k) DSCE_DOUBLES(plhs[0])[k] = c[k];
+}
+
 static const struct {
     const char* name;
     int nrhs_min, nrhs_max, nlhs;
@@ -410,6 +546,10 @@ static const struct {
     {"scheme_dims", 2, 2, 1, c_scheme_dims},
     {"path_info", 2, 2, 1, c_path_info},
     {"set_option", 3, 3, 0, c_set_option},
+    {"tx_matrices", 2, 2, 2, c_tx_matrices},
+    {"enable_mse", 2, 2, 0, c_enable_mse},
+    {"get_mse", 1, 1, 2, c_get_mse},
+    {"structured_check", 2, 2, 1, c_structured_check},
 };
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {

@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 4
+#define DSCE_ABI_VERSION 5
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
@@ -168,7 +168,10 @@ typedef struct {
 
 /* Per-stage trace of one unit (dsce_trace_unit_ex).  Every pointer is optional
  * (null: not returned).  Complex buffers interleaved; "stage" s = 0 one-tap,
- * s = i IC iteration i; (1 + n_iter) rows, each LK (or NP / ND) long. */
+ * s = i IC iteration i; (1 + n_iter) rows, each LK (or NP / ND) long.
+ * Entries no kernel of the path forms are NaN (since ABI 4; ABI 3 left 0):
+ * e.g. the pilot rows of yperf_stages on the fused perfect-CSI paths, and
+ * hest_stages / yest_stages rows of symbols a stage kernel does not visit. */
 typedef struct {
     double* y;                  /* LK: y = Q'r                                    script:406-409 */
     double* h_perfect;          /* LK: diag(D), D = Q'HG                           script:388-393 */
@@ -326,6 +329,23 @@ int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, doubl
  * into it, the diag(D_hat) = Wd hP products) and the number of W bytes streamed
  * per contraction launch. */
 int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per_rep, double* w_bytes_per_snr);
+/* Algorithmic work per realisation of one timed kernel group (the names of
+ * dsce_kernel_time) as configured by the last dsce_run, summed over the
+ * schemes that ran it: flops (8 per complex multiply-accumulate, 5 n log2 n per
+ * n-point DFT; transcendentals and RNG integer work not counted) and the
+ * compulsory HBM bytes (each operand read once per realisation / unit, each
+ * result written once).  Modelled: the FFT-form OFDM chain (k_jakes, tx,
+ * rx_front, perfect_ic, k_mic_pilot, k_mic_data) and the W contraction
+ * (k_wcontract); 0 = not modelled for the path that ran.  DESIGN.md section 4
+ * lists the per-unit formulas. */
+int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, double* bytes_per_rep);
+/* The guard of the structured MMSE IC (D_hat = Q' H_hat G, DSCE_PATH_MIC_FFT),
+ * evaluated at dsce_build_mmse: out[0] = worst over the (variant, SNR) slices of
+ * max |Q' H_hat G - W_thr| / (out[3] max |W|) over every entry the IC uses
+ * (the path is kept iff <= 1), out[1] = the largest absolute deviation, out[2]
+ * = the largest |W|, out[3] = the relative tolerance (rounding level, 1e-11).
+ * out[0..2] = -1 when the scheme is not eligible (the W contraction runs). */
+int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out4);
 /* Measured FP64 matrix-core peak of the context's GPU: back-to-back
  * v_mfma_f64_16x16x4_f64 on independent accumulators, 8 waves per SIMD,
  * best of 3 timed launches (TFLOP/s). */

@@ -331,8 +331,9 @@ def _hadamard(n):
 
 
 # The interferer threshold of IIC.m:72-73 / :113-114 in exact-arithmetic
-# semantics: magnitudes equal to it up to TIE_RTOL count as >= (at C4 it falls
-# inside a class of 8 interferers equal in exact arithmetic, whose floating-point
+# semantics: magnitudes equal to it up to TIE_RTOL count as >= (for 'Coding' at C4
+# and C5 it falls inside a class of 8 interferers per pilot equal in exact
+# arithmetic, whose floating-point
 # order is an FFT rounding accident; MATLAB's own choice is unknowable offline).
 # The product mirror uses the same rule (dsce/estimation.py TIE_RTOL).
 TIE_RTOL = 1e-12

@@ -41,6 +41,35 @@ static mxArray* Lg(size_t n) {
     return a;
 }
 
+/* Modulation.OFDM / Modulation.FBMC objects with the properties dsce_mex's
+ * tx_matrices reads (OFDM.m:53-88, FBMC.m:61-160 field names; C2 / C3 values) */
+static mxArray* St(int n, const char* const* nm, mxArray** v) { return tst_struct(n, nm, v); }
+static mxArray* ofdm_object(int real_signal) {
+    const char* nn[] = {"Subcarriers", "MCSymbols", "SamplesTotal"};
+    mxArray* nv[] = {D(24), D(14), D(540)};
+    const char* pn[] = {"TransmitRealSignal", "SubcarrierSpacing", "SamplingRate"};
+    mxArray* pv[] = {D(real_signal), D(15e3), D(360e3)};
+    const char* in[] = {"FFTSize", "IntermediateFrequency", "TimeSpacing", "NormalizationFactor", "CyclicPrefix",
+                        "ZeroGuardSamples"};
+    mxArray* iv[] = {D(24), D(0), D(26), D(1.0), D(2), D(88)};
+    const char* on[] = {"Nr", "PHY", "Implementation"};
+    mxArray* ov[] = {St(3, nn, nv), St(3, pn, pv), St(6, in, iv)};
+    return tst_object("Modulation.OFDM", 3, on, ov);
+}
+static mxArray* fbmc_object(const char* method) {
+    const char* nn[] = {"Subcarriers", "MCSymbols", "SamplesTotal"};
+    mxArray* nv[] = {D(24), D(30), D(540)};
+    const char* pn[] = {"TransmitRealSignal", "SubcarrierSpacing", "SamplingRate", "TimeSpacing"};
+    mxArray* pv[] = {D(0), D(15e3), D(360e3), D(12.0 / 360e3)};
+    const char* in[] = {"FFTSize", "IntermediateFrequency", "TimeSpacing", "NormalizationFactor", "InitialPhaseShift"};
+    mxArray* iv[] = {D(24), D(0), D(12), D(1.0), D(0)};
+    const char* fn[] = {"TimeDomain"};
+    mxArray* fv[] = {M(192, 1, 0)};
+    const char* on[] = {"Nr", "PHY", "Implementation", "PrototypeFilter", "Method"};
+    mxArray* ov[] = {St(3, nn, nv), St(4, pn, pv), St(5, in, iv), St(1, fn, fv), S(method)};
+    return tst_object("Modulation.FBMC", 5, on, ov);
+}
+
 static mxArray* g_last_out;
 
 static void call(const char* tag, int nlhs, int nrhs, mxArray** in) {
@@ -112,6 +141,8 @@ static mxArray* default_arg(const char* cmd, int pos) {
     if (!strcmp(cmd, "set_noise_slot")) return D(pos == 1 ? 1 : 0);
     if (!strcmp(cmd, "set_interpolation")) return pos == 2 ? M(336, 16, 0) : D(1);
     if (!strcmp(cmd, "set_option")) return pos == 1 ? S("xcd") : D(1);
+    if (!strcmp(cmd, "tx_matrices")) return ofdm_object(0);
+    if (!strcmp(cmd, "enable_mse")) return D(1);
     return D(1);   /* bits_per_rep, scheme_dims, path_info: scheme id 1 */
 }
 
@@ -187,6 +218,27 @@ int main(int argc, char** argv) {
     call("set_channel", 0, 7, a);
     a[3] = D(540.5);
     call("set_channel_fractional_N", 0, 7, a);
+    a[0] = S("tx_matrices"); a[1] = ofdm_object(0);
+    call("tx_matrices_ofdm", 2, 2, a);
+    check_out("tx_matrices", 0);
+    a[1] = fbmc_object("Hermite-OQAM");
+    call("tx_matrices_fbmc", 1, 2, a);
+    check_out("tx_matrices_fbmc", 0);
+    a[1] = D(1);
+    call("tx_matrices_not_object", 1, 2, a);
+    a[1] = ofdm_object(1);
+    call("tx_matrices_real_signal", 2, 2, a);
+    a[1] = fbmc_object("PHYDYAS-OQAM");
+    call("tx_matrices_phydyas", 1, 2, a);
+    a[1] = ofdm_object(0);
+    call("tx_matrices_3_outputs", 3, 2, a);
+    a[0] = S("enable_mse"); a[1] = D(1);
+    call("enable_mse", 0, 2, a);
+    a[0] = S("get_mse");
+    call("get_mse", 2, 1, a);
+    call("get_mse_extra_arg", 2, 2, a);
+    a[0] = S("structured_check"); a[1] = D(1);
+    call("structured_check", 1, 2, a);
     a[0] = S("no_such_command");
     call("unknown", 0, 1, a);
     a[0] = S("destroy");

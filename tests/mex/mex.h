@@ -22,7 +22,7 @@
 
 typedef size_t mwSize;
 typedef bool mxLogical;
-typedef enum { mxDOUBLE_CLASS, mxINT64_CLASS, mxLOGICAL_CLASS, mxCHAR_CLASS } mxClassID;
+typedef enum { mxDOUBLE_CLASS, mxINT64_CLASS, mxLOGICAL_CLASS, mxCHAR_CLASS, mxSTRUCT_CLASS, mxOBJECT_CLASS } mxClassID;
 typedef enum { mxREAL, mxCOMPLEX } mxComplexity;
 typedef struct { double real, imag; } mxComplexDouble;
 typedef struct mxArray_tag {
@@ -31,7 +31,10 @@ typedef struct mxArray_tag {
     size_t m, n;
     void* data;          /* interleaved API: (re, im) pairs; split API: real plane */
     void* imag;          /* split API: imaginary plane of a complex array */
-    char* str;
+    char* str;           /* char arrays; objects: the class name */
+    int nfields;         /* struct (1 x 1) / object: named fields / properties */
+    char** fnames;
+    struct mxArray_tag** fvals;
 } mxArray;
 
 int mxGetString(const mxArray* a, char* buf, mwSize len);
@@ -63,6 +66,12 @@ mxArray* mxCreateNumericArray(mwSize nd, const mwSize* dims, mxClassID cls, mxCo
 void* mxMalloc(size_t n);
 void mxFree(void* p);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
+/* structs and classdef objects (scalar): mxGetProperty returns a copy the
+   caller destroys, mxGetField the struct's own field */
+bool mxIsStruct(const mxArray* a);
+bool mxIsClass(const mxArray* a, const char* name);
+mxArray* mxGetProperty(const mxArray* a, mwSize index, const char* name);
+mxArray* mxGetField(const mxArray* a, mwSize index, const char* name);
 int mexAtExit(void (*fn)(void));
 void mexLock(void);
 void mexUnlock(void);
@@ -70,4 +79,7 @@ void mexUnlock(void);
 /* test helpers (driver.c / mex_stub.c): element k of a complex array, either API */
 void tst_get_c(const mxArray* a, size_t k, double* re, double* im);
 void tst_set_c(mxArray* a, size_t k, double re, double im);
+/* a scalar struct / object with n named fields (the values are owned by it) */
+mxArray* tst_struct(int n, const char* const* names, mxArray** values);
+mxArray* tst_object(const char* cls, int n, const char* const* names, mxArray** values);
 #endif

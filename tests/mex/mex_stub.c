@@ -79,8 +79,19 @@ bool mxIsLogical(const mxArray* a) { return a->cls == mxLOGICAL_CLASS; }
 bool mxIsChar(const mxArray* a) { return a->cls == mxCHAR_CLASS; }
 mxArray* mxDuplicateArray(const mxArray* a) {
     mxArray* b = mk(a->cls, a->cplx, a->m, a->n);
-    memcpy(b->data, a->data, a->m * a->n * elsize(a));
+    /* char arrays keep their text in str (driver.c S()), data is a 1-byte dummy */
+    if (a->cls != mxCHAR_CLASS) memcpy(b->data, a->data, a->m * a->n * elsize(a));
     if (a->imag) memcpy(b->imag, a->imag, a->m * a->n * 8);
+    if (a->str) b->str = strdup(a->str);
+    if (a->nfields) {
+        b->nfields = a->nfields;
+        b->fnames = calloc(a->nfields, sizeof(char*));
+        b->fvals = calloc(a->nfields, sizeof(mxArray*));
+        for (int i = 0; i < a->nfields; ++i) {
+            b->fnames[i] = strdup(a->fnames[i]);
+            b->fvals[i] = mxDuplicateArray(a->fvals[i]);
+        }
+    }
     return b;
 }
 #if MX_HAS_INTERLEAVED_COMPLEX
@@ -95,7 +106,47 @@ int mxMakeArrayComplex(mxArray* a) {
     return 1;
 }
 #endif
-void mxDestroyArray(mxArray* a) { if (a) { free(a->data); free(a->imag); free(a->str); free(a); } }
+void mxDestroyArray(mxArray* a) {
+    if (!a) return;
+    for (int i = 0; i < a->nfields; ++i) {
+        free(a->fnames[i]);
+        mxDestroyArray(a->fvals[i]);
+    }
+    free(a->fnames);
+    free(a->fvals);
+    free(a->data); free(a->imag); free(a->str); free(a);
+}
+mxArray* tst_struct(int n, const char* const* names, mxArray** values) {
+    mxArray* a = mk(mxSTRUCT_CLASS, 0, 1, 1);
+    a->nfields = n;
+    a->fnames = calloc(n ? n : 1, sizeof(char*));
+    a->fvals = calloc(n ? n : 1, sizeof(mxArray*));
+    for (int i = 0; i < n; ++i) {
+        a->fnames[i] = strdup(names[i]);
+        a->fvals[i] = values[i];
+    }
+    return a;
+}
+mxArray* tst_object(const char* cls, int n, const char* const* names, mxArray** values) {
+    mxArray* a = tst_struct(n, names, values);
+    a->cls = mxOBJECT_CLASS;
+    a->str = strdup(cls);
+    return a;
+}
+bool mxIsStruct(const mxArray* a) { return a->cls == mxSTRUCT_CLASS; }
+bool mxIsClass(const mxArray* a, const char* name) { return a->cls == mxOBJECT_CLASS && !strcmp(a->str, name); }
+static mxArray* find_field(const mxArray* a, const char* name) {
+    for (int i = 0; i < a->nfields; ++i)
+        if (!strcmp(a->fnames[i], name)) return a->fvals[i];
+    return NULL;
+}
+mxArray* mxGetField(const mxArray* a, mwSize index, const char* name) {
+    return (a->cls == mxSTRUCT_CLASS && index == 0) ? find_field(a, name) : NULL;
+}
+mxArray* mxGetProperty(const mxArray* a, mwSize index, const char* name) {
+    mxArray* v = (a->cls == mxOBJECT_CLASS && index == 0) ? find_field(a, name) : NULL;
+    return v ? mxDuplicateArray(v) : NULL;
+}
 mxArray* mxCreateDoubleScalar(double v) { mxArray* a = mk(mxDOUBLE_CLASS, 0, 1, 1); ((double*)a->data)[0] = v; return a; }
 mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity c) { return mk(mxDOUBLE_CLASS, c == mxCOMPLEX, m, n); }
 mxArray* mxCreateNumericArray(mwSize nd, const mwSize* dims, mxClassID cls, mxComplexity c) {
@@ -207,3 +258,37 @@ int dsce_set_interpolation(dsce_ctx* c, int32_t id, const double* I) {
 }
 int dsce_path_info(dsce_ctx* c, int32_t id, uint32_t* f) { (void)c; (void)id; *f = 0x0f; return 0; }
 int dsce_set_option(dsce_ctx* c, const char* n, int64_t v) { (void)c; printf("  set_option %s=%lld\n", n, (long long)v); return 0; }
+
+/* tx_matrices: the descriptor must carry the object's fields as the driver set
+   them (driver.c ofdm_object / fbmc_object); G / Q written in full (N x LK) */
+int dsce_tx_matrices(dsce_ctx* c, const dsce_tx_desc* d, double* G, double* Q) {
+    (void)c;
+    const size_t n = (size_t)d->n_samples * d->n_subcarriers * d->n_symbols;
+    int ok;
+    if (d->kind == 0)
+        ok = d->n_subcarriers == 24 && d->n_symbols == 14 && d->n_samples == 540 && d->fft_size == 24 &&
+             d->time_spacing == 26 && d->cyclic_prefix == 2 && d->zero_guard == 88 && d->prototype == NULL &&
+             d->norm == 1.0 && d->rx_scale == 24.0 * 15e3 / 360e3;
+    else
+        ok = d->n_subcarriers == 24 && d->n_symbols == 30 && d->n_samples == 540 && d->fft_size == 24 &&
+             d->time_spacing == 12 && d->proto_len == 192 && d->prototype && d->prototype[191] == 1.0 + 191 % 7 &&
+             d->initial_phase == 0.0 && d->rx_scale == 24.0 / (360e3 * (12.0 / 360e3));
+    printf("  check tx_matrices desc %s\n", ok ? "OK" : "BAD");
+    for (size_t i = 0; i < 2 * n; ++i) G[i] = (double)i;      /* element k = 2k + (2k+1) j */
+    if (Q)
+        for (size_t i = 0; i < 2 * n; ++i) Q[i] = (double)i;
+    return 0;
+}
+int dsce_enable_mse(dsce_ctx* c, int32_t on) { (void)c; printf("  enable_mse %d\n", on); return 0; }
+int dsce_get_mse(dsce_ctx* c, double* err, double* pw) {
+    (void)c;
+    for (int i = 0; i < SSNR * (SIT + 1); ++i) err[i] = 0.5 * i;
+    for (int i = 0; i < SSNR; ++i) pw[i] = 1.0 + i;
+    return 0;
+}
+int dsce_structured_check(dsce_ctx* c, int32_t id, double* out) {
+    (void)c;
+    if (id != 0) return DSCE_EINVAL;
+    out[0] = 0.07; out[1] = 3e-13; out[2] = 0.59; out[3] = 1e-11;
+    return 0;
+}

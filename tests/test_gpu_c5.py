@@ -94,3 +94,19 @@ def test_c5_fbmc_matches_oracle(name):
     path = eng.path_info(0)
     assert ("stage_split" in path) == (name == "fbmc_cod") and "pic_passes" in path, path
     eng.close()
+
+
+@pytest.mark.parametrize("name", ["ofdm", "fbmc_aux", "fbmc_cod"])
+def test_c5_counts_at_plot_point_and_low_snr(name):
+    """C5 counts of every scheme at the script's
+    PlotIteration point, 32 dB (script:42-46: Figure 5's SNR), and at a low-SNR
+    point, 10 dB (the first of the 16-point sweep), against the oracle with D_hat
+    formed from W's stored non-zeros (refsim.simulate w_sparse); 32 realisations
+    per point, one-tap + 4 IC iterations, both CSI branches, with and without
+    edges.  The bench's kernels (TRACE = false instantiations) produce these
+    counts; the per-element traces above cover the TRACE = true ones."""
+    S = harness.setup("c5", schemes=(name,), snr_db=[10.0, 32.0])
+    eng = harness.engine(S, batch=64)
+    cg = _check_counts(S, name, eng, 128, 32, w_sparse=True)
+    assert np.all(cg[0, :, 0, 0, 0] > cg[0, :, 0, 1, 0])      # fewer errors at 32 dB than at 10 dB (one-tap)
+    eng.close()

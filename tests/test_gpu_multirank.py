@@ -80,3 +80,27 @@ def test_bench_gpus_flag_launches_ranks():
     bad = subprocess.run([sys.executable, os.path.join(harness.ROOT, "bench.py"), "--gpus", "2"],
                          env=dict(env, WORLD_SIZE="1"), timeout=120, capture_output=True, text=True)
     assert bad.returncode != 0
+
+
+def test_rccl_allreduce_one_rank(tmp_path):
+    """The counter all-reduce on the RCCL path (backend 'nccl' = RCCL on ROCm,
+    device tensors), exercised on the one-GPU box: dsce.simulate under
+    torch.distributed.run --nproc-per-node 1 with the default backend reports an
+    all-reduce over nccl on a cuda tensor and returns exactly the counts and MSE
+    sums of the plain single-process run.  The same code path carries the 8-rank
+    run of SURVEY §8e; only the world size differs."""
+    args = ["--config", "default", "--schemes", "ofdm", "--reps", "512", "--batch", "256", "--mse"]
+    env = {k: v for k, v in os.environ.items() if k != "DSCE_DIST_BACKEND"}
+    env["PYTHONPATH"] = harness.PKG
+    one, ranked = tmp_path / "one.json", tmp_path / "rccl.json"
+    subprocess.run([sys.executable, "-m", "dsce.simulate", *args, "--out", str(one)], cwd=harness.PKG, env=env,
+                   check=True, timeout=240, capture_output=True)
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                    "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "dsce.simulate", *args,
+                    "--out", str(ranked)], cwd=harness.PKG, env=env, check=True, timeout=240, capture_output=True)
+    a, b = json.load(open(one)), json.load(open(ranked))
+    ar = b["allreduce"]
+    assert ar["backend"] == "nccl" and ar["device"].startswith("cuda") and ar["world"] == 1, ar
+    assert "allreduce" not in a
+    assert np.array_equal(np.array(a["counts"]), np.array(b["counts"]))
+    np.testing.assert_array_equal(np.array(a["nmse"]["ofdm"]), np.array(b["nmse"]["ofdm"]))

@@ -227,11 +227,17 @@ def test_fbmc_error_counts(fbmc):
     res = harness.simulate(S, SEED, 64, 64, [name])
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
     _check_mse(eng, res)
+    err64, pw64 = eng.mse()
+    # ragged runs (padding lanes of a partial wave count nothing, neither in the
+    # counters nor in the MSE sums of any FBMC stage kernel): the same 64
+    # realisations as 25 + 39, and as 1 + 63
+    for a, b in ((25, 39), (1, 63)):
+        eng.enable_mse()                                # resets the sums
+        np.testing.assert_array_equal(eng.run(SEED, 64, a) + eng.run(SEED, 64 + a, b), cg)
+        err, pw = eng.mse()
+        np.testing.assert_allclose(err, err64, rtol=1e-12, atol=0)
+        np.testing.assert_allclose(pw, pw64, rtol=1e-12, atol=0)
     eng.enable_mse(False)
-    # ragged runs (padding lanes of a partial wave count nothing): the same
-    # 64 realisations as 25 + 39, and as 1 + 63
-    np.testing.assert_array_equal(eng.run(SEED, 64, 25) + eng.run(SEED, 89, 39), cg)
-    np.testing.assert_array_equal(eng.run(SEED, 64, 1) + eng.run(SEED, 65, 63), cg)
 
 
 def _check_mse(eng, res):
@@ -320,11 +326,41 @@ def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
     res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
     assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
     eng.close()
-    # the script's threshold keeps the structured path (C2: 6e-5 x tolerance)
+    # the script's threshold keeps the structured path: Q' H_hat G equals the
+    # thresholded W to rounding (oracle, tools/threshold_study.py: <= 7e-13
+    # absolute at max|W| 0.41-0.59)
     S.zero_threshold = 1e-8
     eng = harness.engine(S, batch=64)
     eng.run(SEED, 0, 64)
     assert "mic_fft" in eng.path_info(0)
+    chk = eng.structured_check(0)
+    assert 0.0 <= chk["ratio"] <= 1.0 and chk["dev"] <= 1e-11 * chk["wmax"], chk
+    eng.close()
+
+
+def test_structured_ofdm_guard_is_at_rounding_level():
+    """a guard at the threshold (r02-r03: thr + 1e-9 max|W|)
+    accepts any geometry whose only deviation is the W threshold itself, since a
+    zeroed entry has |W_s| < thr by definition.  At ZeroThreshold 1e-6 the
+    thresholds of script:287-289 / :306-308 zero C2 entries of magnitude
+    1e-7..1e-6 (oracle: max |W_thr - W_s| = 0.94 thr, tools/threshold_study.py),
+    which the old guard accepted (deviation < thr) and the rounding-level guard
+    (1e-11 max|W|, dsce_structured_check) must reject: the W contraction runs and
+    the counts equal the oracle's literal thresholded W."""
+    from types import SimpleNamespace
+    S = SimpleNamespace(**vars(harness.setup("default", schemes=("ofdm",))))
+    S.zero_threshold = 1e-6
+    eng = harness.engine(S, batch=64)
+    chk = eng.structured_check(0)
+    # the old guard would have accepted: every deviation is below the threshold
+    assert 0.0 < chk["dev"] < S.zero_threshold, chk
+    # ... but it is far above rounding
+    assert chk["ratio"] > 1e3 and chk["rtol"] == 1e-11, chk
+    cg = eng.run(SEED, 0, 64)
+    path = eng.path_info(0)
+    assert "mic_fft" not in path and "wpair3_fused" in path, path
+    res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
     eng.close()
 
 

@@ -125,8 +125,11 @@ def _integration_calls():
     return _calls(code + "\n" + "\n".join(inline))
 
 
-def _patch_calls():
-    plus = [l[1:] for l in open(PATCH).read().splitlines() if l.startswith("+") and not l.startswith("+++")]
+FF_PATCH = os.path.join(harness.PKG, "matlab", "fastfading_dsce.patch")
+
+
+def _patch_calls(path=PATCH):
+    plus = [l[1:] for l in open(path).read().splitlines() if l.startswith("+") and not l.startswith("+++")]
     return _calls("\n".join(plus))
 
 
@@ -135,11 +138,13 @@ def test_integration_md_calls_run_through_the_gateway(built):
     PSACE 'MMSE' patch) is accepted by the gateway with that many inputs and
     outputs: a documented call the gateway rejects (round-2: 'run' with 7
     arguments) fails here."""
-    calls = _integration_calls() + _patch_calls()
+    calls = _integration_calls() + _patch_calls() + _patch_calls(FF_PATCH)
     cmds = {c[0] for c in calls}
     assert {"create", "set_channel", "set_snr", "add_scheme", "build_mmse", "run", "bits_per_rep",
-            "mmse_onetap", "set_interpolation", "set_noise_slot"} <= cmds, cmds
+            "mmse_onetap", "set_interpolation", "set_noise_slot", "tx_matrices", "enable_mse", "get_mse",
+            "channel_realise"} <= cmds, cmds
     assert ("run", 4, 1) in calls and ("mmse_onetap", 5, 1) in _patch_calls()
+    assert {("set_channel", 7, 0), ("channel_realise", 3, 1)} <= set(_patch_calls(FF_PATCH))
     # create first (the gateway refuses any other command before it)
     triples = ["create:1:0"] + ["%s:%d:%d" % c for c in calls if c[0] != "create"]
     res, stdout = _run(built, ["replay", *triples])
@@ -161,6 +166,24 @@ def test_psace_patch_applies_to_the_reference(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     body = (d / "PilotSymbolAidedChannelEstimation.m").read_text()
     assert "Needs to be" not in body and body.count("dsce_mex('mmse_onetap'") == 1
+    assert "numel(varargin) < 4" in body                  # the missing [SchemeId SNRIndex] is an error()
+
+
+def test_fastfading_patch_applies_to_the_reference(tmp_path):
+    """The FastFading shim (NewRealization routed to dsce_channel_realise,
+    FastFading.m:194-250) applies cleanly to the reference's class and adds
+    exactly one UseEngine method and one engine branch in NewRealization."""
+    ref = "/root/reference/+Channel/FastFading.m"
+    if not os.path.exists(ref) or not shutil.which("patch"):
+        pytest.skip("reference or patch(1) not available")
+    d = tmp_path / "+Channel"
+    d.mkdir()
+    shutil.copy(ref, d / "FastFading.m")
+    out = subprocess.run(["patch", "-p1", "-i", FF_PATCH], cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    body = (d / "FastFading.m").read_text(encoding="latin-1")
+    assert body.count("function UseEngine( obj, Seed, FirstRealization )") == 1
+    assert body.count("dsce_mex('channel_realise'") == 1 and body.count("dsce_mex('set_channel'") == 1
 
 
 def test_outputs_sized_from_engine_state(results):
@@ -171,17 +194,23 @@ def test_outputs_sized_from_engine_state(results):
     assert results["channel_realise"] == ("OK", "540x2")
     assert results["add_scheme"] == ("OK", "1x1")
     assert results["scheme_dims"] == ("OK", "1x9")
-    for k in ("set_interpolation", "set_option", "set_channel", "create", "destroy"):
+    for k in ("set_interpolation", "set_option", "set_channel", "create", "destroy", "enable_mse"):
         assert results[k][0] == "OK", k
+    # the object's properties reach dsce_tx_desc (mex_stub.c checks every field)
+    assert results["tx_matrices_ofdm"] == ("OK", "540x336") and results["tx_matrices_fbmc"] == ("OK", "540x720")
+    assert results["get_mse"] == ("OK", "5x7")                          # [iter+1, snr, scheme]
+    assert results["structured_check"] == ("OK", "1x4")
 
 
 def test_arity_and_argument_checks(results):
     usage = ("run_old_7_args", "mmse_onetap_4_args", "mmse_onetap_old_6_args", "get_W_old_5_args",
-             "channel_realise_old_5_args", "add_scheme_15_args", "scheme_dims_2_outputs", "unknown")
+             "channel_realise_old_5_args", "add_scheme_15_args", "scheme_dims_2_outputs", "unknown",
+             "tx_matrices_3_outputs", "get_mse_extra_arg")
     for k in usage:
         assert results[k] == ("ERR", "dsce:usage"), (k, results[k])
     args = ("mmse_onetap_wrong_np", "get_W_scheme_0", "add_scheme_bad_Q", "add_scheme_bad_dataIdx",
-            "set_interpolation_bad", "set_option_bad_name", "set_channel_fractional_N")
+            "set_interpolation_bad", "set_option_bad_name", "set_channel_fractional_N", "tx_matrices_not_object",
+            "tx_matrices_real_signal", "tx_matrices_phydyas")
     for k in args:
         assert results[k] == ("ERR", "dsce:args"), (k, results[k])
     assert results["run_before_create"] == ("ERR", "dsce:state")

@@ -139,3 +139,57 @@ def test_c5_sizes_and_mirror():
     assert len(O["schemes"]["ofdm"]["pilot_pos"]) == 32 and len(O["chan"]["idx_taps"]) == 3
     for f in ("G", "Q", "P"):
         np.testing.assert_allclose(getattr(S.schemes["ofdm"], f), O["schemes"]["ofdm"][f], rtol=0, atol=1e-13)
+
+
+def _pm_of(sc, LK):
+    pm = np.zeros(LK)
+    pm[sc["pilot_pos"]] = 1
+    if not sc["despread"]:                                  # auxiliary symbols: neither pilot nor data
+        aux = np.ones(LK, dtype=bool)
+        aux[sc["pilot_pos"]] = False
+        aux[sc["data_pos"]] = False
+        pm[aux] = -1
+    return pm
+
+
+@pytest.mark.parametrize("config", ["default", "c5"])
+def test_tie_rtol_changes_only_the_c4_tie_class(config, monkeypatch):
+    """TIE_RTOL loosens the interferer test |D(pilot, :)| >= thr of
+    IIC.m:72-73 / :113-114 for every configuration and method.  Against plain
+    floating-point >=, the interferer sets differ only for the 'Coding' precoder
+    (C4 at 24 x 30 and the 48 x 30 C5 geometry alike: the 21st-largest corner
+    interference falls inside a class of 8 interferers per pilot that are equal
+    in exact arithmetic), and there only by members of those tie classes;
+    'Auxiliary' (28 interferers) keeps the same sets.  Nothing else lies within
+    1e-6 of the threshold, so the tolerance cannot have pulled in a near-tie."""
+    O = osu.script_setup(config, schemes=("fbmc_aux", "fbmc_cod"))
+    D = O["fbmc"].fbmc_matrix()
+    LK = D.shape[0]
+    L = O["L"]
+    for key, method, ncan, p2d in (("fbmc_aux", "Auxiliary", 28, 4.685), ("fbmc_cod", "Coding", 20, 4.0)):
+        sc = O["schemes"][key]
+        pm = _pm_of(sc, LK).reshape(L, LK // L, order="F")
+        tol = sc["iic"]["considered"]
+        monkeypatch.setattr(osu, "TIE_RTOL", 0.0)
+        plain = osu.iic(method, pm, D, ncan, p2d)["considered"]
+        monkeypatch.setattr(osu, "TIE_RTOL", 1e-12)
+        diff = np.flatnonzero(np.asarray(tol) != np.asarray(plain))
+        if key == "fbmc_cod":
+            # only members of the pilots' exact-arithmetic tie classes (8 per
+            # pilot: |D(pilot, x)| equal to the threshold to 1e-12) change: all
+            # are kept with the tolerance, half of them dropped without it
+            thr = np.sort(np.abs(np.concatenate([np.concatenate([np.abs(D[:, LK - 1]).reshape(L, -1, order="F"),
+                                                                  np.abs(D[:, LK - L]).reshape(L, -1, order="F")[1:]], 0),
+                                                  np.concatenate([np.abs(D[:, L - 1]).reshape(L, -1, order="F")[:, 1:],
+                                                                  np.abs(D[:, 0]).reshape(L, -1, order="F")[1:, 1:]],
+                                                                 0)], 1)).ravel())[::-1][ncan]
+            a = np.abs(D[sc["pilot_pos"], :])
+            rel = np.abs(a - thr) / thr
+            assert np.all((rel <= 1e-12).sum(axis=1) == 8), (rel <= 1e-12).sum(axis=1)
+            tie = np.flatnonzero((rel <= 1e-12).any(axis=0))
+            assert diff.size > 0 and set(diff) <= set(tie), diff
+            assert np.all(np.asarray(plain)[diff] == 0) and np.all(np.asarray(tol)[diff] < 0), diff
+            # nothing else sits near the threshold: the tolerance has a wide margin
+            assert rel[rel > 1e-12].min() > 1e-6
+        else:
+            assert diff.size == 0, (config, key, diff)
