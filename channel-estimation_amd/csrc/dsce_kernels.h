@@ -30,6 +30,8 @@ struct Opts {
     int mic_net = 1;          // the same network for k_mic_data (bit 0) / k_mic_pilot (bit 1), whose tap GEMM then
                               // needs no exchange: data 3.99 -> 3.65 ms, pilot 1.91 -> 2.00 ms (237 VGPRs): 1
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
+    int pic_skip = 1;         // k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
+                              // iterations are copies); 0 = compute every iteration
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower

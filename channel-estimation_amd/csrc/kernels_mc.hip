@@ -977,6 +977,7 @@ struct StorePerfectDetect {
     const uint16_t* sidr;              // transmitted symbol index per data row [LK][R]
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
+    int skip;                          // k_pic_fft: stop at the IC's fixed point (Opts::pic_skip)
     double2* sym;
     SlicerLds* slt;
     int c0, c1;
@@ -1557,6 +1558,16 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     }
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     int ncnt = 0;
+    // The IC's fixed point (o.skip): D, h and y do not change between the
+    // iterations of the perfect-CSI branch (script:541-561), so an iteration
+    // whose decisions equal the previous iteration's for every data row of the
+    // wave's 16 units (the symbol blocks of OFDM are independent: D is block-
+    // diagonal) is reproduced exactly — same inputs, same instructions — by
+    // every later one: their counts (and traces) are copies.  pk: the last
+    // decisions, 8 bits per row; have: pk is valid (stage 0 ran here, or an
+    // iteration did).
+    unsigned pk[2] = {0u, 0u};
+    bool have = S0, conv = false;
     if (S0) {
         // stage 0: y / h and 1 / h now, one-tap z = y / h, slicer, counts, decisions
         int code[6], dp[6];
@@ -1593,11 +1604,17 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
             u[a].x = data ? nv.x : u[a].x;
             u[a].y = data ? nv.y : u[a].y;
+            pk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
         cntl[w][0] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);
         ncnt = 0;
     }
     for (int it = 1; it <= niter; ++it) {
+        if (conv) {
+            // the fixed point (below): this iteration reproduces the previous one
+            cntl[w][it] = cntl[w][it - 1];
+            continue;
+        }
         // an opaque zero keeps the per-iteration LDS twiddle reads inside the loop
         // (hoisted, they would hold 56 more registers)
         int oz = 0;
@@ -1666,6 +1683,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         // epilogue per row 4a + r: z = y / h - acc / h + u, slicer, counts,
         // re-precoded decision into u
         int code[6], dp[6];
+        unsigned npk[2] = {0u, 0u};
         int anytie = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -1705,9 +1723,29 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
             u[a].x = data ? nv.x : u[a].x;
             u[a].y = data ? nv.y : u[a].y;
+            npk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
         cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
+        const bool same = have && npk[0] == pk[0] && npk[1] == pk[1];
+        pk[0] = npk[0];
+        pk[1] = npk[1];
+        have = true;
+        if (o.skip && it < niter && __all(same)) {
+            conv = true;
+            if (TRACE)
+#pragma unroll
+                for (int a = 0; a < 6; ++a)
+                    if (((dmask >> a) & 1) && unit == o.tr->unit) {
+                        const int row = row0 + 4 * a + r;
+                        const double2 yv = o.y[(size_t)row * U + unit], hh = o.h[(size_t)row * R + rl];
+                        const double2 yp = c_add(c_sub(yv, x[p6(a)]), c_mul(hh, u[a]));
+                        for (int i2 = it + 1; i2 <= niter; ++i2) {
+                            o.tr->yperf[(size_t)i2 * o.tr->LK + row] = yp;
+                            o.tr->dec_p[(size_t)i2 * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+                        }
+                    }
+        }
     }
     // counters of every stage, summed over the block's 4 waves: thread
     // 2 (it - it0) + edge issues the block's one atomic per counter
@@ -2579,6 +2617,7 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     if (!pic_fft_ok(op, sk, ch, b, niter))
         throw std::logic_error("launch_perfect_chain: no chain kernel for this scheme (perfect_chain_ok is false)");
     StorePerfectDetect o = chain_detect(sk, b, pd, 1);
+    o.skip = op.pic_skip;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
     // stage0: the chain also runs stage 0 of the branch (with k_mic_pilot /

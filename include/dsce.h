@@ -311,7 +311,11 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   the schemes' windows read, zero elsewhere, with the run's Jakes kernels),
  *   tx_rows (1: TX symbols of a row-local precoder drawn row-parallel), snr_base
  *   (0..255: the noise of SNR index k is sub-stream snr_base + k, so a rank
- *   serving SNR points [b, ...) of a sweep draws the one-rank run's noise).
+ *   serving SNR points [b, ...) of a sweep draws the one-rank run's noise),
+ *   pic_skip (1: k_pic_fft stops a wave of 16 units x one symbol at the
+ *   perfect-CSI IC's fixed point — an iteration that repeats the previous
+ *   decisions of every data row is repeated exactly by every later one, whose
+ *   counts it copies; 0: every iteration computed).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */

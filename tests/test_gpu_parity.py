@@ -498,3 +498,25 @@ def test_setup_with_gpu_tx_matrices_gives_the_same_counts():
         ea.close()
         eb.close()
 
+
+
+def test_pic_fixed_point_skip_is_exact():
+    """k_pic_fft's early exit (option pic_skip): a wave whose iteration repeats
+    the previous decisions of every data row copies that iteration's counts and
+    traces into the later ones instead of computing them.  Exact by construction
+    (same inputs, same instructions); checked here against the full computation
+    at every SNR point of the script (where most waves converge at high SNR):
+    identical counts over 512 realisations, and an identical per-stage trace of
+    a unit, decisions and y_perf included."""
+    S = harness.setup("default", schemes=("ofdm",))
+    full = harness.engine(S, batch=256, options={"pic_skip": 0})
+    fast = harness.engine(S, batch=256)
+    assert fast.get_option("pic_skip") == 1
+    np.testing.assert_array_equal(fast.run(SEED, 0, 512), full.run(SEED, 0, 512))
+    for k in (0, 6):
+        a, b = fast.trace_unit(0, SEED, 21, k), full.trace_unit(0, SEED, 21, k)
+        np.testing.assert_array_equal(a["dec_p"], b["dec_p"])
+        np.testing.assert_array_equal(np.nan_to_num(a["yperf"]), np.nan_to_num(b["yperf"]))
+    assert "pic_fft" in fast.path_info(0)
+    full.close()
+    fast.close()
