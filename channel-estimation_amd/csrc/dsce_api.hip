@@ -109,6 +109,11 @@ struct Scheme {
     int npb = 0;
     int* dblk = nullptr;            // QH blocks without pilot rows (k_mic_data)
     int ndb = 0;
+    // low-rank form of Bv (build_mic_lr): Bv[q][n][p] = sum_k T_k[n] Bz[q k][p]; null: not eligible
+    double2* Bz = nullptr;          // [var][snr][ntap * MIC_NB][NP]
+    double* Tw = nullptr;           // [QH blk][MIC_NB][24]
+    double* Ts = nullptr;           // [QH blk][MIC_NB]
+    double lr_resid = -1.0;         // max |Bv - T Bz| / max |Bv| of the fit (-1: not built)
     long long wp_elems = 0, wp_exec = 0;
     long long w_diag = 0;           // (r, r) pairs inside the band (stored as zeros: diag(D_hat) comes from Wd)
     unsigned path = 0;              // PATH_* bits of the last dsce_run / trace (dsce_path_info)
@@ -696,6 +701,109 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 // In FFT form block b of Q' H_hat_p G is, with w = e^(2 pi i / 24), m = n - klo_b,
 //   D_p[lr, lc] = qs gs sum_q w^(-lc d_q) F_q[lc - lr],  F_q[k] = sum_m w^(k m) Bv[q][klo_b + m][p]
 // (Q^H row lr = qs w^(-lr m), G column lc = gs w^(lc m), cyclic over the prefix).
+// The low-rank form of the structured MMSE IC operator (Opts::mic_lr).  For
+// OFDM the pilot columns of Q and G are one FFT window's exponentials, so
+// Q[b + d_q, j] conj(G[b, j]) is a constant over pilot j's window and k_mcoef's
+// m[j][q][n - d_q] = kappa_qj T_{k(j)}[n] with T_k[n] = sum_{b in W_k} J0(n - b)
+// the J0 kernel summed over the FFT window W_k of pilot symbol k, for every tap.
+// Hence Bv[q][n][p] = sum_k T_k[n] Bz[q k][p], Bz[q k][p] = sum_{j in W_k}
+// kappa_qj pinv(R)[j][p]: the estimated taps of a symbol are MIC_NB real x
+// complex MACs per tap and sample from Z = Bz hP (NT MIC_NB x NP complex MACs per
+// unit and stage, shared by every symbol) instead of NP complex MACs from hP.
+// Bz is fitted here to the Bv the guard above checked (least squares over every
+// FFT-window sample, long-double QR of the MIC_NB columns of T) and kept only if
+// the fit reproduces Bv to rounding: max |Bv - T Bz| <= LR_RTOL max |Bv|.
+static constexpr double LR_RTOL = 1e-13;
+void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<double2>& bv, const std::vector<int>& pb) {
+    const int NP = s.d.n_pilots, N = s.N, nt = c->ch.ntap, nsl = 2 * c->nsnr, nblk = s.k.QH.nblk;
+    if ((int)pb.size() != MIC_NB || nt > 2) return;
+    std::vector<double> j0((size_t)2 * N - 1);
+    DSCE_HIP_CHECK(hipMemcpy(j0.data(), a.j0tab, j0.size() * sizeof(double), hipMemcpyDeviceToHost));
+    // rows: every FFT-window sample of the scheme's blocks
+    std::vector<int> rows;
+    for (int b = 0; b < nblk; ++b)
+        for (int m = 0; m < 24; ++m) rows.push_back(s.qband.klo[b] + m);
+    const int nr = (int)rows.size();
+    auto Tk = [&](int k, int n) {
+        long double t = 0.0L;
+        const int w0 = s.qband.klo[pb[k]];
+        for (int m = 0; m < 24; ++m) t += (long double)j0[(size_t)(n - (w0 + m) + N - 1)];
+        return t;
+    };
+    std::vector<long double> T((size_t)nr * MIC_NB);
+    for (int i = 0; i < nr; ++i)
+        for (int k = 0; k < MIC_NB; ++k) T[(size_t)i * MIC_NB + k] = Tk(k, rows[i]);
+    // modified Gram-Schmidt QR of T (nr x MIC_NB)
+    std::vector<long double> Qm(T), Rm(MIC_NB * MIC_NB, 0.0L);
+    for (int k = 0; k < MIC_NB; ++k) {
+        for (int j = 0; j < k; ++j) {
+            long double d = 0.0L;
+            for (int i = 0; i < nr; ++i) d += Qm[(size_t)i * MIC_NB + j] * Qm[(size_t)i * MIC_NB + k];
+            Rm[j * MIC_NB + k] = d;
+            for (int i = 0; i < nr; ++i) Qm[(size_t)i * MIC_NB + k] -= d * Qm[(size_t)i * MIC_NB + j];
+        }
+        long double nn = 0.0L;
+        for (int i = 0; i < nr; ++i) nn += Qm[(size_t)i * MIC_NB + k] * Qm[(size_t)i * MIC_NB + k];
+        nn = sqrtl(nn);
+        if (!(nn > 0.0L)) return;
+        Rm[k * MIC_NB + k] = nn;
+        for (int i = 0; i < nr; ++i) Qm[(size_t)i * MIC_NB + k] /= nn;
+    }
+    std::vector<double2> bz((size_t)nsl * nt * MIC_NB * NP);
+    double mx = 0.0, dev = 0.0;
+    for (int sl = 0; sl < nsl; ++sl)
+        for (int q = 0; q < nt; ++q)
+            for (int p = 0; p < NP; ++p) {
+                long double zr[MIC_NB], zi[MIC_NB];
+                for (int k = 0; k < MIC_NB; ++k) {           // Q^T b
+                    long double ar = 0.0L, ai = 0.0L;
+                    for (int i = 0; i < nr; ++i) {
+                        const double2 v = bv[(((size_t)sl * nt + q) * N + rows[i]) * NP + p];
+                        ar += Qm[(size_t)i * MIC_NB + k] * v.x;
+                        ai += Qm[(size_t)i * MIC_NB + k] * v.y;
+                    }
+                    zr[k] = ar;
+                    zi[k] = ai;
+                }
+                for (int k = MIC_NB - 1; k >= 0; --k) {      // R z = Q^T b
+                    for (int j = k + 1; j < MIC_NB; ++j) {
+                        zr[k] -= Rm[k * MIC_NB + j] * zr[j];
+                        zi[k] -= Rm[k * MIC_NB + j] * zi[j];
+                    }
+                    zr[k] /= Rm[k * MIC_NB + k];
+                    zi[k] /= Rm[k * MIC_NB + k];
+                }
+                for (int k = 0; k < MIC_NB; ++k)
+                    bz[(((size_t)sl * nt + q) * MIC_NB + k) * NP + p] = make_double2((double)zr[k], (double)zi[k]);
+                for (int i = 0; i < nr; ++i) {
+                    const double2 v = bv[(((size_t)sl * nt + q) * N + rows[i]) * NP + p];
+                    long double er = -(long double)v.x, ei = -(long double)v.y;
+                    for (int k = 0; k < MIC_NB; ++k) {
+                        er += T[(size_t)i * MIC_NB + k] * (long double)(double)zr[k];
+                        ei += T[(size_t)i * MIC_NB + k] * (long double)(double)zi[k];
+                    }
+                    dev = std::max(dev, (double)sqrtl(er * er + ei * ei));
+                    mx = std::max(mx, std::hypot(v.x, v.y));
+                }
+            }
+    s.lr_resid = mx > 0.0 ? dev / mx : -1.0;
+    if (!(mx > 0.0) || dev > LR_RTOL * mx) return;
+    std::vector<double> tw((size_t)nblk * MIC_NB * 24), ts((size_t)nblk * MIC_NB);
+    for (int b = 0; b < nblk; ++b)
+        for (int k = 0; k < MIC_NB; ++k) {
+            long double sum = 0.0L;
+            for (int m = 0; m < 24; ++m) {
+                const long double t = Tk(k, s.qband.klo[b] + m);
+                tw[((size_t)b * MIC_NB + k) * 24 + m] = (double)t;
+                sum += t;
+            }
+            ts[(size_t)b * MIC_NB + k] = (double)sum;
+        }
+    s.Bz = dupload(c, bz);
+    s.Tw = dupload(c, tw);
+    s.Ts = dupload(c, ts);
+}
+
 static constexpr double MIC_RTOL = 1e-11;
 void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, const double2* rinv) {
     const int NP = s.d.n_pilots, LK = s.LK, N = s.N, nsl = 2 * c->nsnr, nt = c->ch.ntap;
@@ -821,6 +929,7 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
         s.pmask = dupload(c, pm);
     }
     if (s.ndb) s.dblk = dupload(c, db);
+    build_mic_lr(c, s, a, bv, pb);
 }
 
 // ---------------------------------------------------------------------------
@@ -843,6 +952,12 @@ void build_mmse(dsce_ctx* c, Scheme& s, double thr) {
         if (s.pil_c0) free_alloc(c, s.pil_c0);
         if (s.Bv) free_alloc(c, s.Bv);
         if (s.Bs) free_alloc(c, s.Bs);
+        if (s.Bz) free_alloc(c, s.Bz);
+        if (s.Tw) free_alloc(c, s.Tw);
+        if (s.Ts) free_alloc(c, s.Ts);
+        s.Bz = nullptr;
+        s.Tw = s.Ts = nullptr;
+        s.lr_resid = -1.0;
         if (s.pblk) free_alloc(c, s.pblk);
         if (s.pmask) free_alloc(c, s.pmask);
         if (s.dblk) free_alloc(c, s.dblk);
@@ -1018,6 +1133,8 @@ void ensure_buffers(dsce_ctx* c, int R) {
     // LS pilot estimates of every stage (k_mic_pilot -> k_mic_data)
     b.hpa_stages = c->niter + 1;
     b.hpa = dalloc<double2>(c, (size_t)b.hpa_stages * NP * U, L);
+    // Z = Bz hP of every stage (low-rank MMSE IC operator, k_mic_pilot -> k_mic_data)
+    b.za = dalloc<double2>(c, (size_t)b.hpa_stages * std::max(1, std::min(c->ch.ntap, 2)) * MIC_NB * U, L);
     DSCE_HIP_CHECK(hipMemsetAsync(b.sidr, 0, (LK + 32) * R * sizeof(uint16_t), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));
@@ -1156,6 +1273,9 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
         mm.npb = s.npb;
         mm.dblk = s.dblk;
         mm.ndb = s.ndb;
+        mm.Bz = s.Bz;
+        mm.Tw = s.Tw;
+        mm.Ts = s.Ts;
         {
             Timed t(c, "tx");
             b.U = R * std::min(chunk, c->nsnr);
@@ -1185,17 +1305,22 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
             // stage 0, the MMSE branch k_mic_pilot + k_mic_data, every stage each
             if (pfuse && mmse_stages_ok(op, s.k, mm, c->ch, b, c->niter)) {
                 PerfectDetectArgs pd{c->d_counters, (int)si, 0, c->niter + 1, c->nsnr, 0, s.k.slI, s.k.slQ};
+                // the low-rank tap operator (both passes or neither: the data pass
+                // reads the pilot pass's Z instead of its LS pilots)
+                const bool lr = op.mic_lr && (op.mic_net & 1) && s.Bz;
                 {
                     Timed t(c, "perfect_ic");
                     s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, true);
                 }
                 {
                     Timed t(c, "k_mic_pilot");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1, (op.mic_net & 2) != 0);
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1, (op.mic_net & 2) != 0,
+                                                 lr);
                 }
                 {
                     Timed t(c, "k_mic_data");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2, (op.mic_net & 1) != 0);
+                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2, (op.mic_net & 1) != 0,
+                                                 lr);
                 }
                 if (to && to->hp_stages)
                     for (int st = 0; st <= c->niter; ++st)
@@ -1355,9 +1480,13 @@ KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
     // (residual + diag(D_hat) v: 2 CMACs, quotient: 1 complex division = 2
     // CMACs), re-precoding (1 CMAC)
     const double chain = 2.0 * DFT + 8.0 * (nt * 24.0 + 24.0 * 5.0);
-    // the MMSE extras per stage and symbol: the estimated taps (nt x 24 x NP),
-    // this stage's window sums Bs hP (nt x NP), diag(D_hat) per row (nt CMACs)
-    const double mmse_extra = 8.0 * (nt * 24.0 * NP + nt * NP + nt * 24.0);
+    // the MMSE extras per stage and symbol: the estimated taps (nt x 24 x NP
+    // complex MACs; low-rank operator: nt x 24 x MIC_NB real x complex MACs at 4
+    // flops), this stage's window sums (Bs hP: nt x NP; low-rank: nt x MIC_NB real
+    // x complex), diag(D_hat) per row (nt CMACs)
+    const bool lrp = (s.path & PATH_MIC_LR) != 0;
+    const double mmse_extra = lrp ? 4.0 * (nt * 24.0 * MIC_NB + nt * MIC_NB) + 8.0 * nt * 24.0
+                                  : 8.0 * (nt * 24.0 * NP + nt * NP + nt * 24.0);
     const double stage0 = 8.0 * (24.0 * 3.0);             // one-tap quotient + re-precoding per row
     if (name == "tx") {
         w.flops = 8.0 * LK;                                // P [xP; xD] (row-local precoder: 1 CMAC per row)
@@ -1374,10 +1503,14 @@ KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
     } else if (name == "k_mic_pilot" || name == "k_mic_data") {
         const double nsym = name == "k_mic_pilot" ? npb : ndb;
         // stage 0: LS / window sums + one-tap; stages 1..it: chain + MMSE extras
-        w.flops = ns * nsym * (stage0 + 8.0 * (nt * NP) + it * (chain + mmse_extra));
-        if (name == "k_mic_pilot") w.flops += ns * (it + 1) * NP * 8.0;   // LS: y_P / x_P / sqrt(kappa)
+        w.flops = ns * nsym * (stage0 + (lrp ? 4.0 * nt * MIC_NB : 8.0 * nt * NP) + it * (chain + mmse_extra));
+        if (name == "k_mic_pilot") {
+            w.flops += ns * (it + 1) * NP * 8.0;                          // LS: y_P / x_P / sqrt(kappa)
+            if (lrp) w.flops += ns * (it + 1) * nt * MIC_NB * NP * 8.0;   // Z = Bz hP, once per unit and stage
+        }
         const double ysym = ns * nsym * 24.0 * B16;                       // y of the kernel's symbols
-        const double hpa = ns * (it + 1) * NP * B16;                      // written (pilot) or read (data)
+        // hP of every stage written (pilot) or read (data); low-rank: Z instead
+        const double hpa = ns * (it + 1) * (lrp ? nt * MIC_NB : NP) * B16;
         w.bytes = ysym + hpa + nsym * 24.0 * (B16 + sizeof(uint16_t));    // + xs, sidr of the symbols
     }
     return w;
@@ -1993,16 +2126,8 @@ int dsce_work_model(dsce_ctx* ctx, int32_t id, double* cmac, double* wbytes) {
     const double fused = (s.path & PATH_WPAIR3_FUSED) ? (double)s.LK * s.d.n_pilots : 0.0;
     if (cmac) *cmac = ((double)(s.w_struct - s.w_diag) + fused) * ctx->nsnr * ctx->niter;
     if (cmac && (s.path & PATH_MIC_STAGES)) {
-        // k_mic_data (the bench's roofline kernel), per unit and data symbol:
-        // stage 0 window sums (ntap x NP) + diag(D_hat) / one-tap (24); every
-        // IC stage the estimated taps (ntap x 24 x NP), their window sums
-        // (ntap x 24), the channel (ntap x 24), diag(D_hat_prev) v (24), this
-        // stage's window sums (ntap x NP) and diag (24), two DFT-24 at 5 n log2 n
-        // flops (counted as flops / 8 CMACs)
-        const double nt = ctx->ch.ntap, NP = s.d.n_pilots, it = ctx->niter;
-        const double st0 = nt * NP + 24;
-        const double sti = nt * 24 * NP + nt * 24 + nt * 24 + 24 + nt * NP + 24 + 2 * (5.0 * 24 * std::log2(24.0)) / 8.0;
-        *cmac = (st0 + it * sti) * s.ndb * ctx->nsnr;
+        // k_mic_data (the bench's roofline kernel): dsce_kernel_work's model in CMACs
+        *cmac = kernel_work(ctx, s, "k_mic_data").flops / 8.0;
     }
     if (wbytes) *wbytes = (double)s.w_elems * sizeof(double2);
     API_END
@@ -2041,6 +2166,8 @@ int dsce_structured_check(dsce_ctx* ctx, int32_t id, double* out) {
     out[1] = s.mic_dev;
     out[2] = s.mic_wmax;
     out[3] = MIC_RTOL;
+    out[4] = s.lr_resid;
+    out[5] = s.Bz ? 1.0 : 0.0;
     API_END
 }
 
@@ -2075,7 +2202,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

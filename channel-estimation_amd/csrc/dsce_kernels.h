@@ -30,6 +30,8 @@ struct Opts {
     int mic_net = 1;          // the same network for k_mic_data (bit 0) / k_mic_pilot (bit 1), whose tap GEMM then
                               // needs no exchange: data 3.99 -> 3.65 ms, pilot 1.91 -> 2.00 ms (237 VGPRs): 1
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
+    int mic_lr = 1;           // MMSE IC taps in the low-rank form T_k Z (k_mic_pilot / k_mic_data) where
+                              // build_mic_lr verified it; 0 = the tap GEMM Bv hP on the matrix cores
     int pic_skip = 1;         // k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
                               // iterations are copies); 0 = compute every iteration
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
@@ -55,6 +57,7 @@ enum : unsigned {
     PATH_TXRX_FFT = 1u << 12,      // k_txrx_fft (TX + channel + noisy receiver front by FFT, OFDM)
     PATH_PILOT_FUSED = 1u << 13,   // retired (r02 k_mic_fft's fused pilot pass)
     PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair
+    PATH_MIC_LR = 1u << 15,        // ... with the low-rank tap operator T_k Z (build_mic_lr)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -104,6 +107,7 @@ struct McBuffers {
     uint16_t* sidr;   // [LK][R]   transmitted symbol index per data row (row-indexed sidx)
     double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (k_mic_pilot -> k_mic_data), or null
     int hpa_stages;   // stages hpa holds
+    double2* za;      // [stage][ntap * MIC_NB][U] Z = Bz hP of every stage (low-rank MMSE IC), or null
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
     const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)
@@ -130,7 +134,14 @@ struct MmseK {
     const int* dblk;      // QH blocks without pilot rows (k_mic_data)
     int ndb;
     const int* pmask;     // [QH blk]: 1 = holds pilot rows
+    // the low-rank form of Bv (build_mic_lr): bv[q][n][p] = sum_k T_k[n] Bz[q k][p],
+    // T_k the J0 kernel summed over pilot symbol k's FFT window; null when not eligible
+    const double2* Bz;    // [var][snr][ntap * MIC_NB][NP]
+    const double* Tw;     // [QH blk][MIC_NB][24]: T_k over the block's FFT window
+    const double* Ts;     // [QH blk][MIC_NB]: its window sums
 };
+// pilot symbols (FFT windows holding pilots) of the low-rank MMSE IC operator
+constexpr int MIC_NB = 4;
 
 // Monte-Carlo pipeline.  Launchers return the PATH_* bits of the kernels they ran.
 // Chunks of the impulse response a batch needs: every sample some Q^H row of
@@ -195,7 +206,7 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
                     int niter);
 // part: 1 = k_mic_pilot, 2 = k_mic_data (the data kernel reads the pilot kernel's hpa)
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm = true);
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm = true, bool lr = false);
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd);
 // The whole perfect-CSI IC chain (iterations 1..niter) in one kernel, u in

@@ -1818,6 +1818,11 @@ struct Mic2Args {
     double* mse_err;
     double* mse_pow;
     int nsnr, N, nblk, niter, scheme;
+    // low-rank operator (LR): Z = Bz hP per unit and stage, the taps T_k Z
+    const double2* bz;                // [var][snr][NT MIC_NB][NP]
+    double2* za;                      // [stage][NT MIC_NB][U]
+    const double* tw;                 // [nblk][MIC_NB][24]
+    const double* ts;                 // [nblk][MIC_NB]
 };
 
 __device__ __forceinline__ int mic_var(int s, int niter) { return (s == 0 || 2 * s <= niter) ? 0 : 1; }
@@ -1956,13 +1961,21 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
 // k_mic_pilot and k_mic_data).  PIL: a pilot symbol (LS of every stage into the
 // block's LDS exchange + hpa, one barrier per stage); otherwise hP_s comes from
 // hpa.  Per-stage counters go to cntl[w][s] (one word per wave and stage).
-template <int NT, int SH, int NP, bool TRACE, bool PIL, bool NM, class ALoad, class BsLoad>
+// LR (the low-rank operator, build_mic_lr): the estimated taps of stage s are
+// sum_k T_k[n] Z_{s-1}[q k] with Z_s = Bz(var_s) hP_s (NT MIC_NB values per unit:
+// the pilot kernel forms them once per unit and stage, LDS szz + HBM za) and
+// T_k the J0 kernel summed over pilot symbol k's window (twl: this symbol's
+// window, tsl: its sums), instead of the tap GEMM Bv hP (NT x 24 x NP complex
+// MACs per symbol and unit); diag(D_hat_s) from S_q = sum_k tsl[k] Z_s[q k].
+template <int NT, int SH, int NP, bool TRACE, bool PIL, bool NM, bool LR, class ALoad, class BsLoad>
 __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
                                             const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
                                             const double2* wrow, double2 (*shp)[NP][17],
                                             const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
                                             int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
-                                            int snr) {
+                                            int snr, const double* twl = nullptr, const double* tsl = nullptr,
+                                            double2 (*szz)[NT * MIC_NB][17] = nullptr, int unit0 = 0) {
+    constexpr int NZ = NT * MIC_NB;
     const int cq = NM ? r : (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
@@ -1995,31 +2008,52 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     // B operand of the tap GEMM (hP_{s-1}) and this stage's LS pilots (a quarter
     // per lane, for diag(D_hat_s)); the data kernel prefetches both for stage
     // s + 1 at the end of stage s and folds hn4 into the window sums sn at once
-    double2 hb[NP / 4], hn4[NP / 4];
+    double2 hb[LR ? 1 : NP / 4], hn4[LR ? 1 : NP / 4];
+    // LR: Z of the previous stage (the taps) and of this stage (diag), whole unit per lane
+    double2 zp[LR ? NZ : 1], zc[LR ? NZ : 1];
     // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s: window sums sn0 / sn1
     auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
         sn0 = sn1 = make_double2(0.0, 0.0);
-        const int vs = mic_var(s, ma.niter);
         bool f0 = true, f1 = true;                          // compile-time: first tap of each sum assigns
+        if constexpr (LR) {
 #pragma unroll
-        for (int q = 0; q < NT; ++q) {
-            double2 sq = c_mul(Bs(vs, q, ro * (NP / 4)), hn4[0]);
+            for (int q = 0; q < NT; ++q) {
+                double2 sq = make_double2(tsl[0] * zc[q * MIC_NB].x, tsl[0] * zc[q * MIC_NB].y);
 #pragma unroll
-            for (int k = 1; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
-            if (NM) {
-                // sum over the unit's four quarters (rows): ones(4 x 4) x B
-                sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.x, 0.0, 0, 0, 0),
-                                  __builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.y, 0.0, 0, 0, 0));
-            } else {
-                sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-                sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+                for (int k = 1; k < MIC_NB; ++k) {
+                    sq.x = fma(tsl[k], zc[q * MIC_NB + k].x, sq.x);
+                    sq.y = fma(tsl[k], zc[q * MIC_NB + k].y, sq.y);
+                }
+                if ((SH >> q) & 1) {
+                    sn1 = f1 ? sq : c_add(sn1, sq);
+                    f1 = false;
+                } else {
+                    sn0 = f0 ? sq : c_add(sn0, sq);
+                    f0 = false;
+                }
             }
-            if ((SH >> q) & 1) {
-                sn1 = f1 ? sq : c_add(sn1, sq);
-                f1 = false;
-            } else {
-                sn0 = f0 ? sq : c_add(sn0, sq);
-                f0 = false;
+        } else {
+            const int vs = mic_var(s, ma.niter);
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                double2 sq = c_mul(Bs(vs, q, ro * (NP / 4)), hn4[0]);
+#pragma unroll
+                for (int k = 1; k < NP / 4; ++k) c_fma(sq, Bs(vs, q, ro * (NP / 4) + k), hn4[k]);
+                if (NM) {
+                    // sum over the unit's four quarters (rows): ones(4 x 4) x B
+                    sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.x, 0.0, 0, 0, 0),
+                                      __builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.y, 0.0, 0, 0, 0));
+                } else {
+                    sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+                    sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+                }
+                if ((SH >> q) & 1) {
+                    sn1 = f1 ? sq : c_add(sn1, sq);
+                    f1 = false;
+                } else {
+                    sn0 = f0 ? sq : c_add(sn0, sq);
+                    f0 = false;
+                }
             }
         }
         sn0 = c_mul(scale, sn0);
@@ -2032,21 +2066,48 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         asm volatile("" : "+v"(oz));
         const int ro = r + oz;
         double2 sn0, sn1;
-        if (!PIL)
+        if (LR) {
+#pragma unroll
+            for (int j = 0; j < NZ; ++j) zp[j] = zc[j];
+            if (!PIL)                                    // this stage's Z (the pilot kernel forms it below)
+#pragma unroll
+                for (int j = 0; j < NZ; ++j) zc[j] = ma.za[((size_t)s * NZ + j) * U + unit];
+        } else if (!PIL) {
 #pragma unroll
             for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
+        }
         double2 ye[6];
         if (s == 0) {
 #pragma unroll
             for (int a = 0; a < 6; ++a) ye[a] = yv[a];
         } else {
             // the previous stage's estimated taps and their window sums
-            if (PIL)
-#pragma unroll
-                for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = shp[(s - 1) & 1][4 * ks + (l >> 4)][l & 15];
             double2 taps[6][NT];
-            mic_taps<NT, NP, NM>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); },
-                                 hb, l, cq);
+            if constexpr (LR) {
+                // T_k of the lane's six samples (this symbol's window, quarter cq)
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    double tk[MIC_NB];
+#pragma unroll
+                    for (int k = 0; k < MIC_NB; ++k) tk[k] = twl[k * 24 + 6 * cq + a + oz];
+#pragma unroll
+                    for (int q = 0; q < NT; ++q) {
+                        double2 t = make_double2(tk[0] * zp[q * MIC_NB].x, tk[0] * zp[q * MIC_NB].y);
+#pragma unroll
+                        for (int k = 1; k < MIC_NB; ++k) {
+                            t.x = fma(tk[k], zp[q * MIC_NB + k].x, t.x);
+                            t.y = fma(tk[k], zp[q * MIC_NB + k].y, t.y);
+                        }
+                        taps[a][q] = t;
+                    }
+                }
+            } else {
+                if (PIL)
+#pragma unroll
+                    for (int ks = 0; ks < NP / 4; ++ks) hb[ks] = shp[(s - 1) & 1][4 * ks + (l >> 4)][l & 15];
+                mic_taps<NT, NP, NM>(taps, [&](int q, int j, int p) { return A(mic_var(s - 1, ma.niter), q, j + oz, p); },
+                                     hb, l, cq);
+            }
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
@@ -2071,12 +2132,30 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                     const double2 q = c_div_fast(ye[a], xpb[pc][ul]);
                     const double2 h = make_double2(q.x * isqk, q.y * isqk);
                     hx[pc * 17 + ul] = h;
-                    ma.hpa[((size_t)s * NP + pc) * U + unit] = h;
+                    if (!LR || TRACE) ma.hpa[((size_t)s * NP + pc) * U + unit] = h;
                 }
             }
             __syncthreads();
+            if constexpr (LR) {
+                // Z_s = Bz(var_s) hP_s for the block's 16 units: one entry per thread
+                const int vs = mic_var(s, ma.niter);
+                const int t = threadIdx.x;
+                if (t < NZ * 16) {
+                    const int j = t >> 4, u = t & 15;
+                    const double2* __restrict__ bz = ma.bz + (((size_t)vs * ma.nsnr + snr) * NZ + j) * NP;
+                    double2 acc = c_mul(bz[0], hx[u]);
 #pragma unroll
-            for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
+                    for (int p = 1; p < NP; ++p) c_fma(acc, bz[p], hx[p * 17 + u]);
+                    szz[s & 1][j][u] = acc;
+                    ma.za[((size_t)s * NZ + j) * U + unit0 + u] = acc;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NZ; ++j) zc[j] = szz[s & 1][j][ul];
+            } else {
+#pragma unroll
+                for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
+            }
             diag_sums(s, ro, sn0, sn1);
         } else {
             diag_sums(s, ro, sn0, sn1);
@@ -2109,7 +2188,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             }
         }
         cntl[s] = wave_sum_dpp(valid ? ncnt : 0);  // uniform: every lane writes the same word
-        if (!PIL && s < ma.niter) {
+        if (!LR && !PIL && s < ma.niter) {
             // stage s + 1's operands: hP_s (tap GEMM) and hP_{s+1} (diag)
             const double2* __restrict__ hs = ma.hpa + (size_t)s * NP * U;
 #pragma unroll
@@ -2174,14 +2253,17 @@ __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, doub
 }
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
-template <int NT, int SH, int NP, bool TRACE, bool NM = false>
+template <int NT, int SH, int NP, bool TRACE, bool NM = false, bool LR = false>
 __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
+    constexpr int NZ = NT * MIC_NB;
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[4][24], wrow[4][24];
     __shared__ int rdc[4][24], rpc[4][24];
-    __shared__ double2 bss[4][2][NT][NP];                   // Bs of each wave's symbol, both variants
+    __shared__ double2 bss[LR ? 1 : 4][2][NT][NP];          // Bs of each wave's symbol, both variants
     __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
     __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
+    __shared__ double2 szz[LR ? 2 : 1][NZ][17];             // LR: Z of the block's 16 units, double-buffered
+    __shared__ double twp[LR ? 4 : 1][MIC_NB * 24 + MIC_NB];   // LR: each wave's T_k window + sums
     __shared__ int cntl[4][PM_MAXIT + 1];
     const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
@@ -2195,9 +2277,12 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
     mic2_tables(tb, o, tid, blockDim.x);
     mic2_rows(rpv[w], rdc[w], rpc[w], wrow[w], sk, o, row0, l);
-    {
+    if (LR) {
+        for (int i = l; i < MIC_NB * 25; i += 64)
+            twp[w][i] = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
+    } else {
         const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
-        bss[w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
+        bss[LR ? 0 : w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
     }
     for (int i = tid; i < NP * 16; i += blockDim.x) {
         const int u16 = ug16 * 16 + (i & 15);
@@ -2209,9 +2294,10 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     // the tap GEMM operand straight from L2 (staging each wave's window in LDS,
     // reloaded at the W -> W0 switch: 40 more VGPRs, 1.97 -> 2.28 ms per step)
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
-    auto Bs = [&](int var, int q, int p) { return bss[w][var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, true, NM>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
-                                             Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    auto Bs = [&](int var, int q, int p) { return bss[LR ? 0 : w][var][q][p]; };
+    mic2_stages<NT, SH, NP, TRACE, true, NM, LR>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
+                                                 Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twp[LR ? w : 0],
+                                                 twp[LR ? w : 0] + MIC_NB * 24, szz, ug16 * 16);
     __syncthreads();
     // one atomic per (stage, edge) per block
     for (int i = tid; i < 2 * (ma.niter + 1); i += blockDim.x) {
@@ -2224,15 +2310,16 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
 }
 
 // 64 units x one data symbol per block (4 waves x 16 units)
-template <int NT, int SH, int NP, bool TRACE, bool NM = false>
+template <int NT, int SH, int NP, bool TRACE, bool NM = false, bool LR = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[24], wrow[24];
     __shared__ int rdc[24], rpc[24];
     constexpr int BVS = NP + 1;
-    __shared__ double2 sbv[2][NT][24][BVS];                 // Bv of the symbol's window, both variants
+    __shared__ double2 sbv[LR ? 1 : 2][NT][LR ? 1 : 24][BVS];   // Bv of the symbol's window, both variants
     __shared__ double2 bss[2][NT][NP];
+    __shared__ double twd[MIC_NB * 24 + MIC_NB];            // LR: T_k over the symbol's window + sums
     __shared__ int cntl[4][PM_MAXIT + 1];
     int ug, bi;
     band_block(ord, ma.nb, ug, bi);
@@ -2245,7 +2332,13 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     const int unit = ug * WAVE + w * 16 + ul, unit_mf = ug * WAVE + w * 16 + (l & 15);
     const int rl = unit % R;
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
-    {
+    if constexpr (LR) {
+        const int i = min(tid, MIC_NB * 25 - 1);
+        const double t = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
+        mic2_tables(tb, o, tid, 256);
+        mic2_rows(rpv, rdc, rpc, wrow, sk, o, row0, tid);
+        twd[i] = t;
+    } else {
         // every global load before the first LDS write (clamped, unconditional)
         constexpr int NBV = 2 * NT * 24 * NP, PER = (NBV + 255) / 256;
         double2 bvr[PER];
@@ -2267,10 +2360,11 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
         bss[var][q][p] = bsv;
     }
     __syncthreads();
-    auto A = [&](int var, int q, int j, int p) { return sbv[var][q][j][p]; };
+    auto A = [&](int var, int q, int j, int p) { return sbv[LR ? 0 : var][q][LR ? 0 : j][p]; };
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, false, NM>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
-                                              row0, unit, unit_mf, ul, l, r, U, R, rl, snr);
+    mic2_stages<NT, SH, NP, TRACE, false, NM, LR>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
+                                                  row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twd,
+                                                  twd + MIC_NB * 24);
     __syncthreads();
     for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
         const int s = i >> 1, edge = i & 1;
@@ -2561,7 +2655,7 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
 }
 
 unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm) {
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm, bool lr) {
     StorePerfectDetect o = chain_detect(sk, b, pd, 0);
     Mic2Args ma{};
     ma.bv = mm.Bv;
@@ -2574,17 +2668,27 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     ma.nblk = sk.QH.nblk;
     ma.niter = niter;
     ma.scheme = pd->scheme;
+    ma.bz = mm.Bz;
+    ma.za = b.za;
+    ma.tw = mm.Tw;
+    ma.ts = mm.Ts;
+    // the low-rank operator: built (build_mic_lr), MIC_NB pilot symbols, Z buffer;
+    // instantiated for the default networks (pilot: DPP, data: matrix cores)
+    const bool use_lr = lr && mm.Bz && mm.Tw && mm.Ts && b.za && mm.npb == MIC_NB;
     const int sh = pic_fft_shift(ch);
     // pilot symbols: one wave each, 16 units per block
     ma.blks = mm.pblk;
     ma.nb = mm.npb;
     if (part & 1) {
         const dim3 grid(b.U / 16), blk(64 * mm.npb);
+        const bool pnm = nm && !use_lr;
 #define LAUNCH_MP(NTV, SHV)                                                                                  \
     do {                                                                                                     \
-        if (b.tr && nm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, ma, o); \
+        if (use_lr && b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, false, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (use_lr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, false, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (b.tr && pnm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, ma, o); \
         else if (b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true>), grid, blk, 0, s, sk, ma, o);   \
-        else if (nm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (pnm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, ma, o); \
         else hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false>), grid, blk, 0, s, sk, ma, o);            \
     } while (0)
         if (ch.ntap == 1) LAUNCH_MP(1, 0);
@@ -2597,19 +2701,25 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     if (part & 2) {
         const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, xcd};
         const dim3 grid((b.U / WAVE) * mm.ndb), blk(256);
+        const bool dlr = use_lr && nm;
 #define LAUNCH_MD(NTV, SHV)                                                                                  \
     do {                                                                                                     \
-        if (b.tr && nm) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, om, ma, o); \
+        if (dlr && b.tr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true, true, true>), grid, blk, 0, s, sk, om, ma, o); \
+        else if (dlr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false, true, true>), grid, blk, 0, s, sk, om, ma, o); \
+        else if (b.tr && nm) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, om, ma, o); \
         else if (b.tr) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, true>), grid, blk, 0, s, sk, om, ma, o); \
         else if (nm) hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false, true>), grid, blk, 0, s, sk, om, ma, o); \
         else hipLaunchKernelGGL((k_mic_data<NTV, SHV, 16, false>), grid, blk, 0, s, sk, om, ma, o);         \
     } while (0)
+        if (use_lr && !dlr)
+            throw std::logic_error("launch_mmse_stages: the low-rank pilot pass needs the low-rank data pass "
+                                   "(mic_net bit 0)");
         if (ch.ntap == 1) LAUNCH_MD(1, 0);
         else if (sh == 1) LAUNCH_MD(2, 1);
         else LAUNCH_MD(2, 2);
 #undef LAUNCH_MD
     }
-    return PATH_MIC_FFT | PATH_MIC_STAGES;
+    return PATH_MIC_FFT | PATH_MIC_STAGES | (use_lr ? PATH_MIC_LR : 0u);
 }
 
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,

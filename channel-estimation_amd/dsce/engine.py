@@ -33,6 +33,7 @@ PATH_BITS = {
     "wpair3_fused": 1 << 0, "wpair3": 1 << 1, "wpair4m": 1 << 2, "wcontract_valu": 1 << 3, "pic_mfma": 1 << 4,
     "pic_chain": 1 << 5, "pic_passes": 1 << 6, "stage_fused": 1 << 7, "stage_split": 1 << 8, "noise_fused": 1 << 9,
     "pic_fft": 1 << 10, "mic_fft": 1 << 11, "txrx_fft": 1 << 12, "pilot_fused": 1 << 13, "mic_stages": 1 << 14,
+    "mic_lr": 1 << 15,
 }
 
 
@@ -398,10 +399,11 @@ class Engine:
 
     def structured_check(self, sid):
         """build_mic's guard of the structured MMSE IC (dsce_structured_check): dict with
-        ratio (kept iff <= 1), dev (max |Q' H_hat G - W_thr|), wmax (max |W|), rtol."""
-        out = (C.c_double * 4)()
+        ratio (kept iff <= 1), dev (max |Q' H_hat G - W_thr|), wmax (max |W|), rtol, and
+        the low-rank tap operator's fit residual lr_resid (relative) and lr (in use)."""
+        out = (C.c_double * 6)()
         self._chk(self.lib.dsce_structured_check(self.h, int(sid), out), "dsce_structured_check")
-        return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3])
+        return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3], lr_resid=out[4], lr=bool(out[5]))
 
     def work_model(self, sid):
         cm = C.c_double()

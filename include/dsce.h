@@ -201,6 +201,8 @@ typedef struct {
 #define DSCE_PATH_PILOT_FUSED     (1u << 13)  /* retired in r03 (k_mic_fft's fused pilot pass); never set     */
 #define DSCE_PATH_MIC_STAGES      (1u << 14)  /* k_mic_pilot + k_mic_data: every MMSE stage of an FFT-form OFDM
                                                  scheme in one launch pair; k_pic_fft with the perfect-CSI stage 0 */
+#define DSCE_PATH_MIC_LR          (1u << 15)  /* ... with the low-rank tap operator: taps = T_k Z, Z = Bz hP once per
+                                                 unit and stage (dsce_structured_check out[5]) */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -312,6 +314,8 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   tx_rows (1: TX symbols of a row-local precoder drawn row-parallel), snr_base
  *   (0..255: the noise of SNR index k is sub-stream snr_base + k, so a rank
  *   serving SNR points [b, ...) of a sweep draws the one-rank run's noise),
+ *   mic_lr (1: the MMSE IC's estimated taps in the low-rank form T_k Z where the
+ *   fit reproduces Bv to rounding, dsce_structured_check; 0: the tap GEMM Bv hP),
  *   pic_skip (1: k_pic_fft stops a wave of 16 units x one symbol at the
  *   perfect-CSI IC's fixed point — an iteration that repeats the previous
  *   decisions of every data row is repeated exactly by every later one, whose
@@ -348,8 +352,12 @@ int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, d
  * max |Q' H_hat G - W_thr| / (out[3] max |W|) over every entry the IC uses
  * (the path is kept iff <= 1), out[1] = the largest absolute deviation, out[2]
  * = the largest |W|, out[3] = the relative tolerance (rounding level, 1e-11).
- * out[0..2] = -1 when the scheme is not eligible (the W contraction runs). */
-int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out4);
+ * out[0..2] = -1 when the scheme is not eligible (the W contraction runs).
+ * The low-rank form of its tap operator (Bv = T Bz, T_k the J0 kernel summed
+ * over pilot symbol k's window; option mic_lr): out[4] = max |Bv - T Bz| /
+ * max |Bv| of the fit (-1: not attempted), out[5] = 1 if it is in use (the fit
+ * is within 1e-13), else 0. */
+int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out6);
 /* Measured FP64 matrix-core peak of the context's GPU: back-to-back
  * v_mfma_f64_16x16x4_f64 on independent accumulators, 8 waves per SIMD,
  * best of 3 timed launches (TFLOP/s). */

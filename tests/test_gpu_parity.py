@@ -97,7 +97,7 @@ def test_mmse_estimator_matches_oracle(ofdm):
 # stage of the MMSE branch (Q' H_hat G by FFT)), and the W contraction
 # (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"mic_fft", "mic_stages", "pic_fft", "noise_fused", "txrx_fft"}
+BENCH_PATH = {"mic_fft", "mic_stages", "mic_lr", "pic_fft", "noise_fused", "txrx_fft"}
 W_PATH = {"wpair3_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
 
 
@@ -335,6 +335,9 @@ def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
     assert "mic_fft" in eng.path_info(0)
     chk = eng.structured_check(0)
     assert 0.0 <= chk["ratio"] <= 1.0 and chk["dev"] <= 1e-11 * chk["wmax"], chk
+    # the low-rank form of the tap operator reproduces Bv to rounding and is used
+    assert chk["lr"] and 0.0 <= chk["lr_resid"] <= 1e-13, chk
+    assert "mic_lr" in eng.path_info(0)
     eng.close()
 
 
@@ -413,7 +416,9 @@ def test_stage_variants_agree(name):
     banded passes instead of k_txrx_fft, the TX symbols one realisation per
     lane (k_tx_symbols, the fallback for non-row-local precoders), k_pic_fft's
     4-point network by DPP instead of on the matrix cores (and k_mic_pilot /
-    k_mic_data's, with the tap GEMM's exchange by ds_bpermute)."""
+    k_mic_data's, with the tap GEMM's exchange by ds_bpermute), the tap GEMM
+    Bv hP instead of the low-rank operator T_k Z (mic_lr 0), every perfect-CSI
+    iteration computed instead of stopping at the fixed point (pic_skip 0)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -430,7 +435,7 @@ def test_stage_variants_agree(name):
                 {"jakes_win": 0}, {"txrx_fft": 0}, {"mmse_ic": 0, "fuse_stage": 0, "pic_chain": 0},
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
-                {"mic_net": 0, "pic_net": 0})
+                {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
