@@ -401,9 +401,10 @@ class Engine:
         """build_mic's guard of the structured MMSE IC (dsce_structured_check): dict with
         ratio (kept iff <= 1), dev (max |Q' H_hat G - W_thr|), wmax (max |W|), rtol, and
         the low-rank tap operator's fit residual lr_resid (relative) and lr (in use)."""
-        out = (C.c_double * 6)()
+        out = (C.c_double * 7)()
         self._chk(self.lib.dsce_structured_check(self.h, int(sid), out), "dsce_structured_check")
-        return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3], lr_resid=out[4], lr=bool(out[5]))
+        return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3], lr_resid=out[4], lr=bool(out[5]),
+                    lr_ratio=out[6])
 
     def work_model(self, sid):
         cm = C.c_double()

@@ -44,7 +44,7 @@
  *            on the GPU from the object's Nr / PHY / Implementation / PrototypeFilter properties
  *   dsce_mex('enable_mse', on)                                      % start (and reset) the MSE sums of 'run'
  *   [err, pow] = dsce_mex('get_mse')                                % err [iter+1, snr, scheme], pow [snr, scheme]
- *   c = dsce_mex('structured_check', id)                           % [ratio, max dev, max |W|, rtol, lr fit, lr used]
+ *   c = dsce_mex('structured_check', id)                           % [ratio, max dev, max |W|, rtol, lr fit, lr used, lr ratio]
  */
 #ifdef MATLAB_MEX_FILE
 #include <math.h>
@@ -517,12 +517,12 @@ static void c_get_mse(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]
 }
 
 static void c_structured_check(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
-    double c[6];
+    double c[7];
     int k;
     (void)nlhs; (void)nrhs;
     check(dsce_structured_check(g_ctx, scheme_id(prhs[1], 1), c), "dsce_structured_check");
-    plhs[0] = mxCreateDoubleMatrix(1, 6, mxREAL);
-    for (k = 0; k < 6; ++k) DSCE_DOUBLES(plhs[0])[k] = c[k];
+    plhs[0] = mxCreateDoubleMatrix(1, 7, mxREAL);
+    for (k = 0; k < 7; ++k) DSCE_DOUBLES(plhs[0])[k] = c[k];
 }
 
 static const struct {

@@ -355,9 +355,10 @@ int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, d
  * out[0..2] = -1 when the scheme is not eligible (the W contraction runs).
  * The low-rank form of its tap operator (Bv = T Bz, T_k the J0 kernel summed
  * over pilot symbol k's window; option mic_lr): out[4] = max |Bv - T Bz| /
- * max |Bv| of the fit (-1: not attempted), out[5] = 1 if it is in use (the fit
- * is within 1e-13), else 0. */
-int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out6);
+ * max |Bv| of the fit (-1: not attempted), out[5] = 1 if it is in use, else 0,
+ * out[6] = the worst slice's deviation over its rounding bar max(1e-13,
+ * 4e-16 ||R||_1 ||pinv(R)||_1) max |Bv| (the operator is used iff <= 1). */
+int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out7);
 /* Measured FP64 matrix-core peak of the context's GPU: back-to-back
  * v_mfma_f64_16x16x4_f64 on independent accumulators, 8 waves per SIMD,
  * best of 3 timed launches (TFLOP/s). */

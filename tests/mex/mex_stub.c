@@ -289,6 +289,6 @@ int dsce_get_mse(dsce_ctx* c, double* err, double* pw) {
 int dsce_structured_check(dsce_ctx* c, int32_t id, double* out) {
     (void)c;
     if (id != 0) return DSCE_EINVAL;
-    out[0] = 0.07; out[1] = 3e-13; out[2] = 0.59; out[3] = 1e-11; out[4] = 2e-16; out[5] = 1.0;
+    out[0] = 0.07; out[1] = 3e-13; out[2] = 0.59; out[3] = 1e-11; out[4] = 2e-16; out[5] = 1.0; out[6] = 0.01;
     return 0;
 }

@@ -199,7 +199,7 @@ def test_outputs_sized_from_engine_state(results):
     # the object's properties reach dsce_tx_desc (mex_stub.c checks every field)
     assert results["tx_matrices_ofdm"] == ("OK", "540x336") and results["tx_matrices_fbmc"] == ("OK", "540x720")
     assert results["get_mse"] == ("OK", "5x7")                          # [iter+1, snr, scheme]
-    assert results["structured_check"] == ("OK", "1x6")
+    assert results["structured_check"] == ("OK", "1x7")
 
 
 def test_arity_and_argument_checks(results):
