@@ -2009,8 +2009,10 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     // per lane, for diag(D_hat_s)); the data kernel prefetches both for stage
     // s + 1 at the end of stage s and folds hn4 into the window sums sn at once
     double2 hb[LR ? 1 : NP / 4], hn4[LR ? 1 : NP / 4];
-    // LR: Z of the previous stage (the taps) and of this stage (diag), whole unit per lane
-    double2 zp[LR ? NZ : 1], zc[LR ? NZ : 1];
+    // LR: Z of the previous stage (the taps) and of this stage (diag), whole unit per
+    // lane (the data kernel; the pilot kernel reads them from its LDS szz instead)
+    constexpr int NZR = LR && !PIL ? NZ : 1;
+    double2 zp[NZR], zc[NZR];
     // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s: window sums sn0 / sn1
     auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
         sn0 = sn1 = make_double2(0.0, 0.0);
@@ -2018,11 +2020,14 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         if constexpr (LR) {
 #pragma unroll
             for (int q = 0; q < NT; ++q) {
-                double2 sq = make_double2(tsl[0] * zc[q * MIC_NB].x, tsl[0] * zc[q * MIC_NB].y);
+                double2 zk[MIC_NB];
+#pragma unroll
+                for (int k = 0; k < MIC_NB; ++k) zk[k] = PIL ? szz[s & 1][q * MIC_NB + k][ul] : zc[(q * MIC_NB + k) % NZR];
+                double2 sq = make_double2(tsl[0] * zk[0].x, tsl[0] * zk[0].y);
 #pragma unroll
                 for (int k = 1; k < MIC_NB; ++k) {
-                    sq.x = fma(tsl[k], zc[q * MIC_NB + k].x, sq.x);
-                    sq.y = fma(tsl[k], zc[q * MIC_NB + k].y, sq.y);
+                    sq.x = fma(tsl[k], zk[k].x, sq.x);
+                    sq.y = fma(tsl[k], zk[k].y, sq.y);
                 }
                 if ((SH >> q) & 1) {
                     sn1 = f1 ? sq : c_add(sn1, sq);
@@ -2066,13 +2071,12 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         asm volatile("" : "+v"(oz));
         const int ro = r + oz;
         double2 sn0, sn1;
-        if (LR) {
+        if (LR && !PIL) {
 #pragma unroll
-            for (int j = 0; j < NZ; ++j) zp[j] = zc[j];
-            if (!PIL)                                    // this stage's Z (the pilot kernel forms it below)
+            for (int j = 0; j < NZR; ++j) zp[j] = zc[j];
 #pragma unroll
-                for (int j = 0; j < NZ; ++j) zc[j] = ma.za[((size_t)s * NZ + j) * U + unit];
-        } else if (!PIL) {
+            for (int j = 0; j < NZR; ++j) zc[j] = ma.za[((size_t)s * NZ + j) * U + unit];     // this stage's Z
+        } else if (!LR && !PIL) {
 #pragma unroll
             for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
         }
@@ -2092,11 +2096,15 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                     for (int k = 0; k < MIC_NB; ++k) tk[k] = twl[k * 24 + 6 * cq + a + oz];
 #pragma unroll
                     for (int q = 0; q < NT; ++q) {
-                        double2 t = make_double2(tk[0] * zp[q * MIC_NB].x, tk[0] * zp[q * MIC_NB].y);
+                        double2 zk[MIC_NB];
+#pragma unroll
+                        for (int k = 0; k < MIC_NB; ++k)
+                            zk[k] = PIL ? szz[(s - 1) & 1][q * MIC_NB + k][ul] : zp[(q * MIC_NB + k) % NZR];
+                        double2 t = make_double2(tk[0] * zk[0].x, tk[0] * zk[0].y);
 #pragma unroll
                         for (int k = 1; k < MIC_NB; ++k) {
-                            t.x = fma(tk[k], zp[q * MIC_NB + k].x, t.x);
-                            t.y = fma(tk[k], zp[q * MIC_NB + k].y, t.y);
+                            t.x = fma(tk[k], zk[k].x, t.x);
+                            t.y = fma(tk[k], zk[k].y, t.y);
                         }
                         taps[a][q] = t;
                     }
@@ -2150,8 +2158,6 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                     ma.za[((size_t)s * NZ + j) * U + unit0 + u] = acc;
                 }
                 __syncthreads();
-#pragma unroll
-                for (int j = 0; j < NZ; ++j) zc[j] = szz[s & 1][j][ul];
             } else {
 #pragma unroll
                 for (int k = 0; k < NP / 4; ++k) hn4[k] = hx[(r * (NP / 4) + k) * 17 + ul];
@@ -2673,7 +2679,7 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     ma.tw = mm.Tw;
     ma.ts = mm.Ts;
     // the low-rank operator: built (build_mic_lr), MIC_NB pilot symbols, Z buffer;
-    // instantiated for the default networks (pilot: DPP, data: matrix cores)
+    // the data pass on the matrix-core network (the caller requires mic_net bit 0)
     const bool use_lr = lr && mm.Bz && mm.Tw && mm.Ts && b.za && mm.npb == MIC_NB;
     const int sh = pic_fft_shift(ch);
     // pilot symbols: one wave each, 16 units per block
@@ -2681,10 +2687,12 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     ma.nb = mm.npb;
     if (part & 1) {
         const dim3 grid(b.U / 16), blk(64 * mm.npb);
-        const bool pnm = nm && !use_lr;
+        const bool pnm = nm;
 #define LAUNCH_MP(NTV, SHV)                                                                                  \
     do {                                                                                                     \
-        if (use_lr && b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, false, true>), grid, blk, 0, s, sk, ma, o); \
+        if (use_lr && b.tr && pnm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, true, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (use_lr && pnm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, true, true>), grid, blk, 0, s, sk, ma, o); \
+        else if (use_lr && b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, false, true>), grid, blk, 0, s, sk, ma, o); \
         else if (use_lr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, false, false, true>), grid, blk, 0, s, sk, ma, o); \
         else if (b.tr && pnm) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true, true>), grid, blk, 0, s, sk, ma, o); \
         else if (b.tr) hipLaunchKernelGGL((k_mic_pilot<NTV, SHV, 16, true>), grid, blk, 0, s, sk, ma, o);   \
