@@ -97,7 +97,15 @@ def test_mmse_estimator_matches_oracle(ofdm):
 # stage of the MMSE branch (Q' H_hat G by FFT)), and the W contraction
 # (k_pilot_pre + fused k_wpair3 epilogue, mmse_ic 0) alongside.
 # ---------------------------------------------------------------------------
-BENCH_PATH = {"mic_fft", "mic_stages", "mic_lr", "pic_fft", "noise_fused", "txrx_fft"}
+BENCH_BASE = {"mic_fft", "mic_stages", "pic_fft", "noise_fused", "txrx_fft"}
+
+
+def bench_path(eng):
+    """The bench path's kernels; the low-rank tap operator (k_mic_pilot /
+    k_mic_data LR) when the engine's mic_lr option is on (its default)."""
+    return BENCH_BASE | ({"mic_lr"} if eng.get_option("mic_lr") else set())
+
+
 W_PATH = {"wpair3_fused", "pic_fft", "stage_fused", "noise_fused", "txrx_fft"}
 
 
@@ -128,7 +136,7 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
     from k_stage_fused, k_pic_fft without its stage 0)."""
     S, eng, mm = ofdm
     rows = S.schemes["ofdm"]["data_pos"]
-    for mic, path in ((1, BENCH_PATH), (0, W_PATH)):
+    for mic, path in ((1, bench_path(eng)), (0, W_PATH)):
         eng.set_option("mmse_ic", mic)
         for rep in (5, 70):
             tr = {}
@@ -153,7 +161,7 @@ def test_error_counts_match_oracle(ofdm):
     for first, n in ((0, 64), (128, 128)):
         eng.set_batch(n)
         cg = eng.run(SEED, first, n)
-        assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+        assert bench_path(eng) <= eng.path_info(0), eng.path_info(0)
         res = harness.simulate(S, SEED, first, n, ["ofdm"])
         assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (first, cg - res["err"])
         if first == 0:
@@ -179,7 +187,7 @@ def test_ic_iteration_counts_match_oracle(n_iter):
     eng = harness.engine(S, batch=64)
     cg = eng.run(SEED, 0, 64)
     path = eng.path_info(0)
-    assert BENCH_PATH <= path, path
+    assert bench_path(eng) <= path, path
     eng.set_option("mmse_ic", 0)                # the W contraction, per-stage launches
     assert np.array_equal(eng.run(SEED, 0, 64), cg)
     assert W_PATH <= eng.path_info(0), eng.path_info(0)
@@ -286,7 +294,7 @@ def test_any_repetition_count(ofdm):
     S, eng, _ = ofdm
     eng.enable_mse()
     c25 = eng.run(SEED, 0, 25)
-    assert BENCH_PATH <= eng.path_info(0), eng.path_info(0)
+    assert bench_path(eng) <= eng.path_info(0), eng.path_info(0)
     res = harness.simulate(S, SEED, 0, 25, ["ofdm"])
     assert np.abs(c25 - res["err"]).sum() <= 8 * res["borderline"].sum(), c25 - res["err"]
     _check_mse(eng, res)
@@ -330,7 +338,7 @@ def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
     # thresholded W to rounding (oracle, tools/threshold_study.py: <= 7e-13
     # absolute at max|W| 0.41-0.59)
     S.zero_threshold = 1e-8
-    eng = harness.engine(S, batch=64)
+    eng = harness.engine(S, batch=64, options={"mic_lr": 1})
     eng.run(SEED, 0, 64)
     assert "mic_fft" in eng.path_info(0)
     chk = eng.structured_check(0)
@@ -515,8 +523,7 @@ def test_pic_fixed_point_skip_is_exact():
     a unit, decisions and y_perf included."""
     S = harness.setup("default", schemes=("ofdm",))
     full = harness.engine(S, batch=256, options={"pic_skip": 0})
-    fast = harness.engine(S, batch=256)
-    assert fast.get_option("pic_skip") == 1
+    fast = harness.engine(S, batch=256, options={"pic_skip": 1})
     np.testing.assert_array_equal(fast.run(SEED, 0, 512), full.run(SEED, 0, 512))
     for k in (0, 6):
         a, b = fast.trace_unit(0, SEED, 21, k), full.trace_unit(0, SEED, 21, k)

@@ -7,4 +7,6 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 50 --option pic_s
 tail -1 gpurun_out/r04b/bench_old.log | cut -c1-300
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 50 --option mic_lr=0 > gpurun_out/r04b/bench_skip.log 2>&1 || { echo bench1_fail; tail -5 gpurun_out/r04b/bench_skip.log; exit 1; }
 tail -1 gpurun_out/r04b/bench_skip.log | cut -c1-300
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 50 --option mic_net=3 > gpurun_out/r04b/bench_pnm.log 2>&1 || { echo bench2_fail; tail -5 gpurun_out/r04b/bench_pnm.log; exit 1; }
+tail -1 gpurun_out/r04b/bench_pnm.log | cut -c1-300
 bash tools/gpu_bench_evidence.sh r04b c2 k_mic_data k_mic_data
