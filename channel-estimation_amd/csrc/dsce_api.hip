@@ -133,6 +133,8 @@ struct Scheme {
     // slices of max |Q' H_hat G - W_thresholded| / (MIC_RTOL max |W|), the largest
     // absolute deviation and the largest |W|; -1 = not evaluated
     double mic_check = -1.0, mic_dev = -1.0, mic_wmax = -1.0;
+    // build_poly: largest |G - A w C| / max|G| or the same of Q (-1: not evaluated)
+    double poly_resid = -1.0;
 };
 
 }  // namespace dsce
@@ -156,7 +158,7 @@ struct dsce_ctx {
     int jakes_kind = 0;                   // which Jakes kernel the last batch ran (JAKES_KIND_*)
     size_t jk_nsch = (size_t)-1;          // scheme count jk was computed for
     McBuffers buf{};
-    size_t buf_key[7] = {0, 0, 0, 0, 0, 0, 0};
+    size_t buf_key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<void*> buf_allocs;
     unsigned long long* d_counters = nullptr;
     size_t counters_n = 0;
@@ -270,6 +272,99 @@ void check_ctx(dsce_ctx* c) {
 Scheme& get_scheme(dsce_ctx* c, int id) {
     if (id < 0 || id >= (int)c->schemes.size()) throw ApiError(DSCE_EINVAL, "bad scheme id");
     return *c->schemes[id];
+}
+
+// ---------------------------------------------------------------------------
+// Polyphase form of G and Q (SchemeK::poly_ok; the perfect-CSI IC passes
+// k_poly_syn / k_poly_chan / k_poly_ana).  M = G or Q (N x LK, column l + L k):
+// every symbol's columns are one real window times the subcarrier tones,
+//   M[n, l + L k] = A_k[n] w^(l n) C[l][k],   w = e^(2 pi i / L)
+// (FBMC: Hermite prototype p(t - k T/2) times e^(i 2 pi l F (t - k T/2)) and the
+// OQAM phase, FBMC.m:255-285 / :318-354; OFDM: its CP / FFT window, OFDM.m:153-218).
+// A_k is column 0 with its largest entry's phase removed, C follows from that
+// entry; the factorisation is then checked on every entry of M.  Returns the
+// largest |M - A w C| / max |M| (2 if a window is not real).
+// ---------------------------------------------------------------------------
+double poly_factor(const std::vector<double2>& M, int N, int L, int K, std::vector<double>& A,
+                   std::vector<double2>& C) {
+    A.assign((size_t)K * N, 0.0);
+    C.assign((size_t)K * L, make_double2(0, 0));
+    std::vector<double2> wt(L);
+    for (int e = 0; e < L; ++e) wt[e] = make_double2(std::cos(2.0 * M_PI * e / L), std::sin(2.0 * M_PI * e / L));
+    double mmax = 0.0;
+    for (auto& z : M) mmax = std::max(mmax, std::hypot(z.x, z.y));
+    if (!(mmax > 0.0)) return 2.0;
+    double worst = 0.0;
+    for (int k = 0; k < K; ++k) {
+        const double2* c0 = &M[(size_t)(L * k) * N];
+        int ns = 0;
+        for (int n = 1; n < N; ++n)
+            if (std::hypot(c0[n].x, c0[n].y) > std::hypot(c0[ns].x, c0[ns].y)) ns = n;
+        const double g = std::hypot(c0[ns].x, c0[ns].y);
+        if (!(g > 0.0)) return 2.0;
+        const double2 ph = make_double2(c0[ns].x / g, -c0[ns].y / g);      // conj(c0[ns]) / |c0[ns]|
+        for (int n = 0; n < N; ++n) {
+            const double2 a = c_mul(c0[n], ph);
+            if (std::fabs(a.y) > 1e-12 * mmax) return 2.0;
+            A[(size_t)k * N + n] = a.x;
+        }
+        for (int l = 0; l < L; ++l) {
+            const double2 wn = wt[(size_t)(((long long)l * ns) % L)];
+            const double2 z = c_mul(M[(size_t)(l + L * k) * N + ns], make_double2(wn.x, -wn.y));
+            C[(size_t)k * L + l] = make_double2(z.x / g, z.y / g);
+        }
+        for (int l = 0; l < L; ++l) {
+            const double2 cl = C[(size_t)k * L + l];
+            const double2* col = &M[(size_t)(l + L * k) * N];
+            for (int n = 0; n < N; ++n) {
+                const double2 wv = wt[(size_t)(((long long)l * n) % L)];
+                const double2 f = c_scale(c_mul(wv, cl), A[(size_t)k * N + n]);
+                worst = std::max(worst, std::hypot(col[n].x - f.x, col[n].y - f.y) / mmax);
+            }
+        }
+    }
+    return worst;
+}
+
+// SchemeK::poly_* from the host G and Q when both factorise to 1e-12 (the
+// tolerance of the OFDM FFT form's check, pack_scheme) with F = L = 24 or 48
+void build_poly(dsce_ctx* c, Scheme& s) {
+    SchemeK& k = s.k;
+    k.poly_ok = 0;
+    const int N = s.N, L = s.d.n_subcarriers, K = s.d.n_symbols;
+    if ((L != 24 && L != 48) || L * K != s.LK || N <= 0) return;
+    const int ni = (N + L - 1) / L;
+    if (ni > POLY_NI) return;
+    std::vector<double> Ag, Aq;
+    std::vector<double2> Cg, Cq;
+    const double rg = poly_factor(s.G, N, L, K, Ag, Cg);
+    const double rq = poly_factor(s.Q, N, L, K, Aq, Cq);
+    s.poly_resid = std::max(rg, rq);
+    if (!(s.poly_resid <= 1e-12)) return;
+    // per residue m: the windows at n = m + L j, zero past N
+    std::vector<double> pa((size_t)L * K * POLY_NI, 0.0), pb((size_t)L * K * POLY_NI, 0.0);
+    for (int m = 0; m < L; ++m)
+        for (int kk = 0; kk < K; ++kk)
+            for (int j = 0; j < POLY_NI; ++j) {
+                const int n = m + L * j;
+                if (n >= N) continue;
+                pa[((size_t)m * K + kk) * POLY_NI + j] = Ag[(size_t)kk * N + n];
+                pb[((size_t)m * K + kk) * POLY_NI + j] = Aq[(size_t)kk * N + n];
+            }
+    // Q^H[l + L k, n] = conj(Q) = B_k[n] w^(-l n) conj(Cq[l][k]): E = conj(Cq)
+    std::vector<double2> E(Cq.size());
+    for (size_t i = 0; i < Cq.size(); ++i) E[i] = make_double2(Cq[i].x, -Cq[i].y);
+    std::vector<double2> tw(L);
+    for (int e = 0; e < L; ++e) tw[e] = make_double2(std::cos(2.0 * M_PI * e / L), std::sin(2.0 * M_PI * e / L));
+    k.poly_F = L;
+    k.poly_K = K;
+    k.poly_ni = ni;
+    k.poly_C = dupload(c, Cg);
+    k.poly_E = dupload(c, E);
+    k.poly_A = dupload(c, pa);
+    k.poly_B = dupload(c, pb);
+    k.poly_tw = dupload(c, tw);
+    k.poly_ok = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -502,6 +597,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
     k.GL = s.GL;
     s.wband_struct = s.wband;
     s.Wb = upload_band(c, s.wband, false);
+    build_poly(c, s);
     // fused-stage maps (select mode): data index per row; row-local precoder
     {
         std::vector<int> row_data(LK, -1), row_pcol(LK, -1);
@@ -1126,7 +1222,9 @@ void ensure_buffers(dsce_ctx* c, int R) {
         NP = std::max<size_t>(NP, s->d.n_pilots);
         ND = std::max<size_t>(ND, s->d.n_data);
     }
-    const size_t key[7] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c), (size_t)c->niter};
+    bool poly = false;      // polyphase perfect-CSI IC scratch, only for schemes that have the form
+    for (auto& sp : c->schemes) poly = poly || sp->k.poly_ok;
+    const size_t key[8] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c), (size_t)c->niter, (size_t)poly};
     if (memcmp(key, c->buf_key, sizeof(key)) == 0) return;
     for (void* p : c->buf_allocs) (void)hipFree(p);
     c->buf_allocs.clear();
@@ -1167,6 +1265,9 @@ void ensure_buffers(dsce_ctx* c, int R) {
     b.hpa = dalloc<double2>(c, (size_t)b.hpa_stages * NP * U, L);
     // Z = Bz hP of every stage (low-rank MMSE IC operator, k_mic_pilot -> k_mic_data)
     b.za = dalloc<double2>(c, (size_t)b.hpa_stages * std::max(1, std::min(c->ch.ntap, 2)) * MIC_NB * U, L);
+    // polyphase perfect-CSI IC scratch (V and the window sums)
+    b.pv = poly ? dalloc<double2>(c, LK * U, L) : nullptr;
+    b.pf = poly ? dalloc<double2>(c, LK * U, L) : nullptr;
     DSCE_HIP_CHECK(hipMemsetAsync(b.sidr, 0, (LK + 32) * R * sizeof(uint16_t), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));
@@ -2235,7 +2336,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr) X(pic_poly)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

@@ -163,7 +163,19 @@ struct SchemeK {
     int pf_ok;
     double2 pf_scale;
     double2 pf_gs, pf_qs;         // the two factors: G block = gs w^(l m), Q^H block = qs w^(-l m)
+    // polyphase form (poly_ok, build_poly): with w = e^(2 pi i / L) and F = L,
+    //   G[n, l + L k] = A_k[n] w^(l n) C[l][k],   Q^H[l + L k, n] = B_k[n] w^(-l n) E[l][k]
+    // (A_k, B_k real windows), so G u = sum_k A_k IDFT(C u_k)(n mod F) and
+    // (Q^H r)_k = E DFT(fold_k), fold_k[m] = sum_{n = m mod F} B_k[n] r[n]
+    int poly_ok, poly_ni;         // poly_ni = ceil(N / F) <= POLY_NI
+    int poly_F, poly_K;           // DFT size F = L, symbols K
+    const double2* poly_C;        // [K][F]
+    const double2* poly_E;        // [K][F]
+    const double* poly_A;         // [F][K][POLY_NI]: A_k[m + F j] (0 outside [0, N))
+    const double* poly_B;         // [F][K][POLY_NI]
+    const double2* poly_tw;       // w^e, e = 0..F-1
 };
+constexpr int POLY_NI = 24;       // samples per residue class the polyphase kernels hold
 
 struct ChannelK {
     int N, ntap;                  // ntap = number of non-zero taps

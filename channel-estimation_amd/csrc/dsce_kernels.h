@@ -34,6 +34,9 @@ struct Opts {
                               // build_mic_lr verified it; 0 = the tap GEMM Bv hP on the matrix cores
     int pic_skip = 1;         // k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
                               // iterations are copies); 0 = compute every iteration
+    int pic_poly = 0;         // perfect-CSI IC passes of polyphase schemes (SchemeK::poly_ok: FBMC, OFDM with
+                              // L != 24) as IDFT-L per symbol + window sums per residue + DFT-L per symbol
+                              // (k_poly_syn / k_poly_chan / k_poly_ana) instead of the two banded passes
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower
@@ -58,6 +61,7 @@ enum : unsigned {
     PATH_PILOT_FUSED = 1u << 13,   // retired (r02 k_mic_fft's fused pilot pass)
     PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair
     PATH_MIC_LR = 1u << 15,        // ... with the low-rank tap operator T_k Z (build_mic_lr)
+    PATH_PIC_POLY = 1u << 16,      // perfect-CSI IC by polyphase synthesis / analysis (k_poly_*)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one
@@ -108,6 +112,8 @@ struct McBuffers {
     double2* hpa;     // [stage][NP][U] LS pilot estimates of every stage (k_mic_pilot -> k_mic_data), or null
     int hpa_stages;   // stages hpa holds
     double2* za;      // [stage][ntap * MIC_NB][U] Z = Bz hP of every stage (low-rank MMSE IC), or null
+    double2* pv;      // [LK][U] polyphase IC: IDFT of each symbol's C u (k_poly_syn), or null
+    double2* pf;      // [LK][U] polyphase IC: window sums of r0 per (symbol, residue) (k_poly_chan), or null
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
     const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)

@@ -2764,14 +2764,259 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     return PATH_PIC_FFT;
 }
 
+// ---------------------------------------------------------------------------
+// Perfect-CSI IC of polyphase schemes (SchemeK::poly_ok, build_poly in
+// dsce_api.hip): D u = Q^H H G u (script:541-543) without the two banded passes.
+// Every column of symbol k of G is a real window times a subcarrier tone,
+// G[n, l + L k] = A_k[n] w^(l n) C[l][k] (FBMC: the Hermite prototype shifted by
+// k TimeSpacing, FBMC.m:255-285 / :318-354; w = e^(2 pi i / F), F = L), so
+//   t = G u:      t[n] = sum_k A_k[n] V_k[n mod F],  V_k = IDFT_F(C_k u_k)
+//   r0 = H t:     r0[n] = sum_q IR_q[n] t[n - d_q]  (FastFading.m:284)
+//   Q^H r0:       out[l + L k] = E[l][k] DFT_F(fold_k)[l],
+//                 fold_k[m] = sum_{n = m mod F} B_k[n] r0[n]
+// FBMC at C3 (F = 24, 30 symbols, windows of 192 samples): 2 x 30 DFT-24 and
+// 2 x 540 x 16 window products per unit instead of 2 x 138 k complex MACs.
+// k_poly_syn (symbol-major) writes V, k_poly_chan (residue-major: the samples
+// n = m + F j of one residue m are one register array) writes fold, k_poly_ana
+// (symbol-major) transforms and hands each row to the pass-2 epilogue (Out:
+// StorePerfectIC, or StorePerfectDetect for row-local precoders).  Lane = unit.
+// ---------------------------------------------------------------------------
+struct PolyArgs {
+    const double2* __restrict__ u;    // [LK][U]
+    double2* __restrict__ v;          // [LK][U]  V_k[m] at row k F + m
+    double2* __restrict__ fo;         // [LK][U]  fold_k[m] at row k F + m
+    const double2* __restrict__ C;    // [K][F]
+    const double2* __restrict__ E;    // [K][F]
+    const double* __restrict__ A;     // [F][K][POLY_NI]
+    const double* __restrict__ B;     // [F][K][POLY_NI]
+    const double2* __restrict__ tw;   // w^e, e = 0..F-1
+    const double2* __restrict__ ir;   // [ntap][N][R]
+    int U, R, K, N, xcd;
+    int delay[4];
+};
+
+// x * w^(S e) (e a compile-time exponent after unrolling: the table entry is a
+// uniform load, and e = 0 mod F costs nothing)
+template <int F, int S>
+__device__ __forceinline__ double2 poly_tw(double2 x, int e, const double2* __restrict__ tw) {
+    const int i = ((S * e) % F + F) % F;
+    if (i == 0) return x;
+    return c_mulf(x, tw[i]);
+}
+
+// y[m] = sum_l x[l] w^(S l m), F = 3 F2: DFT-3 over l1 (l = F2 l1 + l2), twiddle
+// w^(S l2 m1), then a DFT-F2 over l2 per m1 (m = m1 + 3 m2), each output handed
+// to emit(m, y[m]) as soon as it is formed.  x is overwritten.
+template <int F, int S, class Emit>
+__device__ __forceinline__ void poly_dft(double2 (&x)[F], const double2* __restrict__ tw, Emit&& emit) {
+    static_assert(F % 3 == 0, "F = 3 F2");
+    constexpr int F2 = F / 3;
+    constexpr double H3 = 0.86602540378443864676;   // sqrt(3) / 2
+#pragma unroll
+    for (int l2 = 0; l2 < F2; ++l2) {
+        const double2 x0 = x[l2], x1 = x[F2 + l2], x2 = x[2 * F2 + l2];
+        const double2 sm = c_add(x1, x2), df = c_sub(x1, x2);
+        const double2 mm = make_double2(fma(-0.5, sm.x, x0.x), fma(-0.5, sm.y, x0.y));
+        const double2 jd = make_double2(-S * H3 * df.y, S * H3 * df.x);   // j S (sqrt 3 / 2) (x1 - x2)
+        x[l2] = c_add(x0, sm);
+        x[F2 + l2] = poly_tw<F, S>(c_add(mm, jd), l2, tw);
+        x[2 * F2 + l2] = poly_tw<F, S>(c_sub(mm, jd), 2 * l2, tw);
+    }
+#pragma unroll
+    for (int m1 = 0; m1 < 3; ++m1)
+#pragma unroll
+        for (int m2 = 0; m2 < F2; ++m2) {
+            double2 acc = x[F2 * m1];
+#pragma unroll
+            for (int l2 = 1; l2 < F2; ++l2) {
+                const int i = ((S * 3 * l2 * m2) % F + F) % F;
+                if (i == 0) acc = c_add(acc, x[F2 * m1 + l2]);
+                else c_fma(acc, x[F2 * m1 + l2], tw[i]);
+            }
+            emit(m1 + 3 * m2, acc);
+        }
+}
+
+// block -> (unit group, index) with the index fastest, XCD-aware
+__device__ __forceinline__ void poly_block(int nidx, int xcd, int& ug, int& idx) {
+    int L = blockIdx.x;
+    if (xcd) L = xcd_remap(L, gridDim.x);
+    idx = L % nidx;
+    ug = L / nidx;
+}
+
+template <int F>
+__global__ void __launch_bounds__(64) k_poly_syn(PolyArgs pa) {
+    int ug, k;
+    poly_block(pa.K, pa.xcd, ug, k);
+    const int lane = ug * WAVE + threadIdx.x;
+    const double2* __restrict__ cg = pa.C + (size_t)k * F;
+    double2 x[F];
+#pragma unroll
+    for (int l = 0; l < F; ++l) x[l] = c_mulf(cg[l], pa.u[(size_t)(k * F + l) * pa.U + lane]);
+    double2* __restrict__ out = pa.v + (size_t)k * F * pa.U + lane;
+    poly_dft<F, 1>(x, pa.tw, [&](int m, double2 y) { out[(size_t)m * pa.U] = y; });
+}
+
+template <int F, int NT>
+__global__ void __launch_bounds__(64) k_poly_chan(PolyArgs pa) {
+    int ug, m;
+    poly_block(F, pa.xcd, ug, m);
+    const int lane = ug * WAVE + threadIdx.x, rep = lane % pa.R;
+    double2 r0[POLY_NI];
+#pragma unroll
+    for (int i = 0; i < POLY_NI; ++i) r0[i] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        // t at the samples n - d_q = mq + F (i - sh) of this residue's r0[i]
+        int mq = m - pa.delay[q], sh = 0;
+        if (mq < 0) {
+            mq += F;
+            sh = 1;
+        }
+        double2 t[POLY_NI];
+#pragma unroll
+        for (int j = 0; j < POLY_NI; ++j) t[j] = make_double2(0.0, 0.0);
+        const double2* __restrict__ vq = pa.v + (size_t)mq * pa.U + lane;
+        const double* __restrict__ aq = pa.A + (size_t)mq * pa.K * POLY_NI;
+        // V_k[mq] in groups of PG symbols, the next group requested before the
+        // current one's products (one wave per SIMD: the loads need ILP)
+        constexpr int PG = 4;
+        double2 vb[PG];
+#pragma unroll
+        for (int g = 0; g < PG; ++g) vb[g] = vq[(size_t)min(g, pa.K - 1) * F * pa.U];
+        for (int k0 = 0; k0 < pa.K; k0 += PG) {
+            double2 vn[PG];
+#pragma unroll
+            for (int g = 0; g < PG; ++g) vn[g] = vq[(size_t)min(k0 + PG + g, pa.K - 1) * F * pa.U];
+#pragma unroll
+            for (int g = 0; g < PG; ++g) {
+                if (k0 + g >= pa.K) break;
+                const double* __restrict__ a = aq + (size_t)(k0 + g) * POLY_NI;
+#pragma unroll
+                for (int j = 0; j < POLY_NI; ++j) {
+                    t[j].x = fma(a[j], vb[g].x, t[j].x);
+                    t[j].y = fma(a[j], vb[g].y, t[j].y);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < PG; ++g) vb[g] = vn[g];
+        }
+        const double2* __restrict__ irq = pa.ir + (size_t)q * pa.N * pa.R + rep;
+        if (sh) {
+#pragma unroll
+            for (int i = 1; i < POLY_NI; ++i) {
+                const int n = m + F * i;
+                if (n < pa.N) c_fma(r0[i], irq[(size_t)n * pa.R], t[i - 1]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < POLY_NI; ++i) {
+                const int n = m + F * i;
+                if (n < pa.N) c_fma(r0[i], irq[(size_t)n * pa.R], t[i]);
+            }
+        }
+    }
+    // fold_k[m] = sum_i B_k[m + F i] r0[i]
+    const double* __restrict__ bm = pa.B + (size_t)m * pa.K * POLY_NI;
+    double2* __restrict__ out = pa.fo + (size_t)m * pa.U + lane;
+    for (int k = 0; k < pa.K; ++k) {
+        const double* __restrict__ bk = bm + (size_t)k * POLY_NI;
+        double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int i = 0; i < POLY_NI; ++i) {
+            acc.x = fma(bk[i], r0[i].x, acc.x);
+            acc.y = fma(bk[i], r0[i].y, acc.y);
+        }
+        out[(size_t)k * F * pa.U] = acc;
+    }
+}
+
+template <int F, class Out>
+__global__ void __launch_bounds__(64) k_poly_ana(PolyArgs pa, Out out) {
+    extern __shared__ double2 poly_lds[];
+    int ug, k;
+    poly_block(pa.K, pa.xcd, ug, k);
+    const int lane = ug * WAVE + threadIdx.x;
+    Out o = out;
+    o.prepare(poly_lds);
+    double2 x[F];
+#pragma unroll
+    for (int m = 0; m < F; ++m) x[m] = pa.fo[(size_t)(k * F + m) * pa.U + lane];
+    const double2* __restrict__ e = pa.E + (size_t)k * F;
+    poly_dft<F, -1>(x, pa.tw, [&](int l, double2 y) { o(k * F + l, lane, c_mulf(e[l], y)); });
+    o.finish(lane);
+}
+
+// eligibility of the polyphase passes (Opts::pic_poly): a factorised scheme,
+// F = 24 or 48 (the instantiated DFT sizes), 1-3 taps with delays below F, the
+// scratch buffers allocated, whole waves of units
+static bool poly_launch_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    if (!op.pic_poly || !sk.poly_ok || !b.pv || !b.pf) return false;
+    if (sk.poly_F != 24 && sk.poly_F != 48) return false;
+    if (sk.poly_F * sk.poly_K != sk.LK || sk.poly_ni > POLY_NI || sk.poly_F * sk.poly_ni < sk.N) return false;
+    if (ch.ntap < 1 || ch.ntap > 3) return false;
+    for (int q = 0; q < ch.ntap; ++q)
+        if (ch.tap_delay[q] < 0 || ch.tap_delay[q] >= sk.poly_F) return false;
+    return b.U % WAVE == 0 && b.R % WAVE == 0;
+}
+
+static PolyArgs poly_args(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
+    PolyArgs pa{};
+    pa.u = b.u;
+    pa.v = b.pv;
+    pa.fo = b.pf;
+    pa.C = sk.poly_C;
+    pa.E = sk.poly_E;
+    pa.A = sk.poly_A;
+    pa.B = sk.poly_B;
+    pa.tw = sk.poly_tw;
+    pa.ir = b.ir;
+    pa.U = b.U;
+    pa.R = b.R;
+    pa.K = sk.poly_K;
+    pa.N = ch.N;
+    pa.xcd = op.xcd;
+    for (int q = 0; q < 4; ++q) pa.delay[q] = q < ch.ntap ? ch.tap_delay[q] : 0;
+    return pa;
+}
+
+// t -> r0 -> fold: the first two of the three polyphase launches
+static void launch_poly_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const PolyArgs& pa) {
+    const int ng = pa.U / WAVE;
+    const dim3 gs(ng * pa.K), gc(ng * sk.poly_F), blk(WAVE);
+#define POLY_CHAN(FV)                                                                              \
+    do {                                                                                           \
+        hipLaunchKernelGGL((k_poly_syn<FV>), gs, blk, 0, s, pa);                                   \
+        if (ch.ntap == 1) hipLaunchKernelGGL((k_poly_chan<FV, 1>), gc, blk, 0, s, pa);             \
+        else if (ch.ntap == 2) hipLaunchKernelGGL((k_poly_chan<FV, 2>), gc, blk, 0, s, pa);        \
+        else hipLaunchKernelGGL((k_poly_chan<FV, 3>), gc, blk, 0, s, pa);                          \
+    } while (0)
+    if (sk.poly_F == 24) POLY_CHAN(24);
+    else POLY_CHAN(48);
+#undef POLY_CHAN
+}
+
+template <class Out>
+static void launch_poly_ana(hipStream_t s, const SchemeK& sk, const PolyArgs& pa, const Out& o, size_t lds) {
+    const dim3 grid((pa.U / WAVE) * pa.K), blk(WAVE);
+    if (sk.poly_F == 24) hipLaunchKernelGGL((k_poly_ana<24, Out>), grid, blk, lds, s, pa, o);
+    else hipLaunchKernelGGL((k_poly_ana<48, Out>), grid, blk, lds, s, pa, o);
+}
+
 unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                            const PerfectDetectArgs* pd) {
-    launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
+    const bool poly = poly_launch_ok(op, sk, ch, b);
+    const PolyArgs pa = poly ? poly_args(op, sk, ch, b) : PolyArgs{};
+    if (poly) launch_poly_front(s, sk, ch, pa);
+    else launch_band(s, sk.G, b.U, nullptr, LoadSoA{b.u, b.U}, StoreSoA{b.t, b.U});
     // SNR-fastest XCD-aware order: the SNR units of a realisation share its taps
     const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
     if (!pd) {
-        launch_pass2_nt(s, sk, ch, b, ord, StorePerfectIC{b.yperf, b.y, b.h, b.u, b.U, b.R});
-        return PATH_PIC_PASSES;
+        const StorePerfectIC o{b.yperf, b.y, b.h, b.u, b.U, b.R};
+        if (poly) launch_poly_ana(s, sk, pa, o, 0);
+        else launch_pass2_nt(s, sk, ch, b, ord, o);
+        return poly ? PATH_PIC_POLY : PATH_PIC_PASSES;
     }
     StorePerfectDetect o{};
     o.y = b.y;
@@ -2803,7 +3048,12 @@ unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, con
     o.sQ = pd->sQ;
     o.tr = b.tr;
     o.stage = pd->stage;
-    launch_pass2_nt(s, sk, ch, b, ord, o, 256 * sizeof(double2) + sizeof(SlicerLds));
+    const size_t lds = 256 * sizeof(double2) + sizeof(SlicerLds);
+    if (poly) {
+        launch_poly_ana(s, sk, pa, o, lds);
+        return PATH_PIC_POLY;
+    }
+    launch_pass2_nt(s, sk, ch, b, ord, o, lds);
     return PATH_PIC_PASSES;
 }
 

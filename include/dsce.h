@@ -203,6 +203,9 @@ typedef struct {
                                                  scheme in one launch pair; k_pic_fft with the perfect-CSI stage 0 */
 #define DSCE_PATH_MIC_LR          (1u << 15)  /* ... with the low-rank tap operator: taps = T_k Z, Z = Bz hP once per
                                                  unit and stage (dsce_structured_check out[5]) */
+#define DSCE_PATH_PIC_POLY        (1u << 16)  /* perfect-CSI IC of a polyphase scheme (FBMC; OFDM with L = 48) as
+                                                 IDFT-L per symbol + window sums per residue + DFT-L per symbol
+                                                 (k_poly_syn / k_poly_chan / k_poly_ana, option pic_poly) */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -319,7 +322,12 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   pic_skip (1: k_pic_fft stops a wave of 16 units x one symbol at the
  *   perfect-CSI IC's fixed point — an iteration that repeats the previous
  *   decisions of every data row is repeated exactly by every later one, whose
- *   counts it copies; 0: every iteration computed).
+ *   counts it copies; 0: every iteration computed), pic_poly (1: the
+ *   perfect-CSI IC passes of a scheme whose G and Q factorise as real windows x
+ *   subcarrier tones, G[n, l + L k] = A_k[n] e^(2 pi i l n / L) C[l][k], checked
+ *   entry by entry to 1e-12 at dsce_add_scheme, with L = 24 or 48, as an IDFT-L
+ *   per symbol, window sums per residue n mod L around the channel, and a DFT-L
+ *   per symbol, DSCE_PATH_PIC_POLY; 0: the two banded passes).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */
