@@ -133,6 +133,7 @@ struct Scheme {
     // slices of max |Q' H_hat G - W_thresholded| / (MIC_RTOL max |W|), the largest
     // absolute deviation and the largest |W|; -1 = not evaluated
     double mic_check = -1.0, mic_dev = -1.0, mic_wmax = -1.0;
+    double mic_rtol = -1.0;         // the largest per-slice bar max(MIC_RTOL, LR_EPS kappa(R)) used
     // build_poly: largest |G - A w C| / max|G| or the same of Q (-1: not evaluated)
     double poly_resid = -1.0;
 };
@@ -788,7 +789,9 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 // thresholded W of every (variant, SNR) slice — the diagonal (Wd, the one-tap
 // channel of script:428/:515) and the off-diagonal entries the IC subtraction
 // uses (the packed band, script:482-484), zero across FFT blocks — to rounding:
-// |difference| <= MIC_RTOL max|W| per entry.  That is the check that the
+// |difference| <= rtol max|W| per entry, rtol = max(MIC_RTOL, LR_EPS kappa(R)) of
+// the slice (capped at MIC_RTOL_MAX; kappa(R) = ||R||_1 ||pinv(R)||_1: W and Bv
+// both carry rounding of order eps kappa(R) through pinv(R)).  That is the check that the
 // sparsification of R_Dij,hP and W (script:264-265, :287-289, :306-308) drops
 // nothing but rounding-level entries: an entry the threshold zeroed has
 // |W_s| < thr, so a guard at thr (r02-r03: thr + 1e-9 max|W|) would accept any
@@ -816,6 +819,25 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 // cond 1.2e5, tests/test_lowrank.py), while a geometry without the structure
 // misses by orders of magnitude.
 static constexpr double LR_EPS = 4e-16;
+// max(column, row) 1-norm of an NP x NP complex matrix (its condition estimate
+// kappa(R) = ||R||_1 ||pinv(R)||_1 sets the rounding bars of build_mic / build_mic_lr)
+double norm1(const double2* m, int NP) {
+    double best = 0.0;
+    for (int j = 0; j < NP; ++j) {
+        double cs = 0.0, rs = 0.0;
+        for (int i = 0; i < NP; ++i) {
+            cs += std::hypot(m[(size_t)j * NP + i].x, m[(size_t)j * NP + i].y);
+            rs += std::hypot(m[(size_t)i * NP + j].x, m[(size_t)i * NP + j].y);
+        }
+        best = std::max(best, std::max(cs, rs));
+    }
+    return best;
+}
+// R of slice sl = var nsnr + snr (R_est for var 0, R_noI for var 1)
+const double2* slice_R(const Scheme& s, int nsnr, int sl) {
+    const int NP = s.d.n_pilots;
+    return sl < nsnr ? s.R_est.data() + (size_t)sl * NP * NP : s.R_noI.data() + (size_t)(sl - nsnr) * NP * NP;
+}
 void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<double2>& bv, const std::vector<int>& pb,
                   const double2* rinv_dev) {
     const int NP = s.d.n_pilots, N = s.N, nt = c->ch.ntap, nsl = 2 * c->nsnr, nblk = s.k.QH.nblk;
@@ -855,24 +877,10 @@ void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<
     // condition estimate of each slice's R: ||R||_1 ||pinv(R)||_1 (slice sl = var nsnr + snr)
     std::vector<double2> ri((size_t)nsl * NP * NP);
     DSCE_HIP_CHECK(hipMemcpy(ri.data(), rinv_dev, ri.size() * sizeof(double2), hipMemcpyDeviceToHost));
-    auto norm1 = [&](const double2* m) {
-        double best = 0.0;
-        for (int j = 0; j < NP; ++j) {
-            double cs = 0.0, rs = 0.0;
-            for (int i = 0; i < NP; ++i) {
-                cs += std::hypot(m[(size_t)j * NP + i].x, m[(size_t)j * NP + i].y);
-                rs += std::hypot(m[(size_t)i * NP + j].x, m[(size_t)i * NP + j].y);
-            }
-            best = std::max(best, std::max(cs, rs));
-        }
-        return best;
-    };
     std::vector<double2> bz((size_t)nsl * nt * MIC_NB * NP);
     double worst = 0.0, rel = 0.0;
     for (int sl = 0; sl < nsl; ++sl) {
-        const int nsnr = c->nsnr;
-        const double2* R = sl < nsnr ? s.R_est.data() + (size_t)sl * NP * NP : s.R_noI.data() + (size_t)(sl - nsnr) * NP * NP;
-        const double kap = norm1(R) * norm1(ri.data() + (size_t)sl * NP * NP);
+        const double kap = norm1(slice_R(s, c->nsnr, sl), NP) * norm1(ri.data() + (size_t)sl * NP * NP, NP);
         const double tol = std::max(1e-13, LR_EPS * kap);
         double mx = 0.0, dev = 0.0;
         for (int q = 0; q < nt; ++q)
@@ -932,7 +940,7 @@ void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<
     s.Ts = dupload(c, ts);
 }
 
-static constexpr double MIC_RTOL = 1e-11;
+static constexpr double MIC_RTOL = 1e-11, MIC_RTOL_MAX = 1e-9;
 void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, const double2* rinv) {
     const int NP = s.d.n_pilots, LK = s.LK, N = s.N, nsl = 2 * c->nsnr, nt = c->ch.ntap;
     const int nblk = s.k.QH.nblk;
@@ -959,9 +967,18 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
     // D[sl][b][p][lr][lc] of one slice at a time
     std::vector<double2> F((size_t)nt * 24), Ds((size_t)nblk * NP * 576);
     std::vector<char> seen((size_t)nblk * 576);
-    double worst = 0.0, dev = 0.0, wmax = 0.0;
+    std::vector<double2> ri((size_t)nsl * NP * NP);
+    DSCE_HIP_CHECK(hipMemcpy(ri.data(), rinv, ri.size() * sizeof(double2), hipMemcpyDeviceToHost));
+    double worst = 0.0, dev = 0.0, wmax = 0.0, rtol_max = MIC_RTOL;
     for (int sl = 0; sl < nsl; ++sl) {
         double mx = 0.0, md = 0.0;
+        // the slice's rounding bar: W = R_Dij pinv(R) and Bv = m pinv(R) carry
+        // rounding of order eps kappa(R) relative (GPU, C2: 5.9e-12 absolute at
+        // max|W| 0.59 and kappa ~1e5), so max(MIC_RTOL, LR_EPS kappa(R)) max|W|
+        // (capped at MIC_RTOL_MAX, a tenth of the script's threshold relative to |W| ~ 1)
+        const double rtol = std::min(MIC_RTOL_MAX, std::max(MIC_RTOL, LR_EPS * norm1(slice_R(s, c->nsnr, sl), NP) *
+                                                                           norm1(ri.data() + (size_t)sl * NP * NP, NP)));
+        rtol_max = std::max(rtol_max, rtol);
         const double2* wds = wd.data() + (size_t)sl * LK * NP;
         const double2* wbs = wb.data() + (size_t)sl * s.w_elems;
         for (int i = 0; i < LK * NP; ++i) mx = std::max(mx, std::hypot(wds[i].x, wds[i].y));
@@ -1030,13 +1047,14 @@ void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, con
                         md = std::max(md, std::hypot(st.x, st.y));
                     }
                 }
-        worst = std::max(worst, md / (MIC_RTOL * mx));
+        worst = std::max(worst, md / (rtol * mx));
         dev = std::max(dev, md);
         wmax = std::max(wmax, mx);
     }
     s.mic_check = worst;
     s.mic_dev = dev;
     s.mic_wmax = wmax;
+    s.mic_rtol = rtol_max;
     if (worst > 1.0) {
         free_alloc(c, s.Bv);
         free_alloc(c, s.Bs);
@@ -2298,7 +2316,7 @@ int dsce_structured_check(dsce_ctx* ctx, int32_t id, double* out) {
     out[0] = s.mic_check;
     out[1] = s.mic_dev;
     out[2] = s.mic_wmax;
-    out[3] = MIC_RTOL;
+    out[3] = s.mic_rtol;
     out[4] = s.lr_resid;
     out[5] = s.Bz ? 1.0 : 0.0;
     out[6] = s.lr_ratio;

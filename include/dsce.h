@@ -357,9 +357,10 @@ int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per
 int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, double* bytes_per_rep);
 /* The guard of the structured MMSE IC (D_hat = Q' H_hat G, DSCE_PATH_MIC_FFT),
  * evaluated at dsce_build_mmse: out[0] = worst over the (variant, SNR) slices of
- * max |Q' H_hat G - W_thr| / (out[3] max |W|) over every entry the IC uses
- * (the path is kept iff <= 1), out[1] = the largest absolute deviation, out[2]
- * = the largest |W|, out[3] = the relative tolerance (rounding level, 1e-11).
+ * max |Q' H_hat G - W_thr| / (rtol max |W|) over every entry the IC uses, with
+ * the slice's rounding bar rtol = min(1e-9, max(1e-11, 4e-16 ||R||_1
+ * ||pinv(R)||_1)) (the path is kept iff <= 1), out[1] = the largest absolute
+ * deviation, out[2] = the largest |W|, out[3] = the largest rtol of the slices.
  * out[0..2] = -1 when the scheme is not eligible (the W contraction runs).
  * The low-rank form of its tap operator (Bv = T Bz, T_k the J0 kernel summed
  * over pilot symbol k's window; option mic_lr): out[4] = max |Bv - T Bz| /

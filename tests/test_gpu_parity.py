@@ -342,7 +342,10 @@ def test_structured_ofdm_guard_rejects_what_the_threshold_changes():
     eng.run(SEED, 0, 64)
     assert "mic_fft" in eng.path_info(0)
     chk = eng.structured_check(0)
-    assert 0.0 <= chk["ratio"] <= 1.0 and chk["dev"] <= 1e-11 * chk["wmax"], chk
+    # the bar is rounding level: max(1e-11, 4e-16 kappa(R)) max|W| per slice (GPU, C2:
+    # dev 5.9e-12 at max|W| 0.59, kappa ~1e5: bars of 1e-11 .. 5e-11; capped at 1e-9)
+    assert 0.0 <= chk["ratio"] <= 1.0 and chk["dev"] <= chk["rtol"] * chk["wmax"], chk
+    assert 1e-11 <= chk["rtol"] <= 1e-9, chk
     # the low-rank form of the tap operator reproduces Bv to rounding and is used
     assert chk["lr"] and 0.0 <= chk["lr_ratio"] <= 1.0 and 0.0 <= chk["lr_resid"] < 1e-10, chk
     assert "mic_lr" in eng.path_info(0)
@@ -356,7 +359,8 @@ def test_structured_ofdm_guard_is_at_rounding_level():
     thresholds of script:287-289 / :306-308 zero C2 entries of magnitude
     1e-7..1e-6 (oracle: max |W_thr - W_s| = 0.94 thr, tools/threshold_study.py),
     which the old guard accepted (deviation < thr) and the rounding-level guard
-    (1e-11 max|W|, dsce_structured_check) must reject: the W contraction runs and
+    (min(1e-9, max(1e-11, 4e-16 kappa(R))) max|W| per slice, dsce_structured_check) must
+    reject: the W contraction runs and
     the counts equal the oracle's literal thresholded W."""
     from types import SimpleNamespace
     S = SimpleNamespace(**vars(harness.setup("default", schemes=("ofdm",))))
@@ -366,7 +370,7 @@ def test_structured_ofdm_guard_is_at_rounding_level():
     # the old guard would have accepted: every deviation is below the threshold
     assert 0.0 < chk["dev"] < S.zero_threshold, chk
     # ... but it is far above rounding
-    assert chk["ratio"] > 1e3 and chk["rtol"] == 1e-11, chk
+    assert chk["ratio"] > 1e2 and 1e-11 <= chk["rtol"] <= 1e-9, chk
     cg = eng.run(SEED, 0, 64)
     path = eng.path_info(0)
     assert "mic_fft" not in path and "wpair3_fused" in path, path
