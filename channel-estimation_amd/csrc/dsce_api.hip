@@ -343,13 +343,14 @@ void build_poly(dsce_ctx* c, Scheme& s) {
     s.poly_resid = std::max(rg, rq);
     if (!(s.poly_resid <= 1e-12)) return;
     // per residue m: the windows at n = m + L j, zero past N
-    std::vector<double> pa((size_t)L * K * POLY_NI, 0.0), pb((size_t)L * K * POLY_NI, 0.0);
+    // (the A rows carry a leading zero: k_poly_chan's halves read j = i0 - 1 ..)
+    std::vector<double> pa((size_t)L * K * POLY_NA, 0.0), pb((size_t)L * K * POLY_NI, 0.0);
     for (int m = 0; m < L; ++m)
         for (int kk = 0; kk < K; ++kk)
             for (int j = 0; j < POLY_NI; ++j) {
                 const int n = m + L * j;
                 if (n >= N) continue;
-                pa[((size_t)m * K + kk) * POLY_NI + j] = Ag[(size_t)kk * N + n];
+                pa[((size_t)m * K + kk) * POLY_NA + j + 1] = Ag[(size_t)kk * N + n];
                 pb[((size_t)m * K + kk) * POLY_NI + j] = Aq[(size_t)kk * N + n];
             }
     // Q^H[l + L k, n] = conj(Q) = B_k[n] w^(-l n) conj(Cq[l][k]): E = conj(Cq)
@@ -1240,8 +1241,8 @@ void ensure_buffers(dsce_ctx* c, int R) {
         NP = std::max<size_t>(NP, s->d.n_pilots);
         ND = std::max<size_t>(ND, s->d.n_data);
     }
-    bool poly = false;      // polyphase perfect-CSI IC scratch, only for schemes that have the form
-    for (auto& sp : c->schemes) poly = poly || sp->k.poly_ok;
+    bool poly = false;      // polyphase perfect-CSI IC scratch: option on and a scheme with the form
+    for (auto& sp : c->schemes) poly = poly || (sp->k.poly_ok && c->op.pic_poly);
     const size_t key[8] = {(size_t)R, N, LK, NP, ND, (size_t)snr_chunk(c), (size_t)c->niter, (size_t)poly};
     if (memcmp(key, c->buf_key, sizeof(key)) == 0) return;
     for (void* p : c->buf_allocs) (void)hipFree(p);
@@ -1286,6 +1287,7 @@ void ensure_buffers(dsce_ctx* c, int R) {
     // polyphase perfect-CSI IC scratch (V and the window sums)
     b.pv = poly ? dalloc<double2>(c, LK * U, L) : nullptr;
     b.pf = poly ? dalloc<double2>(c, LK * U, L) : nullptr;
+    b.pf2 = poly ? dalloc<double2>(c, LK * U, L) : nullptr;
     DSCE_HIP_CHECK(hipMemsetAsync(b.sidr, 0, (LK + 32) * R * sizeof(uint16_t), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.ir + (size_t)c->ch.ntap * N * R, 0, 4 * (size_t)R * sizeof(double2), c->stream));
     DSCE_HIP_CHECK(hipMemsetAsync(b.h + LK * R, 0, 32 * (size_t)R * sizeof(double2), c->stream));

@@ -171,11 +171,13 @@ struct SchemeK {
     int poly_F, poly_K;           // DFT size F = L, symbols K
     const double2* poly_C;        // [K][F]
     const double2* poly_E;        // [K][F]
-    const double* poly_A;         // [F][K][POLY_NI]: A_k[m + F j] (0 outside [0, N))
+    const double* poly_A;         // [F][K][POLY_NA]: A_k[m + F j] at j + 1 (0 at index 0 and outside [0, N))
     const double* poly_B;         // [F][K][POLY_NI]
     const double2* poly_tw;       // w^e, e = 0..F-1
 };
 constexpr int POLY_NI = 24;       // samples per residue class the polyphase kernels hold
+constexpr int POLY_IH = POLY_NI / 2;   // ... per half (k_poly_chan block)
+constexpr int POLY_NA = POLY_NI + 1;   // A table row: j = -1 .. POLY_NI - 1
 
 struct ChannelK {
     int N, ntap;                  // ntap = number of non-zero taps

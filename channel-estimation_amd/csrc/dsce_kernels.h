@@ -27,16 +27,19 @@ struct Opts {
     int snr_base = 0;         // noise sub-stream of SNR index k is snr_base + k (SNR-sharded sweeps)
     int tx_rows = 1;          // row-local precoders: TX symbols drawn row-parallel (k_tx_rows)
     int pic_net = 1;          // k_pic_fft's 4-point network: 1 = v_mfma_f64_4x4x4 (quarters on 16-lane rows), 0 = DPP
-    int mic_net = 1;          // the same network for k_mic_data (bit 0) / k_mic_pilot (bit 1), whose tap GEMM then
-                              // needs no exchange: data 3.99 -> 3.65 ms, pilot 1.91 -> 2.00 ms (237 VGPRs): 1
+    int mic_net = 3;          // the same network for k_mic_data (bit 0) / k_mic_pilot (bit 1), whose tap GEMM then
+                              // needs no exchange: data 3.99 -> 3.65 ms, pilot 1.91 -> 2.00 ms (237 VGPRs, r03: 1);
+                              // with the low-rank taps the pilot kernel gains too: 1.625 -> 1.576 ms (r04: 3)
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int mic_lr = 1;           // MMSE IC taps in the low-rank form T_k Z (k_mic_pilot / k_mic_data) where
                               // build_mic_lr verified it; 0 = the tap GEMM Bv hP on the matrix cores
-    int pic_skip = 1;         // k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
-                              // iterations are copies); 0 = compute every iteration
-    int pic_poly = 0;         // perfect-CSI IC passes of polyphase schemes (SchemeK::poly_ok: FBMC, OFDM with
+    int pic_skip = 0;         // 1: k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
+                              // iterations are copies); exact, but rarely a whole wave converges and the
+                              // test costs more than it saves (r04 box: 2.626 -> 2.665 ms per step): 0
+    int pic_poly = 1;         // perfect-CSI IC passes of polyphase schemes (SchemeK::poly_ok: FBMC, OFDM with
                               // L != 24) as IDFT-L per symbol + window sums per residue + DFT-L per symbol
                               // (k_poly_syn / k_poly_chan / k_poly_ana) instead of the two banded passes
+                              // (r04 box, C3: 14.3 -> 8.7 ms per iteration); 0 = the banded passes
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower
@@ -113,7 +116,8 @@ struct McBuffers {
     int hpa_stages;   // stages hpa holds
     double2* za;      // [stage][ntap * MIC_NB][U] Z = Bz hP of every stage (low-rank MMSE IC), or null
     double2* pv;      // [LK][U] polyphase IC: IDFT of each symbol's C u (k_poly_syn), or null
-    double2* pf;      // [LK][U] polyphase IC: window sums of r0 per (symbol, residue) (k_poly_chan), or null
+    double2* pf;      // [LK][U] polyphase IC: window sums of r0 per (symbol, residue), first half (k_poly_chan)
+    double2* pf2;     // [LK][U] ... second half; pv / pf / pf2 null unless Opts::pic_poly and a scheme has the form
     double* mse_err;  // null, or [scheme][snr][stage] sums of |h_hat - h|^2 (dsce_enable_mse)
     double* mse_pow;  // [scheme][snr] sums of |h|^2
     const TraceK* tr; // device trace of one unit (null: not tracing this scheme / chunk)

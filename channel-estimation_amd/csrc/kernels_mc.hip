@@ -2784,10 +2784,11 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
 struct PolyArgs {
     const double2* __restrict__ u;    // [LK][U]
     double2* __restrict__ v;          // [LK][U]  V_k[m] at row k F + m
-    double2* __restrict__ fo;         // [LK][U]  fold_k[m] at row k F + m
+    double2* __restrict__ fo;         // [LK][U]  fold_k[m] at row k F + m, samples of the first half
+    double2* __restrict__ fo2;        // [LK][U]  ... of the second half
     const double2* __restrict__ C;    // [K][F]
     const double2* __restrict__ E;    // [K][F]
-    const double* __restrict__ A;     // [F][K][POLY_NI]
+    const double* __restrict__ A;     // [F][K][POLY_NA]: A(j) at j + 1, index 0 = 0
     const double* __restrict__ B;     // [F][K][POLY_NI]
     const double2* __restrict__ tw;   // w^e, e = 0..F-1
     const double2* __restrict__ ir;   // [ntap][N][R]
@@ -2858,29 +2859,40 @@ __global__ void __launch_bounds__(64) k_poly_syn(PolyArgs pa) {
     poly_dft<F, 1>(x, pa.tw, [&](int m, double2 y) { out[(size_t)m * pa.U] = y; });
 }
 
+// Block = (unit group, residue m, half h): the half's POLY_IH samples
+// n = m + F i, i in [h IH, (h + 1) IH), and its partial window sums into fo
+// (h = 0) / fo2 (h = 1), which k_poly_ana adds.  Halves keep a wave at ~150
+// VGPRs (3 waves per SIMD) where the whole residue (r0 and t of 24 samples)
+// took 288 and one wave per SIMD left the V loads' latency exposed (r04 box,
+// C3: 6.3 -> 3.6 ms per iteration; the two halves as the waves of one block,
+// their partial sums met in LDS instead of fo2: 5.3 ms, LDS-limited occupancy
+// and the barrier cost more than the extra 16 B per entry).
 template <int F, int NT>
 __global__ void __launch_bounds__(64) k_poly_chan(PolyArgs pa) {
-    int ug, m;
-    poly_block(F, pa.xcd, ug, m);
+    int ug, mh;
+    poly_block(2 * F, pa.xcd, ug, mh);
+    const int m = mh >> 1, h = mh & 1, i0 = h * POLY_IH;
     const int lane = ug * WAVE + threadIdx.x, rep = lane % pa.R;
-    double2 r0[POLY_NI];
+    double2 r0[POLY_IH];
 #pragma unroll
-    for (int i = 0; i < POLY_NI; ++i) r0[i] = make_double2(0.0, 0.0);
+    for (int i = 0; i < POLY_IH; ++i) r0[i] = make_double2(0.0, 0.0);
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
-        // t at the samples n - d_q = mq + F (i - sh) of this residue's r0[i]
+        // t at the samples mq + F j, j = i0 - 1 + jj (jj = 0..IH): the tap's
+        // n - d_q = mq + F (i - sh) for the half's r0[i]
         int mq = m - pa.delay[q], sh = 0;
         if (mq < 0) {
             mq += F;
             sh = 1;
         }
-        double2 t[POLY_NI];
+        double2 t[POLY_IH + 1];
 #pragma unroll
-        for (int j = 0; j < POLY_NI; ++j) t[j] = make_double2(0.0, 0.0);
+        for (int j = 0; j <= POLY_IH; ++j) t[j] = make_double2(0.0, 0.0);
         const double2* __restrict__ vq = pa.v + (size_t)mq * pa.U + lane;
-        const double* __restrict__ aq = pa.A + (size_t)mq * pa.K * POLY_NI;
+        // A(j) at index j + 1 (index 0: j = -1, zero): the half's t[jj] reads index i0 + jj
+        const double* __restrict__ aq = pa.A + (size_t)mq * pa.K * POLY_NA + i0;
         // V_k[mq] in groups of PG symbols, the next group requested before the
-        // current one's products (one wave per SIMD: the loads need ILP)
+        // current one's products
         constexpr int PG = 4;
         double2 vb[PG];
 #pragma unroll
@@ -2892,9 +2904,9 @@ __global__ void __launch_bounds__(64) k_poly_chan(PolyArgs pa) {
 #pragma unroll
             for (int g = 0; g < PG; ++g) {
                 if (k0 + g >= pa.K) break;
-                const double* __restrict__ a = aq + (size_t)(k0 + g) * POLY_NI;
+                const double* __restrict__ a = aq + (size_t)(k0 + g) * POLY_NA;
 #pragma unroll
-                for (int j = 0; j < POLY_NI; ++j) {
+                for (int j = 0; j <= POLY_IH; ++j) {
                     t[j].x = fma(a[j], vb[g].x, t[j].x);
                     t[j].y = fma(a[j], vb[g].y, t[j].y);
                 }
@@ -2902,29 +2914,33 @@ __global__ void __launch_bounds__(64) k_poly_chan(PolyArgs pa) {
 #pragma unroll
             for (int g = 0; g < PG; ++g) vb[g] = vn[g];
         }
+        // the taps' loads after the window sums (hoisted above them they would
+        // hold 4 IH more registers through the loop)
+        __builtin_amdgcn_sched_barrier(0);
         const double2* __restrict__ irq = pa.ir + (size_t)q * pa.N * pa.R + rep;
         if (sh) {
 #pragma unroll
-            for (int i = 1; i < POLY_NI; ++i) {
-                const int n = m + F * i;
-                if (n < pa.N) c_fma(r0[i], irq[(size_t)n * pa.R], t[i - 1]);
+            for (int i = 0; i < POLY_IH; ++i) {
+                const int n = m + F * (i0 + i);
+                if (n < pa.N && i0 + i >= 1) c_fma(r0[i], irq[(size_t)n * pa.R], t[i]);
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < POLY_NI; ++i) {
-                const int n = m + F * i;
-                if (n < pa.N) c_fma(r0[i], irq[(size_t)n * pa.R], t[i]);
+            for (int i = 0; i < POLY_IH; ++i) {
+                const int n = m + F * (i0 + i);
+                if (n < pa.N) c_fma(r0[i], irq[(size_t)n * pa.R], t[i + 1]);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
-    // fold_k[m] = sum_i B_k[m + F i] r0[i]
-    const double* __restrict__ bm = pa.B + (size_t)m * pa.K * POLY_NI;
-    double2* __restrict__ out = pa.fo + (size_t)m * pa.U + lane;
+    // partial fold_k[m] = sum_{i in half} B_k[m + F i] r0[i]
+    const double* __restrict__ bm = pa.B + (size_t)m * pa.K * POLY_NI + i0;
+    double2* __restrict__ out = (h ? pa.fo2 : pa.fo) + (size_t)m * pa.U + lane;
     for (int k = 0; k < pa.K; ++k) {
         const double* __restrict__ bk = bm + (size_t)k * POLY_NI;
         double2 acc = make_double2(0.0, 0.0);
 #pragma unroll
-        for (int i = 0; i < POLY_NI; ++i) {
+        for (int i = 0; i < POLY_IH; ++i) {
             acc.x = fma(bk[i], r0[i].x, acc.x);
             acc.y = fma(bk[i], r0[i].y, acc.y);
         }
@@ -2942,7 +2958,10 @@ __global__ void __launch_bounds__(64) k_poly_ana(PolyArgs pa, Out out) {
     o.prepare(poly_lds);
     double2 x[F];
 #pragma unroll
-    for (int m = 0; m < F; ++m) x[m] = pa.fo[(size_t)(k * F + m) * pa.U + lane];
+    for (int m = 0; m < F; ++m) {
+        const size_t i = (size_t)(k * F + m) * pa.U + lane;
+        x[m] = c_add(pa.fo[i], pa.fo2[i]);                    // the two halves' window sums
+    }
     const double2* __restrict__ e = pa.E + (size_t)k * F;
     poly_dft<F, -1>(x, pa.tw, [&](int l, double2 y) { o(k * F + l, lane, c_mulf(e[l], y)); });
     o.finish(lane);
@@ -2952,7 +2971,7 @@ __global__ void __launch_bounds__(64) k_poly_ana(PolyArgs pa, Out out) {
 // F = 24 or 48 (the instantiated DFT sizes), 1-3 taps with delays below F, the
 // scratch buffers allocated, whole waves of units
 static bool poly_launch_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b) {
-    if (!op.pic_poly || !sk.poly_ok || !b.pv || !b.pf) return false;
+    if (!op.pic_poly || !sk.poly_ok || !b.pv || !b.pf || !b.pf2) return false;
     if (sk.poly_F != 24 && sk.poly_F != 48) return false;
     if (sk.poly_F * sk.poly_K != sk.LK || sk.poly_ni > POLY_NI || sk.poly_F * sk.poly_ni < sk.N) return false;
     if (ch.ntap < 1 || ch.ntap > 3) return false;
@@ -2966,6 +2985,7 @@ static PolyArgs poly_args(const Opts& op, const SchemeK& sk, const ChannelK& ch,
     pa.u = b.u;
     pa.v = b.pv;
     pa.fo = b.pf;
+    pa.fo2 = b.pf2;
     pa.C = sk.poly_C;
     pa.E = sk.poly_E;
     pa.A = sk.poly_A;
@@ -2984,13 +3004,13 @@ static PolyArgs poly_args(const Opts& op, const SchemeK& sk, const ChannelK& ch,
 // t -> r0 -> fold: the first two of the three polyphase launches
 static void launch_poly_front(hipStream_t s, const SchemeK& sk, const ChannelK& ch, const PolyArgs& pa) {
     const int ng = pa.U / WAVE;
-    const dim3 gs(ng * pa.K), gc(ng * sk.poly_F), blk(WAVE);
+    const dim3 gs(ng * pa.K), gc(ng * 2 * sk.poly_F), blk(WAVE);
 #define POLY_CHAN(FV)                                                                              \
     do {                                                                                           \
         hipLaunchKernelGGL((k_poly_syn<FV>), gs, blk, 0, s, pa);                                   \
-        if (ch.ntap == 1) hipLaunchKernelGGL((k_poly_chan<FV, 1>), gc, blk, 0, s, pa);             \
-        else if (ch.ntap == 2) hipLaunchKernelGGL((k_poly_chan<FV, 2>), gc, blk, 0, s, pa);        \
-        else hipLaunchKernelGGL((k_poly_chan<FV, 3>), gc, blk, 0, s, pa);                          \
+        if (ch.ntap == 1) hipLaunchKernelGGL((k_poly_chan<FV, 1>), gc, blk, 0, s, pa);            \
+        else if (ch.ntap == 2) hipLaunchKernelGGL((k_poly_chan<FV, 2>), gc, blk, 0, s, pa);       \
+        else hipLaunchKernelGGL((k_poly_chan<FV, 3>), gc, blk, 0, s, pa);                         \
     } while (0)
     if (sk.poly_F == 24) POLY_CHAN(24);
     else POLY_CHAN(48);

@@ -322,12 +322,13 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   pic_skip (1: k_pic_fft stops a wave of 16 units x one symbol at the
  *   perfect-CSI IC's fixed point — an iteration that repeats the previous
  *   decisions of every data row is repeated exactly by every later one, whose
- *   counts it copies; 0: every iteration computed), pic_poly (1: the
+ *   counts it copies; 0, the default: every iteration computed — whole waves
+ *   rarely converge and the test costs more than it saves), pic_poly (1: the
  *   perfect-CSI IC passes of a scheme whose G and Q factorise as real windows x
  *   subcarrier tones, G[n, l + L k] = A_k[n] e^(2 pi i l n / L) C[l][k], checked
  *   entry by entry to 1e-12 at dsce_add_scheme, with L = 24 or 48, as an IDFT-L
  *   per symbol, window sums per residue n mod L around the channel, and a DFT-L
- *   per symbol, DSCE_PATH_PIC_POLY; 0: the two banded passes).
+ *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */

@@ -82,7 +82,8 @@ def test_c5_fbmc_matches_oracle(name):
     """C5 FBMC auxiliary (Fig. 3) and data spreading (Fig. 4, IIC.m:106-210,
     despread detection script:436, :520) at 48 x 30: W / W0 of the 32-pilot
     estimator, a per-element trace of every stage of one unit (y_perf of every
-    row: the unfused perfect-CSI passes), and the counts of 64 realisations."""
+    row: the unfused perfect-CSI passes, polyphase by default), and the counts
+    of 64 realisations."""
     S = harness.setup("c5", schemes=(name,), snr_db=SNR[1:])
     sc = S.schemes[name]
     assert sc["G"].shape[1] == 1440 and len(sc["pilot_pos"]) == 32 and bool(sc["despread"]) == (name == "fbmc_cod")
@@ -92,7 +93,7 @@ def test_c5_fbmc_matches_oracle(name):
     _check_trace(S, name, eng, 2, (0,), yperf=True, w_sparse=True)
     _check_counts(S, name, eng, 0, 64, w_sparse=True)
     path = eng.path_info(0)
-    assert ("stage_split" in path) == (name == "fbmc_cod") and "pic_passes" in path, path
+    assert ("stage_split" in path) == (name == "fbmc_cod") and "pic_poly" in path, path
     eng.close()
 
 

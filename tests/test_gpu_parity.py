@@ -430,9 +430,10 @@ def test_stage_variants_agree(name):
     4-point network by DPP instead of on the matrix cores (and k_mic_pilot /
     k_mic_data's, with the tap GEMM's exchange by ds_bpermute), the tap GEMM
     Bv hP instead of the low-rank operator T_k Z (mic_lr 0), every perfect-CSI
-    iteration computed instead of stopping at the fixed point (pic_skip 0), the
-    perfect-CSI passes in polyphase form (pic_poly 1; with pic_chain 0 for OFDM,
-    whose chain is otherwise k_pic_fft)."""
+    iteration stopping at the fixed point instead of computed (pic_skip 1), the
+    perfect-CSI passes banded instead of polyphase (pic_poly 0; FBMC) and
+    polyphase for OFDM too (pic_poly 1 with pic_chain 0: OFDM's chain is
+    otherwise k_pic_fft)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -449,8 +450,8 @@ def test_stage_variants_agree(name):
                 {"jakes_win": 0}, {"txrx_fft": 0}, {"mmse_ic": 0, "fuse_stage": 0, "pic_chain": 0},
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
-                {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 0},
-                {"pic_poly": 1}, {"pic_poly": 1, "pic_chain": 0})
+                {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 1},
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
