@@ -11,6 +11,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <cstdio>
 #include <vector>
 
 #include "dsce.h"
@@ -268,6 +269,10 @@ Band upload_band(dsce_ctx* c, const HostBand& h, bool with_vals) {
 void check_ctx(dsce_ctx* c) {
     if (!c) throw ApiError(DSCE_EINVAL, "null context");
     DSCE_HIP_CHECK(hipSetDevice(c->device));
+    // errors are per call: a failure some earlier call already returned (or a
+    // teardown ignored) must not be reported again by this call's hipGetLastError
+    const hipError_t stale = hipGetLastError();
+    if (stale != hipSuccess) fprintf(stderr, "dsce: clearing a stale HIP error at entry: %s\n", hipGetErrorString(stale));
 }
 
 Scheme& get_scheme(dsce_ctx* c, int id) {
@@ -1701,17 +1706,30 @@ int dsce_create(int hip_device, dsce_ctx** out) {
 
 void dsce_destroy(dsce_ctx* ctx) {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (void* p : ctx->buf_allocs) (void)hipFree(p);
-    for (void* p : ctx->allocs) (void)hipFree(p);
+    // Teardown cannot fail the caller, but a failing call is reported (stderr)
+    // and its error cleared, so it does not surface in the next context's
+    // hipGetLastError (r04: a stale 'invalid argument' met a later build_mmse).
+    const char* first = nullptr;
+    hipError_t ferr = hipSuccess;
+    auto note = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && !first) {
+            first = what;
+            ferr = e;
+        }
+    };
+    note(hipSetDevice(ctx->device), "hipSetDevice");
+    if (ctx->stream) note(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    for (void* p : ctx->buf_allocs) note(hipFree(p), "hipFree (batch buffers)");
+    for (void* p : ctx->allocs) note(hipFree(p), "hipFree (operators)");
     for (auto& e : ctx->pending) {
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
+        note(hipEventDestroy(e.a), "hipEventDestroy");
+        note(hipEventDestroy(e.b), "hipEventDestroy");
     }
-    for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    for (auto e : ctx->event_pool) note(hipEventDestroy(e), "hipEventDestroy (pool)");
+    if (ctx->stream) note(hipStreamDestroy(ctx->stream), "hipStreamDestroy");
     delete ctx;
+    if (first) fprintf(stderr, "dsce_destroy: %s failed: %s\n", first, hipGetErrorString(ferr));
+    (void)hipGetLastError();
 }
 
 const char* dsce_last_error(const dsce_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
