@@ -1976,8 +1976,10 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     std::vector<double2> h((size_t)ctx->ch.ntap * N * R);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ir, h.size() * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    DSCE_HIP_CHECK(hipFree(ir));
-    ctx->allocs.pop_back();
+    // by pointer: update_jakes_chunks / _groups above may have allocated after ir
+    // (r04: popping the list's last entry freed ir twice at dsce_destroy and
+    // dropped the Jakes groups from the list)
+    free_alloc(ctx, ir);
     const int ntot = (int)ctx->pdp_norm.size();
     for (size_t i = 0; i < (size_t)N * ntot * 2; ++i) ir_out[i] = 0.0;
     for (int q = 0; q < ctx->ch.ntap; ++q)
