@@ -137,6 +137,7 @@ struct Scheme {
     double mic_rtol = -1.0;         // the largest per-slice bar max(MIC_RTOL, LR_EPS kappa(R)) used
     // build_poly: largest |G - A w C| / max|G| or the same of Q (-1: not evaluated)
     double poly_resid = -1.0;
+    double poly_nnz_a = 0.0, poly_nnz_b = 0.0;   // non-zero window samples of G's / Q's symbols
 };
 
 }  // namespace dsce
@@ -363,6 +364,11 @@ void build_poly(dsce_ctx* c, Scheme& s) {
     for (size_t i = 0; i < Cq.size(); ++i) E[i] = make_double2(Cq[i].x, -Cq[i].y);
     std::vector<double2> tw(L);
     for (int e = 0; e < L; ++e) tw[e] = make_double2(std::cos(2.0 * M_PI * e / L), std::sin(2.0 * M_PI * e / L));
+    s.poly_nnz_a = s.poly_nnz_b = 0.0;
+    for (size_t i = 0; i < Ag.size(); ++i) {
+        s.poly_nnz_a += Ag[i] != 0.0;
+        s.poly_nnz_b += Aq[i] != 0.0;
+    }
     k.poly_F = L;
     k.poly_K = K;
     k.poly_ni = ni;
@@ -1629,6 +1635,19 @@ KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
         // per unit and iteration: y, hP and v read, y_est written (W itself is
         // shared by the batch: dsce_work_model's bytes per SNR point)
         w.bytes = ns * it * (3.0 * LK + NP) * B16;
+        return w;
+    }
+    if (name == "perfect_ic" && (s.path & PATH_PIC_POLY)) {
+        // polyphase passes per unit and IC iteration: C u and an IDFT-F per
+        // symbol, the synthesis window sums (nnz(A) real x complex MACs per tap),
+        // the channel (nt CMACs per sample), the analysis window sums (nnz(B)),
+        // a DFT-F and E per symbol, y - out + h u per row; bytes: u, y, h read
+        // and y_perf written (V and the window sums are the kernels' own scratch)
+        const double F = s.k.poly_F, K = s.k.poly_K, DF = 5.0 * F * std::log2(F);
+        const double per = 2.0 * K * (DF + 8.0 * F) + 4.0 * nt * s.poly_nnz_a + 8.0 * nt * s.N +
+                           4.0 * s.poly_nnz_b + 16.0 * LK;
+        w.flops = ns * it * per;
+        w.bytes = ns * it * 3.0 * LK * B16 + it * LK * B16;
         return w;
     }
     if (!fft) return w;

@@ -352,8 +352,9 @@ int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per
  * n-point DFT; transcendentals and RNG integer work not counted) and the
  * compulsory HBM bytes (each operand read once per realisation / unit, each
  * result written once).  Modelled: the FFT-form OFDM chain (k_jakes, tx,
- * rx_front, perfect_ic, k_mic_pilot, k_mic_data) and the W contraction
- * (k_wcontract); 0 = not modelled for the path that ran.  DESIGN.md section 4
+ * rx_front, perfect_ic, k_mic_pilot, k_mic_data), the polyphase perfect-CSI
+ * passes (perfect_ic of FBMC / L = 48 OFDM) and the W contraction (k_wcontract);
+ * 0 = not modelled for the path that ran.  DESIGN.md section 4
  * lists the per-unit formulas. */
 int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, double* bytes_per_rep);
 /* The guard of the structured MMSE IC (D_hat = Q' H_hat G, DSCE_PATH_MIC_FFT),
