@@ -603,10 +603,11 @@ def main():
                    "parallelism": "dp%d" % world, "options": options},
         "roofline": {"bound": bound,
                      "kernel": ("k_mic_data: every MMSE stage (one-tap + IC iterations) of the OFDM symbols without "
-                                "pilots, decisions in registers: per stage H_hat = Bv hP on the matrix cores (3M), "
-                                "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain, one-tap + detection on the "
-                                "VALU; FP64 roofline (MFMA and VALU FP64 share the SIMD on gfx950, no overlap; both "
-                                "peaks 78.6 TF)") if mic_l else
+                                "pilots, decisions in registers: per stage the estimated taps H_hat = T_k Z (low-rank "
+                                "operator, Z = Bz hP from k_mic_pilot; without it Bv hP on the matrix cores), "
+                                "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain (4-point network on the "
+                                "matrix cores), one-tap + detection on the VALU; FP64 roofline (MFMA and VALU FP64 "
+                                "share the SIMD on gfx950, no overlap; both peaks 78.6 TF)") if mic_l else
                                ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
                                 "diag(D_hat) + detection in its epilogue)"),
                      "achieved": roof_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -625,10 +626,11 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
                      "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
                      "flops_per_launch": flops / launches if launches else None,
-                     "work_model": ("per unit and data symbol: stage 0 window sums ntap x NP + 24; per IC stage the "
-                                    "estimated taps ntap x 24 x NP CMACs, their window sums ntap x 24, the channel "
-                                    "ntap x 24, diag(D_hat_prev) v 24, this stage's window sums ntap x NP and diag 24 "
-                                    "(8 flops per CMAC) + two DFT-24 at 5 n log2 n flops") if mic_l else
+                     "work_model": ("dsce_kernel_work('k_mic_data'), per unit and data symbol: stage 0 one-tap; per "
+                                    "IC stage two DFT-24 (5 n log2 n), the channel, y_ic / one-tap / re-precoding "
+                                    "(8 flops per CMAC) and the estimated taps: low-rank ntap x 24 x 4 real x complex "
+                                    "MACs + window sums (4 flops each) + diag ntap x 24 CMACs (GEMM form: ntap x 24 x "
+                                    "NP CMACs); DESIGN.md section 4.0") if mic_l else
                                    ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
                                     "fused diag(D_hat)); achieved / frac count the executed 6 flops per CMAC of the 3M "
                                     "form, achieved_algorithmic_8flop the 8-flop equivalent; mfma_busy = executed "
