@@ -504,7 +504,7 @@ def main():
         flops += f
         # matrix-core flops actually executed per counted flop: 3 real MFMAs per
         # complex product in the 3M form (the W contraction is that GEMM alone)
-        executed += f * (0.75 if ({"wpair3", "wpair3_fused"} & p) and not mic_l else 1.0)
+        executed += f * (0.75 if ({"wpair3", "wpair3_fused", "wrow3"} & p) and not mic_l else 1.0)
     paths = [sorted(p) for p in paths]
     work = {name: {"cmac_per_rep": eng.work_model(sid)[0], "mmse_kernel": mmse_kernel(set(paths[sid]))}
             for sid, name in enumerate(schemes)}
@@ -608,8 +608,9 @@ def main():
                                 "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain (4-point network on the "
                                 "matrix cores), one-tap + detection on the VALU; FP64 roofline (MFMA and VALU FP64 "
                                 "share the SIMD on gfx950, no overlap; both peaks 78.6 TF)") if mic_l else
-                               ("k_wcontract: MMSE contraction (k_wpair3 pair tiles, 3M; OFDM: with the next stage's "
-                                "diag(D_hat) + detection in its epilogue)"),
+                               ("k_wcontract: MMSE contraction, 3M on the matrix cores (32-row blocks: k_wrow3, one "
+                                "GEMM per row tile with B = hP v_c; k_wpair3 pair tiles otherwise; OFDM: with the "
+                                "next stage's diag(D_hat) + detection in its epilogue)"),
                      "achieved": roof_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (roof_tf / FP64_PEAK_TFLOPS) if roof_tf else None,
                      "achieved_basis": "8 flops per complex MAC (algorithmic)" if mic_l else

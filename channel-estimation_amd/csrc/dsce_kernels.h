@@ -40,6 +40,8 @@ struct Opts {
                               // L != 24) as IDFT-L per symbol + window sums per residue + DFT-L per symbol
                               // (k_poly_syn / k_poly_chan / k_poly_ana) instead of the two banded passes
                               // (r04 box, C3: 14.3 -> 8.7 ms per iteration); 0 = the banded passes
+    int wrow = 1;             // unfused W contraction of 32-row blocks (FBMC, C5) as one GEMM per row tile
+                              // (k_wrow3: X = hP v_c as the B operand, no per-tile epilogue); 0 = k_wpair3
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower
@@ -65,6 +67,7 @@ enum : unsigned {
     PATH_MIC_STAGES = 1u << 14,    // k_mic_pilot + k_mic_data: every MMSE stage in one launch pair
     PATH_MIC_LR = 1u << 15,        // ... with the low-rank tap operator T_k Z (build_mic_lr)
     PATH_PIC_POLY = 1u << 16,      // perfect-CSI IC by polyphase synthesis / analysis (k_poly_*)
+    PATH_WROW3 = 1u << 17,         // unfused W contraction as one GEMM per row tile (k_wrow3)
 };
 
 // Per-stage trace of one unit (dsce_trace_unit_ex): every kernel that forms one

@@ -3418,6 +3418,110 @@ __global__ void __launch_bounds__(256)
     wpair3_body<RBP, NKS, FUSE>(P, W3, wp_elems, var, nsnr, snr0, R, U, hp, v, y, yest, sk, fa);
 }
 
+// The unfused W contraction of 32-row blocks (FBMC, C5) as ONE GEMM per row
+// tile (k_wrow3, Opts::wrow): y_est[r] = y[r] - sum_(c,p) W[(r,c),p] X[(c,p)]
+// with X[(c,p)] = hP_p v_c per unit.  M = the block's rows (two 16-row tiles),
+// K = (column, pilot), N = units: the pair tile t = 2 c + h of k_wpair3's
+// storage IS the A fragment of row tile h and column c (pairs q = 32 c + r), so
+// the same W3 planes feed it.  The accumulators (3M: P1, P2, P3 per row tile)
+// stay in registers over every column of the band and the complex
+// D_hat[r,c] v_c epilogue of each tile disappears: per column the VALU forms
+// X = hP v_c once (NKS complex products, shared by both row tiles) instead of
+// 2 x 4 complex MACs plus the 3M recombination per tile (k_wpair3: 17 % of the
+// issue next to 3 NKS MFMAs per tile at C3 / C4).  Same flops, other rounding
+// order (parity to 1e-9 like every contraction path).
+template <int NKS>
+__global__ void __launch_bounds__(256)
+    k_wrow3(PairBand P, const double* __restrict__ W3, long long wp_elems, int var, int nsnr, int snr0, int R, int U,
+            const double2* __restrict__ hp, const double2* __restrict__ v, const double2* __restrict__ y,
+            double2* __restrict__ yest) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+    const int unit = blockIdx.x * 64 + wv * 16 + j;
+    const int snr = snr0 + (blockIdx.x * 64) / R;
+    const int blk = blockIdx.y;
+    double2 hpl[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) hpl[ks] = hp[(size_t)(4 * ks + g) * U + unit];
+    const int clo = P.clo[blk], ntile = P.ntile[blk];
+    const double* __restrict__ w =
+        W3 + ((size_t)var * nsnr + snr) * 3 * (size_t)wp_elems + 3 * P.off[blk] + 2 * lane;
+    const double2* __restrict__ vb = v + (size_t)clo * U + unit;
+    struct T3 {
+        double r[NKS], i[NKS], s[NKS];
+    };
+    auto ldt = [&](int t, T3& a) {
+#pragma unroll
+        for (int kp = 0; kp < NKS / 2; ++kp) {
+            const double2* q = reinterpret_cast<const double2*>(w + ((size_t)t * (NKS / 2) + kp) * 384);
+            const double2 r = q[0], i = q[64], sm = q[128];
+            a.r[2 * kp] = r.x;
+            a.r[2 * kp + 1] = r.y;
+            a.i[2 * kp] = i.x;
+            a.i[2 * kp + 1] = i.y;
+            a.s[2 * kp] = sm.x;
+            a.s[2 * kp + 1] = sm.y;
+        }
+    };
+    double xr[NKS], xi[NKS], xs[NKS];
+    auto formx = [&](double2 vc) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const double2 xv = c_mulf(hpl[ks], vc);
+            xr[ks] = xv.x;
+            xi[ks] = xv.y;
+            xs[ks] = xv.x + xv.y;
+        }
+    };
+    d4 p[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[h][k] = d4{0.0, 0.0, 0.0, 0.0};
+    auto mma = [&](const T3& a, auto hc) {
+        constexpr int h = decltype(hc)::value;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            p[h][0] = MFMA64(a.r[ks], xr[ks], p[h][0]);
+            p[h][1] = MFMA64(a.i[ks], xi[ks], p[h][1]);
+            p[h][2] = MFMA64(a.s[ks], xs[ks], p[h][2]);
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    // ping-pong W tiles (tile t + 1's loads issued before tile t's MFMAs) and v
+    // one column ahead; a column is two tiles (row tiles 0 and 1)
+    T3 A0, A1;
+    const int ncol = ntile / 2;
+    double2 vn = ncol > 0 ? vb[0] : make_double2(0.0, 0.0);
+    if (ntile > 0) ldt(0, A0);
+    for (int c = 0; c < ncol; ++c) {
+        const int t0 = 2 * c;
+        formx(vn);
+        vn = vb[(size_t)(c + 1 < ncol ? c + 1 : c) * U];
+        ldt(t0 + 1, A1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A0, I0{});
+        __builtin_amdgcn_sched_barrier(0);
+        ldt(t0 + 2 < ntile ? t0 + 2 : t0 + 1, A0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(A1, I1{});
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int row0 = P.row0[blk], nrows = P.nrows[blk];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = 16 * h + g + 4 * i;
+            if (r < nrows) {
+                const size_t ix = (size_t)(row0 + r) * U + unit;
+                const double re = p[h][0][i] - p[h][1][i], im = p[h][2][i] - p[h][0][i] - p[h][1][i];
+                yest[ix] = c_sub(y[ix], make_double2(re, im));
+            }
+        }
+}
+
 // Pre-pass of the fused MMSE stage of IC iteration `stage` (script:482-489):
 // y_est at the NP pilot rows with the previous stage's D_hat (W of var_prev,
 // the contraction's), then the LS estimates hP = y_est(pilots) ./ xP /
@@ -3509,6 +3613,18 @@ unsigned launch_wcontract(hipStream_t s, const Opts& op, const SchemeK& sk, cons
     // packed band where no pair tiles exist (a block wider than 32 rows) or on
     // request (Opts::wcontract_valu)
     const bool pair_ok = mm.Wp3 && (b.U % 64) == 0 && (b.R % 64) == 0 && !op.wcontract_valu;
+    if (pair_ok && op.wrow && mm.Pb.rbp == 32) {
+        // 32-row blocks: one GEMM per row tile, no per-tile epilogue (k_wrow3)
+        const dim3 grid(b.U / 64, mm.Pb.nblk);
+#define LAUNCH_WR(NKSV)                                                                                            \
+    hipLaunchKernelGGL((k_wrow3<NKSV>), grid, dim3(256), 0, s, mm.Pb, mm.Wp3, mm.wp_elems, var, mm.nsnr, b.snr0, b.R, \
+                       b.U, b.hp, b.v, b.y, b.yest)
+        if (mm.Pb.nks == 2) LAUNCH_WR(2);
+        else if (mm.Pb.nks == 4) LAUNCH_WR(4);
+        else LAUNCH_WR(8);
+#undef LAUNCH_WR
+        return PATH_WROW3;
+    }
     if (pair_ok) {
         const dim3 grid(b.U / 64, mm.Pb.nblk);
 #define LAUNCH_W3(RBPV, NKSV)                                                                                  \

@@ -33,7 +33,7 @@ PATH_BITS = {
     "wpair3_fused": 1 << 0, "wpair3": 1 << 1, "wpair4m": 1 << 2, "wcontract_valu": 1 << 3, "pic_mfma": 1 << 4,
     "pic_chain": 1 << 5, "pic_passes": 1 << 6, "stage_fused": 1 << 7, "stage_split": 1 << 8, "noise_fused": 1 << 9,
     "pic_fft": 1 << 10, "mic_fft": 1 << 11, "txrx_fft": 1 << 12, "pilot_fused": 1 << 13, "mic_stages": 1 << 14,
-    "mic_lr": 1 << 15, "pic_poly": 1 << 16,
+    "mic_lr": 1 << 15, "pic_poly": 1 << 16, "wrow3": 1 << 17,
 }
 
 

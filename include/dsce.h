@@ -206,6 +206,8 @@ typedef struct {
 #define DSCE_PATH_PIC_POLY        (1u << 16)  /* perfect-CSI IC of a polyphase scheme (FBMC; OFDM with L = 48) as
                                                  IDFT-L per symbol + window sums per residue + DFT-L per symbol
                                                  (k_poly_syn / k_poly_chan / k_poly_ana, option pic_poly) */
+#define DSCE_PATH_WROW3           (1u << 17)  /* unfused W contraction of 32-row blocks as one GEMM per row tile,
+                                                 B = hP v_c (k_wrow3, option wrow) */
 
 int dsce_abi_version(void);
 int dsce_device_count(int* count);
@@ -328,7 +330,10 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   subcarrier tones, G[n, l + L k] = A_k[n] e^(2 pi i l n / L) C[l][k], checked
  *   entry by entry to 1e-12 at dsce_add_scheme, with L = 24 or 48, as an IDFT-L
  *   per symbol, window sums per residue n mod L around the channel, and a DFT-L
- *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes).
+ *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes),
+ *   wrow (1: the unfused W contraction of 32-row blocks — FBMC, C5 — as one
+ *   GEMM per 16-row tile over (column, pilot) with B = hP v_c, no per-tile
+ *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */

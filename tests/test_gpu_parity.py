@@ -226,6 +226,8 @@ def test_fbmc_estimator_and_trace(fbmc):
         ns = _check_trace(g, u, "%s snr %d" % (name, k))
         for st in range(1, ns):        # unfused perfect-CSI passes: y_perf of every row
             np.testing.assert_allclose(g["yperf"][st], u["yperf"][st], rtol=0, atol=1e-9)
+    # the row-tile GEMM contraction and the polyphase perfect-CSI passes ran
+    assert {"wrow3", "pic_poly"} <= eng.path_info(0), eng.path_info(0)
 
 
 def test_fbmc_error_counts(fbmc):
@@ -433,7 +435,8 @@ def test_stage_variants_agree(name):
     iteration stopping at the fixed point instead of computed (pic_skip 1), the
     perfect-CSI passes banded instead of polyphase (pic_poly 0; FBMC) and
     polyphase for OFDM too (pic_poly 1 with pic_chain 0: OFDM's chain is
-    otherwise k_pic_fft)."""
+    otherwise k_pic_fft), the FBMC contraction as k_wpair3's pair tiles instead
+    of k_wrow3's row-tile GEMM (wrow 0)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -451,7 +454,7 @@ def test_stage_variants_agree(name):
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
                 {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 1},
-                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0})
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
