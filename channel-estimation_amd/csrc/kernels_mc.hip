@@ -3756,8 +3756,20 @@ __global__ void __launch_bounds__(64) k_detect(SchemeK sk, StageArgs st, const u
             if (sk.despread) {                                  // x = P' (y ./ h), script:436 / :520
                 const int row = sk.NP + i;
                 double2 acc = make_double2(0.0, 0.0);
-                for (int j = sk.ph_ptr[row]; j < sk.ph_ptr[row + 1]; ++j)
-                    c_fma(acc, sk.ph_val[j], e[(size_t)sk.ph_col[j] * U + unit]);
+                // entries in groups of 4, every load of a group issued before its
+                // products (one global round trip per group instead of per entry)
+                const int j0 = sk.ph_ptr[row], j1 = sk.ph_ptr[row + 1];
+                for (int jb = j0; jb < j1; jb += 4) {
+                    double2 ev[4], pv[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int jj = min(jb + g, j1 - 1);
+                        pv[g] = jb + g < j1 ? sk.ph_val[jj] : make_double2(0.0, 0.0);
+                        ev[g] = e[(size_t)sk.ph_col[jj] * U + unit];
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) c_fma(acc, pv[g], ev[g]);
+                }
                 z = acc;
                 z = sk.real_detect ? make_double2(z.x / sk.data_div, 0.0)
                                    : make_double2(z.x / sk.data_div, z.y / sk.data_div);
@@ -3795,16 +3807,33 @@ __global__ void __launch_bounds__(64) k_precode(SchemeK sk, StageArgs st, const 
     const int r1 = min(sk.LK, r0 + DSCE_RB);
     for (int r = r0; r < r1; ++r) {
         double2 av = make_double2(0.0, 0.0), au = make_double2(0.0, 0.0);
-        for (int j = sk.p_ptr[r]; j < sk.p_ptr[r + 1]; ++j) {
-            const int k = sk.p_col[j];
-            const double2 pv = sk.p_val[j];
-            if (k < sk.NP) {
-                const double2 x = xp[(size_t)k * R + rl];
-                c_fma(av, pv, x);
-                c_fma(au, pv, x);
-            } else {
-                c_fma(av, pv, sym[qe[(size_t)(k - sk.NP) * U + unit]]);
-                c_fma(au, pv, sym[qp[(size_t)(k - sk.NP) * U + unit]]);
+        const int j0 = sk.p_ptr[r], j1 = sk.p_ptr[r + 1];
+        // entries in groups of PJ: every index / pilot load of a group is issued
+        // before the first LDS lookup (a row of the auxiliary-symbol precoder has
+        // ~30 entries; one dependent global -> LDS -> FMA round trip per entry
+        // left the kernel latency-bound, r04: 4.3 ms per C3 launch)
+        constexpr int PJ = 4;
+        for (int jb = j0; jb < j1; jb += PJ) {
+            int ie[PJ], iq[PJ];
+            double2 xv[PJ];
+#pragma unroll
+            for (int g = 0; g < PJ; ++g) {
+                const int k = sk.p_col[min(jb + g, j1 - 1)];
+                if (k < sk.NP) {                                  // uniform branch
+                    xv[g] = xp[(size_t)k * R + rl];
+                    ie[g] = iq[g] = -1;
+                } else {
+                    xv[g] = make_double2(0.0, 0.0);
+                    ie[g] = qe[(size_t)(k - sk.NP) * U + unit];
+                    iq[g] = qp[(size_t)(k - sk.NP) * U + unit];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < PJ; ++g) {
+                if (jb + g >= j1) break;                          // uniform
+                const double2 pv = sk.p_val[jb + g];
+                c_fma(av, pv, ie[g] >= 0 ? sym[ie[g]] : xv[g]);
+                c_fma(au, pv, iq[g] >= 0 ? sym[iq[g]] : xv[g]);
             }
         }
         v[(size_t)r * U + unit] = av;
