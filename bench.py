@@ -301,6 +301,19 @@ def stored_pmc(kernel_tag, workload):
     return None, "no PMC profile of this source build (%s) for %s under profiles/" % (src, workload)
 
 
+def dominant_by_time(kernels, roof_kernel):
+    """The kernel group with the largest share of the measured step, with its own
+    algorithmic rate and limiter (bench line `kernels`), or None when that is the
+    roofline kernel itself."""
+    if not kernels:
+        return None
+    k, e = max(kernels.items(), key=lambda kv: kv[1].get("ms_per_step") or 0.0)
+    if k == roof_kernel:
+        return None
+    keys = ("ms_per_step", "share", "tflops", "frac_fp64", "traffic_per_launch", "valu_issue", "mfma_busy", "limiter")
+    return dict({"kernel": k}, **{kk: e.get(kk) for kk in keys})
+
+
 def stored_pmc_all(workload):
     """The committed per-kernel-group PMC summary (profiles/*_pmc_all.json,
     tools/prof_summary.py --all) of THIS source build and workload, or None."""
@@ -638,7 +651,10 @@ def main():
                                     "matrix-core flops / measured peak"),
                      "paths": paths,
                      "limiter": lim["limiter"] if lim else None,
-                     "counters": lim},
+                     "counters": lim,
+                     # the largest kernel group by measured time, when it is not the roofline kernel
+                     # above (C2 since r04: k_pic_fft's perfect_ic group, as large as k_mic_data)
+                     "dominant_by_time": dominant_by_time(kernels, kname)},
         "cpu_baseline": cpu,
         "allreduce": allreduce,
         "setup_s": setup_s,
