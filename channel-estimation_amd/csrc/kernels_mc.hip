@@ -1974,7 +1974,8 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                                             const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
                                             int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
                                             int snr, const double* twl = nullptr, const double* tsl = nullptr,
-                                            double2 (*szz)[NT * MIC_NB][17] = nullptr, int unit0 = 0) {
+                                            double2 (*szz)[NT * MIC_NB][17] = nullptr, int unit0 = 0,
+                                            const double2* bzl = nullptr) {
     constexpr int NZ = NT * MIC_NB;
     const int cq = NM ? r : (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
@@ -2146,11 +2147,13 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             __syncthreads();
             if constexpr (LR) {
                 // Z_s = Bz(var_s) hP_s for the block's 16 units: one entry per thread
+                // (Bz of both variants staged in LDS at kernel start: no global
+                // round trip between the stage's two barriers)
                 const int vs = mic_var(s, ma.niter);
                 const int t = threadIdx.x;
                 if (t < NZ * 16) {
                     const int j = t >> 4, u = t & 15;
-                    const double2* __restrict__ bz = ma.bz + (((size_t)vs * ma.nsnr + snr) * NZ + j) * NP;
+                    const double2* bz = bzl + ((size_t)vs * NZ + j) * NP;
                     double2 acc = c_mul(bz[0], hx[u]);
 #pragma unroll
                     for (int p = 1; p < NP; ++p) c_fma(acc, bz[p], hx[p * 17 + u]);
@@ -2270,6 +2273,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
     __shared__ double2 szz[LR ? 2 : 1][NZ][17];             // LR: Z of the block's 16 units, double-buffered
     __shared__ double twp[LR ? 4 : 1][MIC_NB * 24 + MIC_NB];   // LR: each wave's T_k window + sums
+    __shared__ double2 bzl[LR ? 2 * NZ * NP : 1];           // LR: Bz of both variants at this SNR
     __shared__ int cntl[4][PM_MAXIT + 1];
     const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
@@ -2286,6 +2290,10 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     if (LR) {
         for (int i = l; i < MIC_NB * 25; i += 64)
             twp[w][i] = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
+        for (int i = tid; i < 2 * NZ * NP; i += blockDim.x) {
+            const int var = i / (NZ * NP), jp = i % (NZ * NP);
+            bzl[i] = ma.bz[((size_t)var * ma.nsnr + snr) * NZ * NP + jp];
+        }
     } else {
         const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
         bss[LR ? 0 : w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
@@ -2303,7 +2311,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     auto Bs = [&](int var, int q, int p) { return bss[LR ? 0 : w][var][q][p]; };
     mic2_stages<NT, SH, NP, TRACE, true, NM, LR>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
                                                  Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twp[LR ? w : 0],
-                                                 twp[LR ? w : 0] + MIC_NB * 24, szz, ug16 * 16);
+                                                 twp[LR ? w : 0] + MIC_NB * 24, szz, ug16 * 16, bzl);
     __syncthreads();
     // one atomic per (stage, edge) per block
     for (int i = tid; i < 2 * (ma.niter + 1); i += blockDim.x) {
