@@ -7,6 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 tag=${1:-x}
 shift
 for c in "$@"; do
-  bash tools/gpu_bench_evidence.sh ${tag}_$c $c k_wcontract k_wpair3 || { echo config_fail $c; exit 1; }
+  # the FBMC / C5 contraction kernel: k_wrow3 (32-row blocks, Opts::wrow) since r04
+  bash tools/gpu_bench_evidence.sh ${tag}_$c $c k_wcontract k_wrow3 || { echo config_fail $c; exit 1; }
 done
 echo configs_ok

@@ -55,8 +55,10 @@ SQ_COUNTERS = ("GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_AN
 
 # rocprof kernel name (substring) -> timing group (dsce_api.hip Timed names)
 GROUPS = (("k_jakes", "k_jakes"), ("k_tx_rows", "tx"), ("k_tx_symbols", "tx"), ("k_txrx_fft", "rx_front"),
-          ("k_pic_fft", "perfect_ic"), ("k_mic_pilot", "k_mic_pilot"), ("k_mic_data", "k_mic_data"),
-          ("k_wpair3", "k_wcontract"), ("k_pilot_pre", "k_pilot_pre"), ("k_stage", "k_stage"))
+          ("k_pic_fft", "perfect_ic"), ("k_poly_", "perfect_ic"), ("k_mic_pilot", "k_mic_pilot"),
+          ("k_mic_data", "k_mic_data"), ("k_wpair3", "k_wcontract"), ("k_wrow3", "k_wcontract"),
+          ("k_wcontract_valu", "k_wcontract"), ("k_pilot_pre", "k_pilot_pre"), ("k_stage", "k_stage"),
+          ("k_precode", "k_stage"), ("k_ls", "k_stage"), ("k_detect", "k_stage"))
 
 
 def short(name):
