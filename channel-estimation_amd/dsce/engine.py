@@ -399,8 +399,10 @@ class Engine:
 
     def structured_check(self, sid):
         """build_mic's guard of the structured MMSE IC (dsce_structured_check): dict with
-        ratio (kept iff <= 1), dev (max |Q' H_hat G - W_thr|), wmax (max |W|), rtol, and
-        the low-rank tap operator's fit residual lr_resid (relative) and lr (in use)."""
+        ratio (kept iff <= 1: the worst slice's deviation over its rounding bar
+        min(1e-9, max(1e-11, 4e-16 kappa(R))) max|W|), dev (max |Q' H_hat G - W_thr|),
+        wmax (max |W|), rtol (the largest per-slice bar), and the low-rank tap
+        operator's fit residual lr_resid (relative), lr (in use) and lr_ratio."""
         out = (C.c_double * 7)()
         self._chk(self.lib.dsce_structured_check(self.h, int(sid), out), "dsce_structured_check")
         return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3], lr_resid=out[4], lr=bool(out[5]),
