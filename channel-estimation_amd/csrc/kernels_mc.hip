@@ -3696,26 +3696,20 @@ struct StageArgs {
     double* mse_pow;
 };
 
-// (1) LS pilot estimates, h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p and the
-// one-tap quotients y./h_hat (MMSE) and y./h (perfect CSI) for a block of 24
-// rows; grid (U/64, ceil(LK/24)).
+// (1) h_hat = diag(D_hat) = sum_p W[(c,c),p] hP_p and the one-tap quotients
+// y./h_hat (MMSE) and y./h (perfect CSI) for a block of DSCE_RB rows, from the
+// LS pilot estimates k_ls wrote (r04: each row block recomputed the NP complex
+// LS divisions itself, and wrote h_hat, which nothing reads, to HBM);
+// grid (U/64, ceil(LK/RB)).
 __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const double2* __restrict__ Wd,
-                                                const double2* __restrict__ xp, const double2* __restrict__ h,
-                                                double2* __restrict__ hp, double2* __restrict__ hest,
+                                                const double2* __restrict__ h, const double2* __restrict__ hp,
                                                 double2* __restrict__ e_est, double2* __restrict__ e_perf) {
     extern __shared__ double2 shp[];                     // [NP][64], each lane its own column
     const int unit = blockIdx.x * WAVE + threadIdx.x;
     const int snr = st.snr0 + (blockIdx.x * WAVE) / st.R;
     const int rl = unit % st.R;
     const int U = st.U, R = st.R;
-    const double sqk = 1.0 / sk.inv_sqrt_kappa;
-    for (int p = 0; p < sk.NP; ++p) {
-        const double2 yv = st.ysrc_e[(size_t)sk.pilot_pos[p] * U + unit];
-        const double2 q = c_div(yv, xp[(size_t)p * R + rl]);
-        const double2 hv = make_double2(q.x / sqk, q.y / sqk);
-        shp[p * WAVE + threadIdx.x] = hv;
-        if (blockIdx.y == 0) hp[(size_t)p * U + unit] = hv;
-    }
+    for (int p = 0; p < sk.NP; ++p) shp[p * WAVE + threadIdx.x] = hp[(size_t)p * U + unit];
     const double2* __restrict__ wd = Wd + ((size_t)st.var * st.nsnr + snr) * (size_t)sk.LK * sk.NP;
     const int r0 = blockIdx.y * DSCE_RB;
     const int r1 = min(sk.LK, r0 + DSCE_RB);
@@ -3725,7 +3719,6 @@ __global__ void __launch_bounds__(64) k_ls_hest(SchemeK sk, StageArgs st, const 
         for (int p = 0; p < sk.NP; ++p) c_fma(acc, wd[(size_t)c * sk.NP + p], shp[p * WAVE + threadIdx.x]);
         const size_t i = (size_t)c * U + unit;
         const double2 hv = h[(size_t)c * R + rl];
-        hest[i] = acc;
         if (st.tr && unit == st.tr->unit) st.tr->hest[(size_t)st.stage * st.tr->LK + c] = acc;
         e_est[i] = c_div(st.ysrc_e[i], acc);
         e_perf[i] = c_div(st.ysrc_p[i], hv);
@@ -4111,8 +4104,9 @@ unsigned launch_stage(hipStream_t s, const Opts& op, const SchemeK& sk, const Mm
                                b.u);
         return PATH_STAGE_FUSED;
     }
+    hipLaunchKernelGGL(k_ls, dim3(b.U / WAVE), dim3(WAVE), 0, s, sk, st, b.xp, b.hp);
     hipLaunchKernelGGL(k_ls_hest, dim3(b.U / WAVE, rblk), dim3(WAVE), (size_t)sk.NP * WAVE * sizeof(double2), s, sk,
-                       st, mm.Wd, b.xp, b.h, b.hp, b.hest, b.e, b.e2);
+                       st, mm.Wd, b.h, b.hp, b.e, b.e2);
     hipLaunchKernelGGL(k_detect, dim3(b.U / WAVE, (sk.ND + DET_CHUNK - 1) / DET_CHUNK), dim3(WAVE), 0, s, sk, st,
                        b.sidx, b.e, b.e2, b.qe, b.qp, counters);
     if (!last)
