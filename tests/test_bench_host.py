@@ -53,7 +53,7 @@ def test_source_hash_covers_the_engine_sources():
     assert h == bench.source_hash()
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(ROOT, "profiles", "r04g*_bench.json"))))
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(ROOT, "profiles", "r04h*_bench.json"))))
 def test_committed_bench_lines_keep_the_contract(path):
     """Every committed final-round bench line: the driver's keys, a roofline
     fraction in (0, 1], the CPU baseline object, and a stamped PMC source."""
