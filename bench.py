@@ -61,6 +61,25 @@ WORKLOADS = {
 }
 
 
+# the roofline object's description of each kernel group (bench line `roofline.kernel`)
+KERNEL_DESC = {
+    "perfect_ic": ("k_pic_fft: the perfect-CSI branch of every FFT-form OFDM symbol, stage 0 one-tap + the 4 IC "
+                   "iterations (script:428-466, :541-561) with u, y / h, 1 / h and the taps in registers: per "
+                   "iteration y - (D - diag h) u by IDFT-24 (prime-factor DFT-6 per lane + 4-point network on "
+                   "v_mfma_f64_4x4x4f64), the channel's taps, DFT-24, then one-tap, slicer, counts, re-precoding; "
+                   "FP64 roofline (f64 VALU and MFMA share the SIMD's issue on gfx950; peak 78.6 TF)"),
+    "k_mic_data": ("k_mic_data: every MMSE stage (one-tap + IC iterations) of the OFDM symbols without pilots, "
+                   "decisions in registers: per stage the estimated taps H_hat = T_k Z (low-rank operator, Z = Bz hP "
+                   "from k_mic_pilot), y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain, one-tap + detection; "
+                   "FP64 roofline (VALU and MFMA share the issue)"),
+    "k_mic_pilot": "k_mic_pilot: every MMSE stage of the pilot symbols, LS pilots and Z = Bz hP per stage",
+    "rx_front": ("k_txrx_fft: TX IDFT-24, the doubly-selective channel, and per SNR point the AWGN draw (Philox4x32-10 "
+                 "+ table-driven Box-Muller) and the receiver DFT-24"),
+    "k_jakes": "k_jakes_grp: the Jakes sum-of-sinusoids taps at the samples the receiver windows read",
+    "tx": "k_tx_rows: bits -> Gray -> P [xP; xD]",
+}
+
+
 def source_hash():
     """sha256 over the engine's sources: stamps PMC profiles to the build they measured."""
     h = hashlib.sha256()
@@ -497,45 +516,6 @@ def main():
     total_reps = B * args.steps * world
     value = total_reps / el
 
-    # roofline of the dominant kernel (HIP events on the engine's stream): each
-    # scheme's MMSE kernel is k_mic_data (FFT-form OFDM: every stage in one launch
-    # pair with k_mic_pilot) or the W contraction k_wcontract; the dominant one by
-    # measured time carries the roofline, with the work model of the schemes it runs
-    def mmse_kernel(p):
-        return "k_mic_data" if "mic_stages" in p else "k_wcontract"
-    paths = [eng.path_info(sid) for sid in range(len(schemes))]
-    kname = max({mmse_kernel(p) for p in paths}, key=lambda k: eng.kernel_time(k)[1])
-    mic_l = kname != "k_wcontract"
-    launches, wc_ms = eng.kernel_time(kname)
-    flops = 0.0
-    executed = 0.0
-    for sid, p in enumerate(paths):
-        if mmse_kernel(p) != kname:
-            continue
-        cmac_per_rep, _ = eng.work_model(sid)
-        f = cmac_per_rep * 8.0 * B * args.steps
-        flops += f
-        # matrix-core flops actually executed per counted flop: 3 real MFMAs per
-        # complex product in the 3M form (the W contraction is that GEMM alone)
-        executed += f * (0.75 if ({"wpair3", "wpair3_fused", "wrow3"} & p) and not mic_l else 1.0)
-    paths = [sorted(p) for p in paths]
-    work = {name: {"cmac_per_rep": eng.work_model(sid)[0], "mmse_kernel": mmse_kernel(set(paths[sid]))}
-            for sid, name in enumerate(schemes)}
-    achieved_tf = flops / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None        # 8 flops per complex MAC
-    exec_tf = executed / (wc_ms * 1e-3) / 1e12 if wc_ms > 0 else None         # what the matrix cores executed
-    # the roofline rate: the 8-flop algorithmic count for k_mic_data (a VALU /
-    # matrix-core mix, below the peak either way); for the 3M contraction the
-    # executed flops (its 8-flop equivalent rate exceeds the peak: VERDICT r03 #6)
-    roof_tf = achieved_tf if mic_l else exec_tf
-    peak_meas = eng.fp64_mfma_peak()
-    pmc, traffic_src = stored_pmc(kname, args.config)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    avg_ms = wc_ms / launches if launches else None
-    lim = derive_limiter(pmc, roof_tf, avg_ms)
-    # the roof the kernel sits closer to: FP64 compute (MFMA / VALU share the
-    # peak) or HBM (traffic from the stamped PMC pass)
-    hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
-    bound = "hbm" if hbm_frac is not None and roof_tf and hbm_frac > roof_tf / FP64_PEAK_TFLOPS else "mfma"
     # every timed kernel group on its own roofline (dsce_kernel_work: algorithmic
     # flops and compulsory bytes per realisation), plus the step as a whole
     pmc_all, pmc_all_src = stored_pmc_all(args.config)
@@ -579,6 +559,57 @@ def main():
                  "frac_fp64": step_flops / (step_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if step_ms else None,
                  "kernel_ms_modelled_share": modelled_ms / tot_ms if tot_ms else None,
                  "note": "algorithmic flops of every modelled kernel group per step / wall time per step / 78.6 TF"}
+
+    # the roofline object: the DOMINANT kernel group by measured time (HIP events
+    # on the engine's stream) among those with a work model (C2's
+    # perfect-CSI chain k_pic_fft became the largest in r04)
+    paths = [eng.path_info(sid) for sid in range(len(schemes))]
+    kname = max((k for k in kernels if kernels[k].get("flops_per_rep")), key=lambda k: kernels[k]["ms_per_step"])
+    launches, k_ms = eng.kernel_time(kname)
+    avg_ms = k_ms / launches if launches else None
+    peak_meas = eng.fp64_mfma_peak()
+    contraction = kname == "k_wcontract"
+    if contraction:
+        # the W contraction: 3M on the matrix cores; the roofline rate counts the
+        # flops the matrix cores execute (its 8-flop equivalent exceeds the peak:
+        # VERDICT r03 #6), traffic and counters from its own stamped PMC summary
+        flops = executed = 0.0
+        for sid, p in enumerate(paths):
+            if "mic_stages" in p:
+                continue
+            cmac_per_rep, _ = eng.work_model(sid)
+            f = cmac_per_rep * 8.0 * B * args.steps
+            flops += f
+            executed += f * (0.75 if {"wpair3", "wpair3_fused", "wrow3"} & p else 1.0)
+        achieved_tf = flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
+        exec_tf = executed / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
+        roof_tf = exec_tf
+        pmc, traffic_src = stored_pmc(kname, args.config)
+    else:
+        # an FFT-form chain kernel group: its dsce_kernel_work flops (8 per complex
+        # MAC, 5 n log2 n per DFT) over its time; traffic and counters from the
+        # stamped per-kernel-group PMC summary of this build
+        flops = kernels[kname]["flops_per_rep"] * B * args.steps
+        achieved_tf = exec_tf = roof_tf = flops / (k_ms * 1e-3) / 1e12 if k_ms > 0 else None
+        kp = (pmc_all or {}).get(kname)
+        pmc = {"sq_per_launch": kp.get("sq_per_launch"), "hbm_bytes_per_launch": kp.get("hbm_bytes_per_launch"),
+               "avg_duration_ns_rocprof": kp.get("avg_duration_ns_rocprof")} if kp else None
+        traffic_src = pmc_all_src
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    lim = derive_limiter(pmc, roof_tf, avg_ms)
+    hbm_frac = traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic and avg_ms else None
+    # the roof the kernel sits closer to: HBM (traffic from the stamped PMC pass)
+    # or FP64 compute — the matrix cores alone for the contraction, the SIMD's
+    # shared FP64 issue (f64 VALU and f64 MFMA do not overlap on gfx950) for the
+    # chain kernels
+    if hbm_frac is not None and roof_tf and hbm_frac > roof_tf / FP64_PEAK_TFLOPS:
+        bound = "hbm"
+    else:
+        bound = "mfma" if contraction else "fp64 (VALU+MFMA shared)"
+    paths = [sorted(p) for p in paths]
+    work = {name: {"cmac_per_rep": eng.work_model(sid)[0],
+                   "mmse_kernel": "k_mic_data" if "mic_stages" in paths[sid] else "k_wcontract"}
+            for sid, name in enumerate(schemes)}
     ber = {}
     for sid, name in enumerate(schemes):
         bits = eng.bits_per_rep(sid)
@@ -615,46 +646,34 @@ def main():
         "config": {"workload": desc, "reps_per_step_per_gpu": B, "engine_batch": batch,
                    "parallelism": "dp%d" % world, "options": options},
         "roofline": {"bound": bound,
-                     "kernel": ("k_mic_data: every MMSE stage (one-tap + IC iterations) of the OFDM symbols without "
-                                "pilots, decisions in registers: per stage the estimated taps H_hat = T_k Z (low-rank "
-                                "operator, Z = Bz hP from k_mic_pilot; without it Bv hP on the matrix cores), "
-                                "y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain (4-point network on the "
-                                "matrix cores), one-tap + detection on the VALU; FP64 roofline (MFMA and VALU FP64 "
-                                "share the SIMD on gfx950, no overlap; both peaks 78.6 TF)") if mic_l else
-                               ("k_wcontract: MMSE contraction, 3M on the matrix cores (32-row blocks: k_wrow3, one "
-                                "GEMM per row tile with B = hP v_c; k_wpair3 pair tiles otherwise; OFDM: with the "
-                                "next stage's diag(D_hat) + detection in its epilogue)"),
+                     "kernel": KERNEL_DESC.get(kname, kname),
+                     "kernel_group": kname,
                      "achieved": roof_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": (roof_tf / FP64_PEAK_TFLOPS) if roof_tf else None,
-                     "achieved_basis": "8 flops per complex MAC (algorithmic)" if mic_l else
-                                       "executed matrix-core flops (3M: 6 per complex MAC)",
+                     "achieved_basis": "executed matrix-core flops (3M: 6 per complex MAC)" if contraction else
+                                       "algorithmic flops (dsce_kernel_work: 8 per complex MAC, 5 n log2 n per DFT)",
                      "achieved_algorithmic_8flop": achieved_tf, "achieved_executed": exec_tf,
                      "peak_measured": peak_meas,
                      "frac_measured": (roof_tf / peak_meas) if roof_tf and peak_meas else None,
-                     # executed matrix-core flops / measured peak from the work model (W contraction), or the
-                     # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (k_mic_data: only its tap GEMM
-                     # runs on the matrix cores)
-                     "mfma_busy": (lim or {}).get("mfma_busy") if mic_l else
-                     ((exec_tf / peak_meas) if exec_tf and peak_meas else None),
+                     # executed matrix-core flops / measured peak (the contraction), or the
+                     # SQ_VALU_MFMA_BUSY_CYCLES share of this build's PMC pass (chain kernels)
+                     "mfma_busy": ((exec_tf / peak_meas) if exec_tf and peak_meas else None) if contraction else
+                     (lim or {}).get("mfma_busy"),
+                     "valu_issue": (lim or {}).get("valu_issue"),
                      "hbm_frac": hbm_frac,
                      "traffic": traffic, "traffic_source": traffic_src, "source_hash": source_hash(),
-                     "launches": launches, "avg_launch_ms": wc_ms / launches if launches else None,
+                     "launches": launches, "avg_launch_ms": avg_ms,
                      "flops_per_launch": flops / launches if launches else None,
-                     "work_model": ("dsce_kernel_work('k_mic_data'), per unit and data symbol: stage 0 one-tap; per "
-                                    "IC stage two DFT-24 (5 n log2 n), the channel, y_ic / one-tap / re-precoding "
-                                    "(8 flops per CMAC) and the estimated taps: low-rank ntap x 24 x 4 real x complex "
-                                    "MACs + window sums (4 flops each) + diag ntap x 24 CMACs (GEMM form: ntap x 24 x "
-                                    "NP CMACs); DESIGN.md section 4.0") if mic_l else
-                                   ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
+                     "work_model": ("support-aware: CMACs over W's off-diagonal (row, column) pairs (+ LK x NP for the "
                                     "fused diag(D_hat)); achieved / frac count the executed 6 flops per CMAC of the 3M "
                                     "form, achieved_algorithmic_8flop the 8-flop equivalent; mfma_busy = executed "
-                                    "matrix-core flops / measured peak"),
+                                    "matrix-core flops / measured peak") if contraction else
+                                   ("dsce_kernel_work('%s') x realisations per launch; DESIGN.md section 4.0" % kname),
                      "paths": paths,
                      "limiter": lim["limiter"] if lim else None,
                      "counters": lim,
-                     # the largest kernel group by measured time, when it is not the roofline kernel
-                     # above (C2 since r04: k_pic_fft's perfect_ic group, as large as k_mic_data)
-                     "dominant_by_time": dominant_by_time(kernels, kname)},
+                     # the next largest kernel group, for the record
+                     "next_by_time": dominant_by_time({k: v for k, v in kernels.items() if k != kname}, None)},
         "cpu_baseline": cpu,
         "allreduce": allreduce,
         "setup_s": setup_s,

@@ -272,8 +272,11 @@ void check_ctx(dsce_ctx* c) {
     DSCE_HIP_CHECK(hipSetDevice(c->device));
     // errors are per call: a failure some earlier call already returned (or a
     // teardown ignored) must not be reported again by this call's hipGetLastError
+    // (every entry point checks its own launches at API_END, so a stale error here
+    // comes from outside the engine; reported only with DSCE_DEBUG set)
     const hipError_t stale = hipGetLastError();
-    if (stale != hipSuccess) fprintf(stderr, "dsce: clearing a stale HIP error at entry: %s\n", hipGetErrorString(stale));
+    if (stale != hipSuccess && getenv("DSCE_DEBUG"))
+        fprintf(stderr, "dsce: clearing a stale HIP error at entry: %s\n", hipGetErrorString(stale));
 }
 
 Scheme& get_scheme(dsce_ctx* c, int id) {
@@ -636,6 +639,17 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
         s.k.row_pval = dupload(c, row_pval);
         s.k.p_diag = diag ? 1 : 0;
         {
+            bool uni = diag, first = true;
+            double2 pv0 = make_double2(0.0, 0.0);
+            for (int r = 0; r < LK && uni; ++r) {
+                if (row_data[r] < 0) continue;
+                if (first) pv0 = row_pval[r], first = false;
+                else if (row_pval[r].x != pv0.x || row_pval[r].y != pv0.y) uni = false;
+            }
+            s.k.pv_uni = uni && !first ? 1 : 0;
+            s.k.pv_data = pv0;
+        }
+        {
             std::vector<int> seen((size_t)NP + s.d.n_data, 0);
             for (int r = 0; r < LK; ++r)
                 if (row_pcol[r] >= 0 && row_pcol[r] < NP + s.d.n_data) ++seen[row_pcol[r]];
@@ -825,12 +839,15 @@ void upload_interp(dsce_ctx* c, Scheme& s) {
 // Bz is fitted here to the Bv the guard above checked (least squares over every
 // FFT-window sample, long-double QR of the MIC_NB columns of T) and kept only if
 // the fit reproduces Bv to rounding in every (variant, SNR) slice:
-// max |Bv - T Bz| <= max(1e-13, LR_EPS kappa(R)) max |Bv| with kappa(R) =
+// max |Bv - T Bz| <= min(MIC_RTOL_MAX, max(1e-13, LR_EPS kappa(R))) max |Bv| with kappa(R) =
 // ||R||_1 ||pinv(R)||_1 — the GPU's Bv = m pinv(R) itself carries rounding of
 // that order (the oracle's C2 fit: 8.6e-15 at cond 1.1e2 up to 7.2e-12 at
 // cond 1.2e5, tests/test_lowrank.py), while a geometry without the structure
 // misses by orders of magnitude.
 static constexpr double LR_EPS = 4e-16;
+// the structured-OFDM guards' per-slice bars (build_mic, build_mic_lr): at least
+// MIC_RTOL, at most MIC_RTOL_MAX, relative to max|W| / max|Bv|
+static constexpr double MIC_RTOL = 1e-11, MIC_RTOL_MAX = 1e-9;
 // max(column, row) 1-norm of an NP x NP complex matrix (its condition estimate
 // kappa(R) = ||R||_1 ||pinv(R)||_1 sets the rounding bars of build_mic / build_mic_lr)
 double norm1(const double2* m, int NP) {
@@ -893,7 +910,9 @@ void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<
     double worst = 0.0, rel = 0.0;
     for (int sl = 0; sl < nsl; ++sl) {
         const double kap = norm1(slice_R(s, c->nsnr, sl), NP) * norm1(ri.data() + (size_t)sl * NP * NP, NP);
-        const double tol = std::max(1e-13, LR_EPS * kap);
+        // capped like build_mic's bar: a badly conditioned slice cannot
+        // admit a fit above the rounding level the structured IC guard enforces
+        const double tol = std::min(MIC_RTOL_MAX, std::max(1e-13, LR_EPS * kap));
         double mx = 0.0, dev = 0.0;
         for (int q = 0; q < nt; ++q)
             for (int p = 0; p < NP; ++p) {
@@ -952,7 +971,6 @@ void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<
     s.Ts = dupload(c, ts);
 }
 
-static constexpr double MIC_RTOL = 1e-11, MIC_RTOL_MAX = 1e-9;
 void build_mic(dsce_ctx* c, Scheme& s, const SetupArgs& a, const double2* m, const double2* rinv) {
     const int NP = s.d.n_pilots, LK = s.LK, N = s.N, nsl = 2 * c->nsnr, nt = c->ch.ntap;
     const int nblk = s.k.QH.nblk;
@@ -1581,8 +1599,12 @@ int api_fail(dsce_ctx* c, int code, const std::string& msg) {
     return code;
 }
 
+// API_END: every entry point that launched work returns the launch errors it
+// left (check_ctx clears stale errors at entry, so an error not
+// checked before returning would otherwise be lost)
 #define API_BEGIN try {
 #define API_END                                                 \
+    DSCE_HIP_CHECK(hipGetLastError());                          \
     }                                                           \
     catch (const ApiError& e) { return api_fail(ctx, e.code, e.what()); } \
     catch (const HipError& e) { return api_fail(ctx, DSCE_EHIP, e.what()); } \
@@ -1723,11 +1745,12 @@ int dsce_create(int hip_device, dsce_ctx** out) {
     return DSCE_OK;
 }
 
-void dsce_destroy(dsce_ctx* ctx) {
-    if (!ctx) return;
-    // Teardown cannot fail the caller, but a failing call is reported (stderr)
-    // and its error cleared, so it does not surface in the next context's
-    // hipGetLastError (r04: a stale 'invalid argument' met a later build_mmse).
+int dsce_destroy(dsce_ctx* ctx) {
+    if (!ctx) return DSCE_OK;
+    // The context is freed whatever happens; a failing call is named (stderr),
+    // its error cleared, so it does not surface in the next context's
+    // hipGetLastError (r04: a stale 'invalid argument' met a later build_mmse),
+    // and returned as DSCE_EHIP (ABI 6: the r04 double free was only printed).
     const char* first = nullptr;
     hipError_t ferr = hipSuccess;
     auto note = [&](hipError_t e, const char* what) {
@@ -1749,6 +1772,7 @@ void dsce_destroy(dsce_ctx* ctx) {
     delete ctx;
     if (first) fprintf(stderr, "dsce_destroy: %s failed: %s\n", first, hipGetErrorString(ferr));
     (void)hipGetLastError();
+    return first ? DSCE_EHIP : DSCE_OK;
 }
 
 const char* dsce_last_error(const dsce_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }

@@ -45,15 +45,22 @@ __device__ __forceinline__ void c_fma(double2& acc, double2 a, double2 b) {
 // ---------------------------------------------------------------------------
 enum { STREAM_THETA = 1, STREAM_PHI = 2, STREAM_BITS = 3, STREAM_PILOTS = 4, STREAM_NOISE = 5 };
 
-__host__ __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                                        uint32_t k0, uint32_t k1) {
+// a ^ b ^ c in one v_bitop3_b32 (gfx950; truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// rounds R0..9 of Philox4x32-10 on the state (c0..c3) with the round-R0 keys
+template <int R0 = 0>
+__device__ __forceinline__ uint4 philox_rounds(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                               uint32_t k1) {
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = R0; r < 10; ++r) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
         uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        uint32_t n0 = xor3(hi1, c1, k0), n2 = xor3(hi0, c3, k1);
         c0 = n0;
         c1 = lo1;
         c2 = n2;
@@ -64,13 +71,35 @@ __host__ __device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1
     return make_uint4(c0, c1, c2, c3);
 }
 
-__host__ __device__ __forceinline__ uint4 stream_block(uint64_t seed, uint64_t rep, uint32_t stream, uint32_t sub,
-                                                       uint32_t idx) {
+__device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                               uint32_t k0, uint32_t k1) {
+    return philox_rounds<0>(c0, c1, c2, c3, k0, k1);
+}
+
+__device__ __forceinline__ uint4 stream_block(uint64_t seed, uint64_t rep, uint32_t stream, uint32_t sub,
+                                              uint32_t idx) {
     return philox4x32_10(idx, (uint32_t)rep, (uint32_t)(rep >> 32), ((stream & 0xFFFFu) << 16) | (sub & 0xFFFFu),
                          (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-__host__ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
+// stream_block of many sub-streams of one (seed, rep, stream, idx) (k_txrx_fft:
+// the SNR points): the first round does not depend on the sub-stream except
+// through one XOR (c2' = hi(M0 idx) ^ c3 ^ k0'), so its two products are formed
+// once (pre) and each block costs nine rounds
+struct PhiloxSub {
+    uint32_t n0, lo1, hk, lo0, k0, k1;
+};
+__device__ __forceinline__ PhiloxSub stream_pre(uint64_t seed, uint64_t rep, uint32_t idx) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * idx, p1 = (uint64_t)0xCD9E8D57u * (uint32_t)(rep >> 32);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    return PhiloxSub{xor3((uint32_t)(p1 >> 32), (uint32_t)rep, k0), (uint32_t)p1, (uint32_t)(p0 >> 32) ^ k1,
+                     (uint32_t)p0, k0 + 0x9E3779B9u, k1 + 0xBB67AE85u};
+}
+__device__ __forceinline__ uint4 stream_sub(const PhiloxSub& p, uint32_t stream, uint32_t sub) {
+    return philox_rounds<1>(p.n0, p.lo1, p.hk ^ (((stream & 0xFFFFu) << 16) | (sub & 0xFFFFu)), p.lo0, p.k0, p.k1);
+}
+
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 
@@ -151,6 +180,11 @@ struct SchemeK {
     const int* row_pcol;          // LK
     const double2* row_pval;      // LK
     int p_diag;
+    // p_diag and every data row carries the same precoder value pv_data (r05:
+    // the chain kernels stage the constellation pre-multiplied by it, so the
+    // re-precoded decision is one LDS read instead of a complex product per row)
+    int pv_uni;
+    double2 pv_data;
     // p_diag and every pilot / data column sits on exactly one row: the TX
     // symbols can be drawn row by row in parallel (k_tx_rows)
     int tx_rows;

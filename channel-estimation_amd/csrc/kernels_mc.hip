@@ -13,6 +13,7 @@
 // round exactly like the NumPy oracle; explicit fma() is used where fusion is
 // wanted (matvec inner loops).
 #include "dsce_kernels.h"
+#include "bm_tables.h"
 
 #include <math.h>
 #include <algorithm>
@@ -613,11 +614,99 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
 // u2 = u53(w2,w3), (re, im) = sqrt(-2 log(1-u1)) (cos, sin)(2 pi u2).
-__device__ __forceinline__ double2 normal_pair(uint4 w) {
-    const double u1 = u53(w.x, w.y), u2 = u53(w.z, w.w);
-    const double rad = sqrt(-2.0 * log(1.0 - u1));
-    const double2 cz = cis_turns(u2);                         // u2 in [0, 1)
+//
+// r05: table-driven, ~48 FP64 instructions per pair instead of
+// ~118 (the library log alone was 68, a double-double evaluation: 43 v_add_f64).
+// Same spec, same uniforms; the pair differs from the NumPy oracle's
+// np.log / np.sqrt / np.cos / np.sin evaluation by a few units in the last
+// place (tests/test_bm_tables.py restates the algorithm and bounds it;
+// test_gpu_doubly_flat.py::test_device_normals_match_oracle on the box).
+// Tables: csrc/bm_tables.h (tools/gen_bm_tables.py).
+//
+// x = 1 - u1 exactly (a multiple of 2^-53 in (0, 1], built by two exact FMAs
+// from the 27 + 26 bits), always a normal double.
+__device__ __forceinline__ double one_minus_u53(uint32_t a, uint32_t b) {
+    return fma(-(double)(a >> 5), 0x1p-27, fma(-(double)(b >> 6), 0x1p-53, 1.0));
+}
+
+// -2 log x for x in (0, 1]: x = m 2^(E - 1022), m in [1/2, 1) taken from the bit
+// pattern (three integer ops, no frexp); interval i = top 7 bits of m with
+// lt[i] = (invc, 2 log invc); r = m invc - 1, |r| <= 2^-7 (2^-8 except at the
+// interval of m = 1/2); -2 log1p(r) = -2 r + r^2 P(r) with the Taylor terms to
+// r^7 (truncation < 2e-18).  For x in [1/2, 1) there is no ln 2 term, so the
+// result's only rounding is the table value's (of the result's size); x -> 1
+// lands in the interval whose centre is 1 (invc = 1, table value 0): full
+// relative precision; x = 1 (E - 1022 = 1, invc = 2) gives exactly 0.
+__device__ __forceinline__ double m2log_unit(double x, const double2* __restrict__ lt) {
+    const int hi = __double2hiint(x);
+    const double m = __hiloint2double((hi & 0x000FFFFF) | 0x3FE00000, __double2loint(x));
+    const double2 t = lt[(hi >> 13) & 127];
+    const double ed = (double)((hi >> 20) - 1022);           // E - 1022 (x > 0: no sign bit)
+    const double r = fma(m, t.x, -1.0);
+    double p = -2.0 / 7.0;
+    p = fma(p, r, 1.0 / 3.0);
+    p = fma(p, r, -2.0 / 5.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, -2.0 / 3.0);
+    p = fma(p, r, 1.0);
+    const double s1 = fma(ed, -1.3862943611198906, t.y);      // -2 ln 2
+    return s1 + fma(r, -2.0, (r * r) * p);
+}
+
+// sqrt(a) for 0 <= a < 2^1000 (a = 0 -> ~1e-150): v_rsq_f64 and the Newton
+// steps of the library sqrt without its range scaling (a is never denormal)
+__device__ __forceinline__ double sqrt_bm(double a) {
+    a = fmax(a, 1e-300);
+    const double y = __builtin_amdgcn_rsq(a);
+    double g = a * y, h = 0.5 * y;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, a);
+    g = fma(d, h, g);
+    d = fma(-g, g, a);
+    return fma(d, h, g);
+}
+
+// (cos, sin)(2 pi u2), u2 = u53(a, b): interval j = top 8 bits of u2, ct[j] =
+// cis(2 pi (j + 1/2) / 256), theta = 2 pi (u2 - (j + 1/2) / 256) in
+// [-pi/256, pi/256) from the remaining 19 + 26 bits; sin to theta^5, cos - 1 to
+// theta^6 (truncation < 1e-17), then ct[j] (1 + (cos - 1) + i sin).
+__device__ __forceinline__ double2 cis_u53(uint32_t a, uint32_t b, const double2* __restrict__ ct) {
+    const double2 t = ct[a >> 24];
+    const double th = fma((double)((a >> 5) & 0x7FFFFu), 0x1p-27 * 6.283185307179586,
+                          fma((double)(b >> 6), 0x1p-53 * 6.283185307179586, -0.012271846303085130));
+    const double t2 = th * th;
+    const double s = fma(th * t2, fma(t2, 1.0 / 120.0, -1.0 / 6.0), th);
+    const double cm1 = t2 * fma(fma(t2, -1.0 / 720.0, 1.0 / 24.0), t2, -0.5);
+    return make_double2(fma(t.x, cm1, fma(-t.y, s, t.x)), fma(t.y, cm1, fma(t.x, s, t.y)));
+}
+
+// The pair's radius and angle; lt / ct: the tables (LDS copies in k_txrx_fft,
+// the __constant__ originals elsewhere: the same values, the same draws).
+__device__ __forceinline__ void bm_parts(uint4 w, const double2* __restrict__ lt, const double2* __restrict__ ct,
+                                         double& rad, double2& cz) {
+    rad = sqrt_bm(m2log_unit(one_minus_u53(w.x, w.y), lt));
+    cz = cis_u53(w.z, w.w, ct);
+}
+
+__device__ __forceinline__ double2 normal_pair(uint4 w, const double2* __restrict__ lt = kLogT,
+                                               const double2* __restrict__ ct = kCisT) {
+    double rad;
+    double2 cz;
+    bm_parts(w, lt, ct, rad, cz);
     return make_double2(rad * cz.x, rad * cz.y);
+}
+
+// r0 + sc z of one noise sample (every AWGN path: k_noise, LoadNoisy,
+// k_txrx_fft — one expression, so the fused and unfused paths draw the same bits)
+__device__ __forceinline__ double2 noise_add(double2 r0, double sc, uint4 w, const double2* __restrict__ lt = kLogT,
+                                             const double2* __restrict__ ct = kCisT) {
+    double rad;
+    double2 cz;
+    bm_parts(w, lt, ct, rad, cz);
+    const double rs = sc * rad;
+    return make_double2(fma(rs, cz.x, r0.x), fma(rs, cz.y, r0.y));
 }
 
 // ---------------------------------------------------------------------------
@@ -978,6 +1067,8 @@ struct StorePerfectDetect {
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
     int skip;                          // k_pic_fft: stop at the IC's fixed point (Opts::pic_skip)
+    int pv_uni;                        // chain kernels: SchemeK::pv_uni (reprecode6 / stage_sym)
+    double pv_re, pv_im;
     double2* sym;
     SlicerLds* slt;
     int c0, c1;
@@ -1243,9 +1334,8 @@ __global__ void __launch_bounds__(64) k_noise(int N, int R, int U, int snr0, int
     const double sc = sqrt(pn[snr] / 2.0);
     const int n0 = blockIdx.y * 64;
     for (int n = n0; n < n0 + 64 && n < N; ++n) {
-        const double2 z = normal_pair(stream_block(seed, rep, STREAM_NOISE, (uint32_t)(base + snr + 256 * slot), (uint32_t)n));
-        const double2 r = r0[(size_t)n * R + rl];
-        rbuf[(size_t)n * U + unit] = make_double2(r.x + sc * z.x, r.y + sc * z.y);
+        const uint4 w = stream_block(seed, rep, STREAM_NOISE, (uint32_t)(base + snr + 256 * slot), (uint32_t)n);
+        rbuf[(size_t)n * U + unit] = noise_add(r0[(size_t)n * R + rl], sc, w);
     }
 }
 
@@ -1262,10 +1352,9 @@ struct LoadNoisy {
     __device__ __forceinline__ Regs load(int n, int lane) const {
         const int snr = snr0 + lane / R, rl = lane % R;
         const double sc = sqrt(pn[snr] / 2.0);
-        const double2 z = normal_pair(stream_block(seed, rep0 + (uint64_t)rl, STREAM_NOISE,
-                                                   (uint32_t)(base + snr + 256 * slot), (uint32_t)n));
-        const double2 r = r0[(size_t)n * R + rl];
-        return make_double2(r.x + sc * z.x, r.y + sc * z.y);
+        const uint4 w = stream_block(seed, rep0 + (uint64_t)rl, STREAM_NOISE, (uint32_t)(base + snr + 256 * slot),
+                                     (uint32_t)n);
+        return noise_add(r0[(size_t)n * R + rl], sc, w);
     }
     __device__ __forceinline__ double2 combine(const Regs& r) const { return r; }
 };
@@ -1322,6 +1411,85 @@ __device__ __forceinline__ int nearest_lin(double x, double scale, double offset
     asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(t), "v"((int)top));
     tie = f == (double)c ? 1 : 0;                        // on the mid-point below level c
     return c;
+}
+
+// The folded slicer of the chain kernels for the lane's six rows (r05): f = z
+// scale + offset per component (nearest_lin's), nearest grid indices by
+// truncation + clamp, symbol from the LDS grid.  An exact mid-point needs f to
+// be an integer below 2^20, so the low word of f is zero: that one integer
+// compare per component flags the (measure-zero) candidates, and the exact test
+// f == (double)c with the first-minimum rule of SignalConstellation.m:88 runs
+// only in the rare branch it takes (r04: a conversion back and an FP64 compare
+// per component and row, 24 FP64 instructions per six rows).
+__device__ __forceinline__ int nearest_idx(double f, double top) {
+    int t, c;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(t) : "v"(f));
+    asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(t), "v"((int)top));
+    return c;
+}
+__device__ __forceinline__ void slice6(int (&dp)[6], const double (&fI)[6], const double (&fQ)[6], double topI,
+                                       double topQ, int nQ, const int* sgrid) {
+    int code[6];
+    bool cand = false;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const int iI = nearest_idx(fI[a], topI), iQ = nearest_idx(fQ[a], topQ);
+        code[a] = iI | (iQ << 8);
+        cand |= (__double2loint(fI[a]) == 0) | (__double2loint(fQ[a]) == 0);
+        dp[a] = sgrid[__umul24(iI, nQ) + iQ];
+    }
+    if (__ballot(cand)) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            // opaque copies: the exact test stays inside the rare branch (if-
+            // converted, the compiler evaluated it for every row)
+            double gI = fI[a], gQ = fQ[a];
+            asm volatile("" : "+v"(gI), "+v"(gQ));
+            const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
+            const int jI = max(iI - (gI == (double)iI ? 1 : 0), 0), jQ = max(iQ - (gQ == (double)iQ ? 1 : 0), 0);
+            dp[a] = min(min(sgrid[iI * nQ + iQ], sgrid[jI * nQ + iQ]), min(sgrid[iI * nQ + jQ], sgrid[jI * nQ + jQ]));
+        }
+    }
+}
+
+// u of the lane's data rows <- the re-precoded decisions P [.; x_hat] (row-local
+// P): the row's precoder value times the decided symbol.  pv_uni (SchemeK): every
+// data row has the same value and the staged constellation (stage_sym) already
+// carries it, so the product is one LDS read (a uniform branch).
+__device__ __forceinline__ void reprecode6(double2 (&u)[6], const int (&dp)[6], unsigned dmask, const double2* rpv, int r,
+                                           const double2* sym, int pv_uni) {
+    if (pv_uni) {
+        // every row reads its entry (dp is a valid index on every row): without the
+        // opaque copy the compiler turned each select into a per-row branch around
+        // the LDS read, each with its own wait (DESIGN.md lesson 4)
+        double2 nv[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) nv[a] = sym[dp[a]];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            asm volatile("" : "+v"(nv[a].x), "+v"(nv[a].y));
+            const bool data = (dmask >> a) & 1;
+            u[a].x = data ? nv[a].x : u[a].x;
+            u[a].y = data ? nv[a].y : u[a].y;
+        }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            const bool data = (dmask >> a) & 1;
+            double2 nv = make_double2(0.0, 0.0);
+            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
+            u[a].x = data ? nv.x : u[a].x;
+            u[a].y = data ? nv.y : u[a].y;
+        }
+    }
+}
+// constellation entry i as staged for reprecode6: times the common data-row
+// precoder value when pv_uni (the very product reprecode6 forms otherwise)
+__device__ __forceinline__ double2 stage_sym(double2 a, int pv_uni, double pvr, double pvi) {
+    if (!pv_uni) return a;
+    double2 nv = make_double2(0.0, 0.0);
+    c_fma(nv, make_double2(pvr, pvi), a);
+    return nv;
 }
 
 // Error counts of a 256-thread block, one atomic per counter per block: every
@@ -1382,16 +1550,16 @@ __device__ __forceinline__ double2 cmul_const(double2 x, double c, double s) {
     return make_double2(fma(x.x, c, -(S * s) * x.y), fma(x.y, c, (S * s) * x.x));
 }
 
-// DFT-3 with sign S (S = +1: sum x[n] e^{+2 pi i nk/3})
+// DFT-3 with sign S (S = +1: sum x[n] e^{+2 pi i nk/3}); the +-i H (b - c)
+// rotation fused into the output FMAs (12 FP64 ops)
 template <int S>
 __device__ __forceinline__ void dft3(double2& a, double2& b, double2& c) {
     constexpr double H = 0.86602540378443865;           // sin(60 deg)
     const double2 t = c_add(b, c), d = c_sub(b, c);
     const double2 m = make_double2(fma(-0.5, t.x, a.x), fma(-0.5, t.y, a.y));
-    const double2 r = make_double2((-S * H) * d.y, (S * H) * d.x);   // S i H (b - c)
     a = c_add(a, t);
-    b = c_add(m, r);
-    c = c_sub(m, r);
+    b = make_double2(fma(-S * H, d.y, m.x), fma(S * H, d.x, m.y));   // m + S i H d
+    c = make_double2(fma(S * H, d.y, m.x), fma(-S * H, d.x, m.y));   // m - S i H d
 }
 
 // a * b with two FMAs (2 mul + 2 fma instead of 4 mul + 2 add under -ffp-contract=off)
@@ -1429,23 +1597,25 @@ __device__ __forceinline__ double2 bperm_c(int addr, double2 v) {
                                          __builtin_amdgcn_ds_bpermute(addr, __double2loint(v.y))));
 }
 
-// position of output k of dft6 in the array (k = k1 + 3 k2 lands at k2 + 2 k1)
-__host__ __device__ constexpr int p6(int k) { return k / 3 + 2 * (k % 3); }
+// position of output k of dft6 in the array: X[k] lands at x[-k mod 6]
+__host__ __device__ constexpr int p6(int k) { return (6 - k) % 6; }
 
-// DFT-6 with sign S in place, natural-order input, output k at x[p6(k)]:
-// n = 2 n1 + n2, k = k1 + 3 k2; DFT-3 over n1, twiddle w6^(S n2 k1), DFT-2 over n2
+// DFT-6 with sign S in place, natural-order input, output k at x[p6(k)]
+// (r05): Good-Thomas prime-factor form, 6 = 2 x 3 coprime, so no twiddles:
+// n = 3 n1 + 2 n2, k = 3 k1 + 4 k2 (mod 6); DFT-3 over n2 of (x0, x2, x4) and
+// (x3, x5, x1), then DFT-2 over n1: 36 FP64 ops instead of 48 (r04: DFT-3 x 2,
+// twiddles w6^1 / w6^2, DFT-2 x 3)
 template <int S>
 __device__ __forceinline__ void dft6(double2 (&x)[6]) {
-    constexpr double C60 = 0.86602540378443865;
     dft3<S>(x[0], x[2], x[4]);
-    dft3<S>(x[1], x[3], x[5]);
-    x[3] = cmul_const<S>(x[3], 0.5, C60);                // w6^1
-    x[5] = cmul_const<S>(x[5], -0.5, C60);               // w6^2
+    dft3<S>(x[3], x[5], x[1]);
+    // pairs (A0[k2], A1[k2]) = (x0, x3), (x2, x5), (x4, x1) -> X[4 k2], X[4 k2 + 3]
 #pragma unroll
-    for (int k1 = 0; k1 < 3; ++k1) {
-        const double2 a = x[2 * k1], b = x[2 * k1 + 1];
-        x[2 * k1] = c_add(a, b);
-        x[2 * k1 + 1] = c_sub(a, b);
+    for (int k2 = 0; k2 < 3; ++k2) {
+        const int i0 = 2 * k2, i1 = (2 * k2 + 3) % 6;
+        const double2 a = x[i0], b = x[i1];
+        x[i0] = c_add(a, b);
+        x[i1] = c_sub(a, b);
     }
 }
 
@@ -1525,7 +1695,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         for (int m = 0; m < 6; ++m)
 #pragma unroll
             for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
-        sym[tid] = make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0);
+        sym[tid] = stage_sym(make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
         sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
         // unconditional (clamped) table writes: a write under `if (tid < 24)`
         // lets the compiler sink the table loads into the branch, behind a
@@ -1570,42 +1740,27 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     bool have = S0, conv = false;
     if (S0) {
         // stage 0: y / h and 1 / h now, one-tap z = y / h, slicer, counts, decisions
-        int code[6], dp[6];
-        int anytie = 0;
+        int dp[6];
+        double fI[6], fQ[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double2 hh = hc[a], yv = yh[a];
             const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
             hc[a] = make_double2(hh.x * id, -hh.y * id);
             yh[a] = c_mulf(yv, hc[a]);
-            int tI, tQ;
-            const int iI = nearest_lin(yh[a].x, o.scI, o.ofI, o.topI, tI);
-            const int iQ = nearest_lin(yh[a].y, o.scQ, o.ofQ, o.topQ, tQ);
-            code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
-            anytie |= tI | tQ;
-            dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+            fI[a] = fma(yh[a].x, o.scI, o.ofI);
+            fQ[a] = fma(yh[a].y, o.scQ, o.ofQ);
         }
-        if (__ballot(anytie)) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
-                const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
-                dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
-                            min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
-            }
-        }
+        slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
             const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
             ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)(rdc[4 * a + r] >> 1)] = dp[a];
-            double2 nv = make_double2(0.0, 0.0);
-            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
-            u[a].x = data ? nv.x : u[a].x;
-            u[a].y = data ? nv.y : u[a].y;
             pk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
+        reprecode6(u, dp, dmask, rpv, r, sym, o.pv_uni);
         cntl[w][0] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);
         ncnt = 0;
     }
@@ -1682,20 +1837,16 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             }
         // epilogue per row 4a + r: z = y / h - acc / h + u, slicer, counts,
         // re-precoded decision into u
-        int code[6], dp[6];
+        int dp[6];
         unsigned npk[2] = {0u, 0u};
-        int anytie = 0;
+        double fI[6], fQ[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double2 ah = c_mulf(x[p6(a)], hc[a]);
             const double zx = (yh[a].x - ah.x) + u[a].x;
             const double zy = (yh[a].y - ah.y) + u[a].y;
-            int tI, tQ;
-            const int iI = nearest_lin(zx, o.scI, o.ofI, o.topI, tI);
-            const int iQ = nearest_lin(zy, o.scQ, o.ofQ, o.topQ, tQ);
-            code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
-            anytie |= tI | tQ;
-            dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+            fI[a] = fma(zx, o.scI, o.ofI);
+            fQ[a] = fma(zy, o.scQ, o.ofQ);
             if (TRACE && ((dmask >> a) & 1) && unit == o.tr->unit) {
                 const int row = row0 + 4 * a + r;
                 const double2 yv = o.y[(size_t)row * U + unit], hh = o.h[(size_t)row * R + rl];
@@ -1703,28 +1854,17 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             }
         }
         // a decision exactly on a mid-point (measure zero): the smallest symbol
-        // index among the tied grid points (one uniform branch)
-        if (__ballot(anytie)) {
-#pragma unroll
-            for (int a = 0; a < 6; ++a) {
-                const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
-                const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
-                dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
-                            min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
-            }
-        }
+        // index among the tied grid points (one uniform branch inside)
+        slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
             const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
             ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)it * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
-            double2 nv = make_double2(0.0, 0.0);
-            c_fma(nv, rpv[4 * a + r], sym[dp[a]]);
-            u[a].x = data ? nv.x : u[a].x;
-            u[a].y = data ? nv.y : u[a].y;
             npk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
+        reprecode6(u, dp, dmask, rpv, r, sym, o.pv_uni);
         cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
         const bool same = have && npk[0] == pk[0] && npk[1] == pk[1];
@@ -1934,27 +2074,14 @@ struct Mic2Tables {
 // the decided symbol indices (first-minimum tie rule, SignalConstellation.m:88)
 __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6], const double2 (&hd)[6],
                                            const StorePerfectDetect& o, const int* sgrid) {
-    int code[6];
-    int anytie = 0;
+    double fI[6], fQ[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const double2 z = c_div_fast(ye[a], hd[a]);
-        int tI, tQ;
-        const int iI = nearest_lin(z.x, o.scI, o.ofI, o.topI, tI);
-        const int iQ = nearest_lin(z.y, o.scQ, o.ofQ, o.topQ, tQ);
-        code[a] = iI | (iQ << 8) | (tI << 16) | (tQ << 17);
-        anytie |= tI | tQ;
-        dp[a] = sgrid[__umul24(iI, o.nQ) + iQ];
+        fI[a] = fma(z.x, o.scI, o.ofI);
+        fQ[a] = fma(z.y, o.scQ, o.ofQ);
     }
-    if (__ballot(anytie)) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-            const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
-            const int jI = max(iI - ((code[a] >> 16) & 1), 0), jQ = max(iQ - ((code[a] >> 17) & 1), 0);
-            dp[a] = min(min(sgrid[iI * o.nQ + iQ], sgrid[jI * o.nQ + iQ]),
-                        min(sgrid[iI * o.nQ + jQ], sgrid[jI * o.nQ + jQ]));
-        }
-    }
+    slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
 }
 
 // Stages 0..niter of the MMSE branch for one symbol of a unit (the common body of
@@ -2185,10 +2312,6 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             const bool data = (dmask >> a) & 1;
             const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
             ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
-            double2 nv = make_double2(0.0, 0.0);
-            c_fma(nv, rpv[4 * a + r], tb.sym[dp[a]]);
-            v[a].x = data ? nv.x : v[a].x;
-            v[a].y = data ? nv.y : v[a].y;
             if (TRACE && unit == o.tr->unit) {
                 const int row = row0 + 4 * a + r;
                 o.tr->yest[(size_t)s * o.tr->LK + row] = ye[a];
@@ -2196,6 +2319,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 if (data) o.tr->dec_e[(size_t)s * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
             }
         }
+        reprecode6(v, dp, dmask, rpv, r, tb.sym, o.pv_uni);
         cntl[s] = wave_sum_dpp(valid ? ncnt : 0);  // uniform: every lane writes the same word
         if (!LR && !PIL && s < ma.niter) {
             // stage s + 1's operands: hP_s (tap GEMM) and hP_{s+1} (diag)
@@ -2222,7 +2346,7 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
     for (int i = tid; i < 256; i += nth) {
         const double2 a = o.symbols[min(i, o.M - 1)];
         const int g = o.grid_sym[min(i, o.nI * o.nQ - 1)];
-        tb.sym[i] = make_double2(i < o.M ? a.x : 0.0, i < o.M ? a.y : 0.0);
+        tb.sym[i] = stage_sym(make_double2(i < o.M ? a.x : 0.0, i < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
         tb.sgrid[i] = i < o.nI * o.nQ ? g : 0;
     }
     if (tid < 48) {
@@ -2347,11 +2471,13 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     const int rl = unit % R;
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
     if constexpr (LR) {
+        // the load clamped and issued first; only the threads with an entry store
+        // (156 threads re-stored entry 99)
         const int i = min(tid, MIC_NB * 25 - 1);
         const double t = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
         mic2_tables(tb, o, tid, 256);
         mic2_rows(rpv, rdc, rpc, wrow, sk, o, row0, tid);
-        twd[i] = t;
+        if (tid < MIC_NB * 25) twd[tid] = t;
     } else {
         // every global load before the first LDS write (clamped, unconditional)
         constexpr int NBV = 2 * NT * 24 * NP, PER = (NBV + 255) / 256;
@@ -2428,6 +2554,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     __shared__ double2 twa[2][4][6];
     __shared__ double2 wrow[24];
     __shared__ double ssc[TXRX_MAXSNR];                        // sqrt(Pn / 2) of the chunk's SNR points
+    __shared__ double2 slt[128], sct[256];                     // the Box-Muller tables (bm_tables.h)
     const double2 gs = sk.pf_gs, qs = sk.pf_qs, ps = sk.pf_scale;
     double2 x[6], taps[6][NT];
     {
@@ -2441,6 +2568,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         const double2 t0 = kW24[lr0 % 12];
         const int kc = min(tid, ta.nchunk - 1);
         const double pnv = ta.pn[ta.snr0 + kc];
+        const double2 cv = kCisT[tid], lv = kLogT[tid & 127];
 #pragma unroll
         for (int a = 0; a < 6; ++a) x[a] = ta.xs[(size_t)(row0 + 4 * a + r) * R + rl];
 #pragma unroll
@@ -2453,6 +2581,8 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
         wrow[lr0] = c_mul(ps, make_double2(wl.x, -wl.y));
         ssc[kc] = sqrt(pnv / 2.0);
+        sct[tid] = cv;
+        slt[tid & 127] = lv;
     }
     __syncthreads();
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
@@ -2503,17 +2633,19 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
             r0[m] = acc;
         }
     }
-    // per SNR point: r = r0 + noise (LoadNoisy's draws), y = qs DFT24(r)
+    // per SNR point: r = r0 + noise (LoadNoisy's draws), y = qs DFT24(r); the
+    // first Philox round of every sample is SNR-independent (stream_pre)
+    PhiloxSub phs[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) phs[m] = stream_pre(ta.seed, ta.rep0 + (uint64_t)rl, (uint32_t)(klo + 6 * cq + m));
     for (int k = 0; k < ta.nchunk; ++k) {
         const int snr = ta.snr0 + k;
         const double sc = ssc[k];
         double2 f[6];
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
-            const double2 z = normal_pair(stream_block(ta.seed, ta.rep0 + (uint64_t)rl, STREAM_NOISE,
-                                                       (uint32_t)(ta.base + snr + 256 * ta.slot),
-                                                       (uint32_t)(klo + 6 * cq + m)));
-            const double2 rv = make_double2(r0[m].x + sc * z.x, r0[m].y + sc * z.y);
+            const uint4 wr = stream_sub(phs[m], STREAM_NOISE, (uint32_t)(ta.base + snr + 256 * ta.slot));
+            const double2 rv = noise_add(r0[m], sc, wr, slt, sct);
             const double2 pv = dpp_c<QP_XOR1>(rv);
             double2 g = make_double2(fma(sg2, rv.x, pv.x), fma(sg2, rv.y, pv.y));
             g = quad_tw<-1>(g, r == 3);
@@ -2654,6 +2786,9 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.topQ = sk.nQ - 1;
     o.pf_scale_re = sk.pf_scale.x;
     o.pf_scale_im = sk.pf_scale.y;
+    o.pv_uni = sk.pv_uni;
+    o.pv_re = sk.pv_data.x;
+    o.pv_im = sk.pv_data.y;
     return o;
 }
 

@@ -26,7 +26,7 @@ EXPORTED = [
     "dsce_kernel_work", "dsce_structured_check",
 ]
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # dsce_path_info bits (include/dsce.h DSCE_PATH_*)
 PATH_BITS = {
@@ -95,7 +95,7 @@ def load_library(path=None):
     lib.dsce_device_count.argtypes = [C.POINTER(C.c_int)]
     lib.dsce_create.argtypes = [C.c_int, C.POINTER(vp)]
     lib.dsce_destroy.argtypes = [vp]
-    lib.dsce_destroy.restype = None
+    lib.dsce_destroy.restype = C.c_int
     lib.dsce_last_error.argtypes = [vp]
     lib.dsce_last_error.restype = C.c_char_p
     lib.dsce_set_channel.argtypes = [vp, C.POINTER(ChannelDesc)]
@@ -128,7 +128,7 @@ def load_library(path=None):
     lib.dsce_structured_check.argtypes = [vp, C.c_int32, dp]
     for name in EXPORTED:
         fn = getattr(lib, name)
-        if name not in ("dsce_destroy", "dsce_last_error"):
+        if name != "dsce_last_error":
             fn.restype = C.c_int
     if path is None:
         _lib = lib
@@ -171,9 +171,13 @@ class Engine:
             raise DsceError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
 
     def close(self):
+        """dsce_destroy; raises DsceError when a HIP call of the teardown failed
+        (ABI 6; the context is freed either way)."""
         if getattr(self, "h", None) is not None and self.h.value:
-            self.lib.dsce_destroy(self.h)
+            rc = self.lib.dsce_destroy(self.h)
             self.h = None
+            if rc != 0:
+                raise DsceError("dsce_destroy failed (%d): a HIP call of the teardown failed (see stderr)" % rc)
 
     def __del__(self):
         try:
@@ -402,7 +406,9 @@ class Engine:
         ratio (kept iff <= 1: the worst slice's deviation over its rounding bar
         min(1e-9, max(1e-11, 4e-16 kappa(R))) max|W|), dev (max |Q' H_hat G - W_thr|),
         wmax (max |W|), rtol (the largest per-slice bar), and the low-rank tap
-        operator's fit residual lr_resid (relative), lr (in use) and lr_ratio."""
+        operator's fit residual lr_resid (relative), lr (built and kept: eligible; a
+        run uses it with options mic_lr = 1 and mic_net bit 0, see path_info's
+        mic_lr) and lr_ratio (capped bar min(1e-9, max(1e-13, 4e-16 kappa(R))))."""
         out = (C.c_double * 7)()
         self._chk(self.lib.dsce_structured_check(self.h, int(sid), out), "dsce_structured_check")
         return dict(ratio=out[0], dev=out[1], wmax=out[2], rtol=out[3], lr_resid=out[4], lr=bool(out[5]),

@@ -44,7 +44,7 @@
  *            on the GPU from the object's Nr / PHY / Implementation / PrototypeFilter properties
  *   dsce_mex('enable_mse', on)                                      % start (and reset) the MSE sums of 'run'
  *   [err, pow] = dsce_mex('get_mse')                                % err [iter+1, snr, scheme], pow [snr, scheme]
- *   c = dsce_mex('structured_check', id)                           % [ratio, max dev, max |W|, rtol, lr fit, lr used, lr ratio]
+ *   c = dsce_mex('structured_check', id)                           % [ratio, max dev, max |W|, rtol, lr fit, lr eligible, lr ratio]
  */
 #ifdef MATLAB_MEX_FILE
 #include <math.h>
@@ -68,8 +68,11 @@
 
 static dsce_ctx* g_ctx = NULL;
 
+/* teardown status (ABI 6): reported as a warning, since cleanup also runs
+ * from mexAtExit where an error cannot be raised */
 static void cleanup(void) {
-    if (g_ctx) dsce_destroy(g_ctx);
+    if (g_ctx && dsce_destroy(g_ctx) != 0)
+        mexWarnMsgIdAndTxt("dsce:teardown", "dsce_destroy: a HIP call of the teardown failed (see stderr)");
     g_ctx = NULL;
 }
 

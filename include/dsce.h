@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 5
+#define DSCE_ABI_VERSION 6
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
@@ -213,7 +213,11 @@ int dsce_abi_version(void);
 int dsce_device_count(int* count);
 
 int dsce_create(int hip_device, dsce_ctx** out);
-void dsce_destroy(dsce_ctx* ctx);
+/* Frees the context (every buffer, event and the stream) and returns DSCE_OK,
+ * or DSCE_EHIP if a HIP call of the teardown failed (the context is freed
+ * either way; the first failing call is named on stderr).  ABI 6: returned
+ * void up to ABI 5 (a double free went unseen). */
+int dsce_destroy(dsce_ctx* ctx);
 const char* dsce_last_error(const dsce_ctx* ctx);
 
 int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* desc);
@@ -371,9 +375,12 @@ int dsce_kernel_work(dsce_ctx* ctx, const char* kernel, double* flops_per_rep, d
  * out[0..2] = -1 when the scheme is not eligible (the W contraction runs).
  * The low-rank form of its tap operator (Bv = T Bz, T_k the J0 kernel summed
  * over pilot symbol k's window; option mic_lr): out[4] = max |Bv - T Bz| /
- * max |Bv| of the fit (-1: not attempted), out[5] = 1 if it is in use, else 0,
- * out[6] = the worst slice's deviation over its rounding bar max(1e-13,
- * 4e-16 ||R||_1 ||pinv(R)||_1) max |Bv| (the operator is used iff <= 1). */
+ * max |Bv| of the fit (-1: not attempted), out[5] = 1 if the operator was
+ * built and kept (eligible), else 0 — a run uses it only with the options
+ * mic_lr = 1 and mic_net bit 0 set, which DSCE_PATH_MIC_LR of dsce_path_info
+ * reports after the run — out[6] = the worst slice's deviation over its rounding
+ * bar min(1e-9, max(1e-13, 4e-16 ||R||_1 ||pinv(R)||_1)) max |Bv| (the operator
+ * is kept iff <= 1). */
 int dsce_structured_check(dsce_ctx* ctx, int32_t scheme_id, double* out7);
 /* Measured FP64 matrix-core peak of the context's GPU: back-to-back
  * v_mfma_f64_16x16x4_f64 on independent accumulators, 8 waves per SIMD,

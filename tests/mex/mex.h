@@ -66,6 +66,7 @@ mxArray* mxCreateNumericArray(mwSize nd, const mwSize* dims, mxClassID cls, mxCo
 void* mxMalloc(size_t n);
 void mxFree(void* p);
 void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...);
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...);
 /* structs and classdef objects (scalar): mxGetProperty returns a copy the
    caller destroys, mxGetField the struct's own field */
 bool mxIsStruct(const mxArray* a);

@@ -166,6 +166,14 @@ void mexErrMsgIdAndTxt(const char* id, const char* fmt, ...) {
     printf("  error %s: %s\n", id, msg);
     longjmp(g_err_jmp, 1);
 }
+void mexWarnMsgIdAndTxt(const char* id, const char* fmt, ...) {
+    va_list ap;
+    char msg[256];
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    printf("  warning %s: %s\n", id, msg);
+}
 int mexAtExit(void (*fn)(void)) { (void)fn; return 0; }
 void mexLock(void) {}
 void mexUnlock(void) {}
@@ -176,7 +184,7 @@ enum { SN = 540, STAPS = 2, SLK = 336, SNP = 16, SND = 320, SSNR = 7, SIT = 4 };
 struct dsce_ctx { int dummy; };
 static struct dsce_ctx g_stub;
 int dsce_create(int dev, dsce_ctx** out) { (void)dev; *out = &g_stub; return 0; }
-void dsce_destroy(dsce_ctx* c) { (void)c; }
+int dsce_destroy(dsce_ctx* c) { (void)c; return 0; }
 const char* dsce_last_error(const dsce_ctx* c) { (void)c; return "stub"; }
 int dsce_scheme_dims(dsce_ctx* c, int32_t id, dsce_dims* d) {
     (void)c;

@@ -43,7 +43,7 @@ def test_simulate_two_ranks_equals_one(tmp_path):
 
 
 def test_simulate_snr_shards_equal_one_rank(tmp_path):
-    """--shard snr: 2 ranks take 2 + 1 of 3 SNR points each with only its own
+    """--shard snr: 2 ranks take 4 + 3 of the 7 SNR points, each with only its own
     estimator (snr_base keys the noise by the sweep's SNR index); counters and
     MSE sums equal the one-rank run exactly.  An odd realisation count
     (64 x 5) is not padded to a multiple of 64 x world."""
@@ -106,3 +106,34 @@ def test_rccl_allreduce_one_rank(tmp_path):
     assert np.array_equal(np.array(a["counts"]), np.array(b["counts"]))
     # the MSE sums are fp64 atomics (their order varies from run to run): rounding level
     np.testing.assert_allclose(np.array(a["nmse"]["ofdm"]), np.array(b["nmse"]["ofdm"]), rtol=1e-12)
+
+
+def test_eight_rank_control_flow_on_one_gpu(tmp_path):
+    """The 8-rank control flow of SURVEY §8e rehearsed on the one-GPU box (8
+    gloo ranks share the device): --shard snr over C2's 7
+    SNR points leaves rank 7 empty, --shard reps splits an odd 520 realisations
+    65 per rank; both equal the one-rank counts and MSE sums.  Then bench.py
+    --gpus 8 launches its own ranks and reports the max-over-ranks time."""
+    args = ["--config", "default", "--schemes", "ofdm", "--reps", "520", "--batch", "128", "--mse"]
+    env = dict(os.environ, DSCE_DIST_BACKEND="gloo", PYTHONPATH=harness.PKG)
+    one = tmp_path / "one.json"
+    subprocess.run([sys.executable, "-m", "dsce.simulate", *args, "--out", str(one)], cwd=harness.PKG, env=env,
+                   check=True, timeout=240, capture_output=True)
+    a = json.load(open(one))
+    assert len(a["snr_db"]) == 7
+    for shard in ("snr", "reps"):
+        out = tmp_path / ("eight_%s.json" % shard)
+        subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "dsce.simulate", *args,
+                        "--shard", shard, "--out", str(out)], cwd=harness.PKG, env=env, check=True, timeout=400,
+                       capture_output=True)
+        b = json.load(open(out))
+        assert b["ranks"] == 8 and b["shard"] == shard and b["n_repetitions"] == 520
+        assert np.array_equal(np.array(a["counts"]), np.array(b["counts"])), shard
+        np.testing.assert_allclose(np.array(a["nmse"]["ofdm"]), np.array(b["nmse"]["ofdm"]), rtol=1e-12)
+    res = subprocess.run([sys.executable, os.path.join(harness.ROOT, "bench.py"), "--gpus", "8", "--steps", "2",
+                          "--warmup", "1", "--reps-per-step", "1024", "--no-cpu-baseline"], env=env, check=True,
+                         timeout=400, capture_output=True, text=True)
+    line = json.loads(res.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 8 and line["config"]["parallelism"] == "dp8"
+    assert line["value"] > 0 and line["steps"] == 2

@@ -2,10 +2,12 @@
 engine's BER curves against the reference's published Figure 3 / Figure 5
 points (dsce/published.py).  No oracle can run at N = 7350 (R_vecH alone has
 324 M non-zeros), so this is a statistical check against the reference's own
-published output: 2048 realisations (about 10 M data bits per SNR point), each
-digitised point within 12 % (digitisation about 3 %, Monte-Carlo spread about
-3 % at the lowest BERs).  The committed 16384-realisation run is
-profiles/r01_paper_ber.json (all points within 0.98-1.06)."""
+published output: 16384 realisations (about 75 M data bits per SNR point), each
+digitised point within 6 % (the r01-r04 gate was 12 % at
+2048 realisations; digitisation about 3 %, Monte-Carlo spread about 1 % at the
+lowest BERs at this size).  The builder's 16384-realisation runs of the same
+seed landed within 0.98-1.06 (profiles/r01_paper_ber.json,
+profiles/r03l_paper_ber.json, results/r04/paper)."""
 import numpy as np
 import pytest
 
@@ -20,12 +22,13 @@ def test_paper_config_ber_matches_published_figures():
     from dsce.engine import build_engine
     S = build_setup("paper", schemes=("fbmc_aux",))
     eng = build_engine(S, batch=1024)
-    reps = 2048
+    reps = 16384
     counts = eng.run(0x5EED0005, 0, reps)
     bits = eng.bits_per_rep(0)
     ber = counts[0] / np.array([bits[0], bits[1]], dtype=float)[None, :, None, None] / reps
     rows = compare(ber, S.snr_db)
-    bad = [r for r in rows if abs(r["ratio"] - 1.0) > 0.12]
+    assert len(rows) >= 30                  # Figure 3 and Figure 5 points
+    bad = [r for r in rows if abs(r["ratio"] - 1.0) > 0.06]
     assert not bad, bad
     # IC gains are monotone in the iteration count at 32 dB (Figure 5)
     k32 = list(S.snr_db).index(32.0)

@@ -59,6 +59,23 @@ def test_jakes_window_kernels_match_oracle(ofdm, mom):
         eng.set_option("jakes_mom", 2)
 
 
+@pytest.mark.parametrize("mom", [2, 1, 0])
+def test_teardown_is_clean_after_window_realisations(mom):
+    """Regression for the r04 double free (fixed in 5b14aa2): dsce_channel_realise
+    with realise_win 1 allocates the Jakes window tables behind its scratch; the
+    scratch is freed by pointer and dsce_destroy (ABI 6: returns a status,
+    Engine.close raises on it) must then free every buffer exactly once.  A run
+    between the realisations puts the batch buffers in the list too."""
+    S = harness.setup("default", schemes=("ofdm",))
+    eng = harness.engine(S, batch=64)
+    eng.set_option("realise_win", 1)
+    eng.set_option("jakes_mom", mom)
+    eng.channel_impulse_response(SEED, 3)
+    eng.run(SEED, 0, 64)
+    eng.channel_impulse_response(SEED, 77)
+    eng.close()          # raises DsceError on a failed teardown call
+
+
 def test_correlation_matrices_match_oracle(ofdm):
     S, eng, mm = ofdm
     rhp, rest, rnoi = eng.correlation(0)

@@ -126,6 +126,7 @@ def _integration_calls():
 
 
 FF_PATCH = os.path.join(harness.PKG, "matlab", "fastfading_dsce.patch")
+MOD_PATCH = os.path.join(harness.PKG, "matlab", "modulation_dsce.patch")
 
 
 def _patch_calls(path=PATCH):
@@ -138,13 +139,14 @@ def test_integration_md_calls_run_through_the_gateway(built):
     PSACE 'MMSE' patch) is accepted by the gateway with that many inputs and
     outputs: a documented call the gateway rejects (round-2: 'run' with 7
     arguments) fails here."""
-    calls = _integration_calls() + _patch_calls() + _patch_calls(FF_PATCH)
+    calls = _integration_calls() + _patch_calls() + _patch_calls(FF_PATCH) + _patch_calls(MOD_PATCH)
     cmds = {c[0] for c in calls}
     assert {"create", "set_channel", "set_snr", "add_scheme", "build_mmse", "run", "bits_per_rep",
             "mmse_onetap", "set_interpolation", "set_noise_slot", "tx_matrices", "enable_mse", "get_mse",
             "channel_realise"} <= cmds, cmds
     assert ("run", 4, 1) in calls and ("mmse_onetap", 5, 1) in _patch_calls()
     assert {("set_channel", 7, 0), ("channel_realise", 3, 1)} <= set(_patch_calls(FF_PATCH))
+    assert set(_patch_calls(MOD_PATCH)) == {("tx_matrices", 2, 2)}
     # create first (the gateway refuses any other command before it)
     triples = ["create:1:0"] + ["%s:%d:%d" % c for c in calls if c[0] != "create"]
     res, stdout = _run(built, ["replay", *triples])
@@ -215,3 +217,24 @@ def test_arity_and_argument_checks(results):
         assert results[k] == ("ERR", "dsce:args"), (k, results[k])
     assert results["run_before_create"] == ("ERR", "dsce:state")
     assert results["after_destroy"] == ("ERR", "dsce:state")
+
+
+def test_modulation_patch_applies_to_the_reference(tmp_path):
+    """The +Modulation shim (GetTXMatrix / GetRXMatrix of OFDM.m:184-218 and
+    FBMC.m:318-354 routed to dsce_mex('tx_matrices')) applies
+    cleanly to both reference classes: one UseEngine method and one engine
+    branch in each of GetTXMatrix / GetRXMatrix per class."""
+    ref = "/root/reference/+Modulation"
+    if not os.path.exists(ref) or not shutil.which("patch"):
+        pytest.skip("reference or patch(1) not available")
+    d = tmp_path / "+Modulation"
+    d.mkdir()
+    for f in ("OFDM.m", "FBMC.m"):
+        shutil.copy(os.path.join(ref, f), d / f)
+    out = subprocess.run(["patch", "-p1", "-i", MOD_PATCH], cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    for f in ("OFDM.m", "FBMC.m"):
+        body = (d / f).read_text(encoding="latin-1")
+        assert body.count("function UseEngine(obj, On)") == 1, f
+        assert body.count("] = dsce_mex('tx_matrices', obj);") == 2, f
+        assert body.count("~obj.PHY.TransmitRealSignal") == 2, f

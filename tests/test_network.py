@@ -48,3 +48,32 @@ def test_forward_network_is_dft24_with_the_output_scale():
     for i in range(4):
         got[4 * np.arange(6) + i] = X[i]
     np.testing.assert_allclose(got, s * np.fft.fft(xt), atol=1e-12)
+
+
+def dft6_pfa(x, sign):
+    """kernels_mc.hip dft6 (r05): Good-Thomas 6 = 2 x 3 with the DFT-3 rotation
+    fused into FMAs; natural-order input, X[k] returned at position p6(k) =
+    -k mod 6 (the order the kernels read it in)."""
+    H = np.sqrt(3.0) / 2.0
+    x = list(x)
+
+    def dft3(a, b, c):
+        t, d = b + c, b - c
+        m = a - 0.5 * t
+        return a + t, m + sign * 1j * H * d, m - sign * 1j * H * d
+
+    x[0], x[2], x[4] = dft3(x[0], x[2], x[4])
+    x[3], x[5], x[1] = dft3(x[3], x[5], x[1])
+    for k2 in range(3):
+        i0, i1 = 2 * k2, (2 * k2 + 3) % 6
+        x[i0], x[i1] = x[i0] + x[i1], x[i0] - x[i1]
+    return x
+
+
+def test_prime_factor_dft6_and_its_output_order():
+    rng = np.random.default_rng(3)
+    for sign in (1, -1):
+        u = rng.standard_normal(6) + 1j * rng.standard_normal(6)
+        got = dft6_pfa(u, sign)
+        ref = np.fft.ifft(u) * 6 if sign > 0 else np.fft.fft(u)
+        np.testing.assert_allclose([got[(6 - k) % 6] for k in range(6)], ref, atol=1e-13)
