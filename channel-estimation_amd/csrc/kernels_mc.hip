@@ -1060,6 +1060,7 @@ struct StorePerfectDetect {
     double idd, sI, sQ;
     // the chains' folded slicer (nearest_lin): f = z scale + offset, top = n - 1
     double scI, ofI, topI, scQ, ofQ, topQ;
+    double rQ;                         // k_pic_fft: scQ / scI (its chain runs on u scI)
     double pf_scale_re, pf_scale_im;   // k_pic_fft: qs gs (SchemeK::pf_scale)
     const double2* xp;                 // pilots [NP][R] (k_mic_pilot: the LS division)
     const double2* xs;                 // precoded symbols P [xP; xD] [LK][R] (the constant rows of v / u)
@@ -1427,18 +1428,23 @@ __device__ __forceinline__ int nearest_idx(double f, double top) {
     asm("v_med3_i32 %0, %1, 0, %2" : "=v"(c) : "v"(t), "v"((int)top));
     return c;
 }
+// g8: the level-grid -> symbol map as bytes at [iI][iQ] with row stride 16
+// (nI, nQ <= 16, M <= 256): the LDS address is one shift-or (r05; an int
+// table at iI nQ + iQ took a multiply and two shifts per row)
 __device__ __forceinline__ void slice6(int (&dp)[6], const double (&fI)[6], const double (&fQ)[6], double topI,
-                                       double topQ, int nQ, const int* sgrid) {
+                                       double topQ, const unsigned char* g8) {
     int code[6];
-    bool cand = false;
+    // candidates: any low word zero, by one unsigned min over the twelve words
+    // (v_min3_u32 chain; r05 — per-word compares cost ~35 instructions)
+    unsigned lo = 0xffffffffu;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const int iI = nearest_idx(fI[a], topI), iQ = nearest_idx(fQ[a], topQ);
         code[a] = iI | (iQ << 8);
-        cand |= (__double2loint(fI[a]) == 0) | (__double2loint(fQ[a]) == 0);
-        dp[a] = sgrid[__umul24(iI, nQ) + iQ];
+        lo = min(lo, min((unsigned)__double2loint(fI[a]), (unsigned)__double2loint(fQ[a])));
+        dp[a] = g8[(iI << 4) | iQ];
     }
-    if (__ballot(cand)) {
+    if (__ballot(lo == 0u)) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             // opaque copies: the exact test stays inside the rare branch (if-
@@ -1447,7 +1453,8 @@ __device__ __forceinline__ void slice6(int (&dp)[6], const double (&fI)[6], cons
             asm volatile("" : "+v"(gI), "+v"(gQ));
             const int iI = code[a] & 0xff, iQ = (code[a] >> 8) & 0xff;
             const int jI = max(iI - (gI == (double)iI ? 1 : 0), 0), jQ = max(iQ - (gQ == (double)iQ ? 1 : 0), 0);
-            dp[a] = min(min(sgrid[iI * nQ + iQ], sgrid[jI * nQ + iQ]), min(sgrid[iI * nQ + jQ], sgrid[jI * nQ + jQ]));
+            dp[a] = min(min((int)g8[(iI << 4) | iQ], (int)g8[(jI << 4) | iQ]),
+                        min((int)g8[(iI << 4) | jQ], (int)g8[(jI << 4) | jQ]));
         }
     }
 }
@@ -1582,7 +1589,9 @@ __device__ __forceinline__ double2 quad_tw(double2 e, bool r3) {
 // accumulating MFMAs each
 __device__ __forceinline__ double2 mfma4_cmul(double2 a, double2 b) {
     double re = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b.x, 0.0, 0, 0, 0);
-    re = __builtin_amdgcn_mfma_f64_4x4x4f64(-a.y, b.y, re, 0, 0, 0);
+    // - Ai Bi by the f64 MFMA's neg modifier on A (the blgp field on gfx950,
+    // neg:[1,0,0]) instead of two VALU moves per product (r05)
+    re = __builtin_amdgcn_mfma_f64_4x4x4f64(a.y, b.y, re, 0, 0, 1);
     double im = __builtin_amdgcn_mfma_f64_4x4x4f64(a.x, b.y, 0.0, 0, 0, 0);
     im = __builtin_amdgcn_mfma_f64_4x4x4f64(a.y, b.x, im, 0, 0, 0);
     return make_double2(re, im);
@@ -1644,7 +1653,19 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // two real K halves, 72 cycles per m per wave on the box) instead of the lane
 // twiddle, 8 DPP moves, 4 FMAs and the +-i selects (100 cycles,
 // tools/ubench/net.hip).  The previous quarter's sample 5 comes by ds_bpermute.
-template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false>
+// r05 (the per-section census, profiles/r05_census_*): the iteration carried
+// ~40 register copies (the fixed-point exit's loop state, now the SKIP variant
+// only), the imaginary A parts were negated by VALU moves (now the f64 MFMA's
+// neg modifier, mfma4_cmul), the tie candidates took ~35 instructions per
+// iteration (now one min3 chain), and the epilogue spent 10 FP64 operations
+// per row.  The chain now runs on u scaled by the slicer's scale c = scI: the
+// transforms are linear, so acc = c D u, and with Yo = c y / h + (ofI, 0) the
+// folded slicer input is
+//   fI = Yo.x + us.x - (acc / h).x,  fQ = (Yo.y + us.y - (acc / h).y) scQ / scI + ofQ
+// (7 FP64 operations per row).  Re-precoded decisions read the scaled
+// constellation; the constant rows of u (pilots) are per-lane LDS slots read
+// through the same address select, so a row's new u is one LDS read.
+template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false, bool SKIP = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
     int ug, blk;
@@ -1655,15 +1676,17 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     const int rl = unit % R;
     const int cq = NM ? r : (r >> 1) + 2 * (r & 1);            // time quarter of this lane
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    const double cs = o.scI, rq = o.rQ;                        // the chain's scale (host: scI != 0), scQ / scI
     __shared__ double2 sym[256];
-    __shared__ int sgrid[256];
+    __shared__ unsigned char sgrid[256];
     __shared__ double2 rpv[24];
     __shared__ int rdc[24];
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
     __shared__ double2 amt[NM ? 2 : 1][6][16];                  // NM: A_m[i][k] at [dir][m][i + 4 k]
     __shared__ int cntl[4][PM_MAXIT + 1];                      // [wave][stage]
-    // decisions u and the iteration-invariant y / h, 1 / h of the lane's rows,
-    // and the channel taps of the lane's samples (registers for all iterations)
+    __shared__ double2 ucst[6][256];                            // the lane's constant rows of u (scaled)
+    // decisions u (scaled) and the iteration-invariant Yo and 1 / h of the lane's
+    // rows, and the channel taps of the lane's samples (registers for all iterations)
     double2 u[6], yh[6], hc[6];
     unsigned txp[2] = {0u, 0u};
     double2 taps[6][NT];
@@ -1675,10 +1698,11 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         // the LDS writes: the writes wait only for the tables (vmcnt retires in
         // order), the per-unit data arrives during the barrier
         const double2 a = o.symbols[min(tid, o.M - 1)];
-        const int g = o.grid_sym[min(tid, o.nI * o.nQ - 1)];
+        const int gi = tid >> 4, gq = tid & 15;
+        const int g = o.grid_sym[min(gi * o.nQ + gq, o.nI * o.nQ - 1)];
         const int rt = min(tid, 23);
         const double2 pv = o.row_pval[row0 + rt];
-        const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+        const int dr = o.row_data[row0 + rt], cns = o.row_cons[row0 + rt];
         const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);   // twa: w24^(r m')
         const double2 tw = kW24[e % 12];
         const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
@@ -1695,13 +1719,14 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         for (int m = 0; m < 6; ++m)
 #pragma unroll
             for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
-        sym[tid] = stage_sym(make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
-        sgrid[tid] = tid < o.nI * o.nQ ? g : 0;
+        const double2 sa = stage_sym(make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
+        sym[tid] = make_double2(sa.x * cs, sa.y * cs);
+        sgrid[tid] = (unsigned char)(gi < o.nI && gq < o.nQ ? g : 0);
         // unconditional (clamped) table writes: a write under `if (tid < 24)`
         // lets the compiler sink the table loads into the branch, behind a
         // vmcnt(0) that also waits for every per-unit load
         rpv[rt] = pv;
-        rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;     // data index << 1 | no-edge, or -1
+        rdc[rt] = dr >= 0 ? (dr << 1) | (cns ? 1 : 0) : -1;    // data index << 1 | no-edge, or -1
         {
             // IFFT w24^(r m'); FFT qs gs w24^-(r m') (the output scale of Q' H G)
             const int tc = min(tid, 47), dir = tc / 24;
@@ -1718,6 +1743,13 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         }
     }
     __syncthreads();
+    // u scaled by c; the constant rows into the lane's own LDS slots (every row:
+    // the data rows' slots are never read; no barrier, only this lane reads them)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        u[a] = make_double2(u[a].x * cs, u[a].y * cs);
+        ucst[a][tid] = u[a];
+    }
     // data / no-edge masks of the lane's rows
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
@@ -1728,7 +1760,7 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     }
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     int ncnt = 0;
-    // The IC's fixed point (o.skip): D, h and y do not change between the
+    // The IC's fixed point (SKIP, o.skip): D, h and y do not change between the
     // iterations of the perfect-CSI branch (script:541-561), so an iteration
     // whose decisions equal the previous iteration's for every data row of the
     // wave's 16 units (the symbol blocks of OFDM are independent: D is block-
@@ -1738,34 +1770,58 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
     // iteration did).
     unsigned pk[2] = {0u, 0u};
     bool have = S0, conv = false;
+    // error-count weight of row a: data rows count 1, no-edge rows also 1 << 16
+    auto cweight = [&](int a) -> int {
+        return ((dmask >> a) & 1) ? (((emask >> a) & 1) ? 0x10001 : 1) : 0;
+    };
+    // the re-precoded decisions (pv_uni): one LDS read per row, the data rows
+    // from the scaled constellation, the others from their constant slot
+    // (neither branch reads the old u: with reprecode6's selects in the other
+    // branch the merge cost 13 register copies per iteration)
+    auto reprecode = [&](const int (&dp)[6]) {
+        double2 nv[6];
+        if (o.pv_uni) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) nv[a] = ((dmask >> a) & 1) ? sym[dp[a]] : ucst[a][tid];
+        } else {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double2 pr = c_mulf(rpv[4 * a + r], sym[dp[a]]), cv = ucst[a][tid];
+                nv[a] = ((dmask >> a) & 1) ? pr : cv;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) u[a] = nv[a];
+    };
     if (S0) {
-        // stage 0: y / h and 1 / h now, one-tap z = y / h, slicer, counts, decisions
+        // stage 0: Yo = c y / h + (ofI, 0) and 1 / h now, one-tap, slicer,
+        // counts, decisions
         int dp[6];
         double fI[6], fQ[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double2 hh = hc[a], yv = yh[a];
-            const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+            const double id = recip_fast(hh.x * hh.x + hh.y * hh.y);
             hc[a] = make_double2(hh.x * id, -hh.y * id);
-            yh[a] = c_mulf(yv, hc[a]);
-            fI[a] = fma(yh[a].x, o.scI, o.ofI);
-            fQ[a] = fma(yh[a].y, o.scQ, o.ofQ);
+            const double2 ys = c_mulf(yv, hc[a]);
+            yh[a] = make_double2(fma(ys.x, cs, o.ofI), ys.y * cs);
+            fI[a] = yh[a].x;
+            fQ[a] = fma(yh[a].y, rq, o.ofQ);
         }
-        slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
+        slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
-            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
-            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)(rdc[4 * a + r] >> 1)] = dp[a];
-            pk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
+            if (SKIP) pk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
-        reprecode6(u, dp, dmask, rpv, r, sym, o.pv_uni);
+        reprecode(dp);
         cntl[w][0] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);
         ncnt = 0;
     }
     for (int it = 1; it <= niter; ++it) {
-        if (conv) {
+        if (SKIP && conv) {
             // the fixed point (below): this iteration reproduces the previous one
             cntl[w][it] = cntl[w][it - 1];
             continue;
@@ -1825,66 +1881,68 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
             }
         }
         dft6<-1>(x);
-        // y / h and 1 / h at the first epilogue (not before the loop): the
-        // first chain runs while y and h are still in flight (S0: formed above)
+        // Yo and hcs at the first epilogue (not before the loop): the first chain
+        // runs while y and h are still in flight (S0: formed above)
         if (it == 1 && !S0)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 const double2 hh = hc[a], yv = yh[a];
-                const double id = 1.0 / (hh.x * hh.x + hh.y * hh.y);
+                const double id = recip_fast(hh.x * hh.x + hh.y * hh.y);
                 hc[a] = make_double2(hh.x * id, -hh.y * id);        // 1 / h
-                yh[a] = c_mulf(yv, hc[a]);                           // y / h
+                const double2 ys = c_mulf(yv, hc[a]);
+                yh[a] = make_double2(fma(ys.x, cs, o.ofI), ys.y * cs); // c y / h + (ofI, 0)
             }
-        // epilogue per row 4a + r: z = y / h - acc / h + u, slicer, counts,
-        // re-precoded decision into u
+        // epilogue per row 4a + r: the folded slicer input of z = y / h - acc / h
+        // + u (above), slicer, counts, re-precoded decision into u
         int dp[6];
-        unsigned npk[2] = {0u, 0u};
         double fI[6], fQ[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-            const double2 ah = c_mulf(x[p6(a)], hc[a]);
-            const double zx = (yh[a].x - ah.x) + u[a].x;
-            const double zy = (yh[a].y - ah.y) + u[a].y;
-            fI[a] = fma(zx, o.scI, o.ofI);
-            fQ[a] = fma(zy, o.scQ, o.ofQ);
+            const double2 xa = x[p6(a)], hh = hc[a];
+            fI[a] = fma(-xa.x, hh.x, fma(xa.y, hh.y, yh[a].x + u[a].x));
+            fQ[a] = fma(fma(-xa.x, hh.y, fma(-xa.y, hh.x, yh[a].y + u[a].y)), rq, o.ofQ);
             if (TRACE && ((dmask >> a) & 1) && unit == o.tr->unit) {
                 const int row = row0 + 4 * a + r;
-                const double2 yv = o.y[(size_t)row * U + unit], hh = o.h[(size_t)row * R + rl];
-                o.tr->yperf[(size_t)it * o.tr->LK + row] = c_add(c_sub(yv, x[p6(a)]), c_mul(hh, u[a]));
+                const double2 yv = o.y[(size_t)row * U + unit], hv = o.h[(size_t)row * R + rl];
+                o.tr->yperf[(size_t)it * o.tr->LK + row] =
+                    c_add(c_sub(yv, make_double2(xa.x / cs, xa.y / cs)), c_mul(hv, make_double2(u[a].x / cs, u[a].y / cs)));
             }
         }
         // a decision exactly on a mid-point (measure zero): the smallest symbol
         // index among the tied grid points (one uniform branch inside)
-        slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
+        slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
+        unsigned npk[2] = {0u, 0u};
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
-            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
-            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)it * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
-            npk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
+            if (SKIP) npk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
-        reprecode6(u, dp, dmask, rpv, r, sym, o.pv_uni);
+        reprecode(dp);
         cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
-        const bool same = have && npk[0] == pk[0] && npk[1] == pk[1];
-        pk[0] = npk[0];
-        pk[1] = npk[1];
-        have = true;
-        if (o.skip && it < niter && __all(same)) {
-            conv = true;
-            if (TRACE)
+        if (SKIP) {
+            const bool same = have && npk[0] == pk[0] && npk[1] == pk[1];
+            pk[0] = npk[0];
+            pk[1] = npk[1];
+            have = true;
+            if (o.skip && it < niter && __all(same)) {
+                conv = true;
+                if (TRACE)
 #pragma unroll
-                for (int a = 0; a < 6; ++a)
-                    if (((dmask >> a) & 1) && unit == o.tr->unit) {
-                        const int row = row0 + 4 * a + r;
-                        const double2 yv = o.y[(size_t)row * U + unit], hh = o.h[(size_t)row * R + rl];
-                        const double2 yp = c_add(c_sub(yv, x[p6(a)]), c_mul(hh, u[a]));
-                        for (int i2 = it + 1; i2 <= niter; ++i2) {
-                            o.tr->yperf[(size_t)i2 * o.tr->LK + row] = yp;
-                            o.tr->dec_p[(size_t)i2 * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+                    for (int a = 0; a < 6; ++a)
+                        if (((dmask >> a) & 1) && unit == o.tr->unit) {
+                            const int row = row0 + 4 * a + r;
+                            const double2 yv = o.y[(size_t)row * U + unit], hv = o.h[(size_t)row * R + rl];
+                            const double2 yp = c_add(c_sub(yv, make_double2(x[p6(a)].x / cs, x[p6(a)].y / cs)),
+                                                     c_mul(hv, make_double2(u[a].x / cs, u[a].y / cs)));
+                            for (int i2 = it + 1; i2 <= niter; ++i2) {
+                                o.tr->yperf[(size_t)i2 * o.tr->LK + row] = yp;
+                                o.tr->dec_p[(size_t)i2 * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
+                            }
                         }
-                    }
+            }
         }
     }
     // counters of every stage, summed over the block's 4 waves: thread
@@ -2065,7 +2123,7 @@ __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[
 // the wave's symbol, lane twiddles, the per-row diag(D_hat) weight of a delayed tap.
 struct Mic2Tables {
     double2 sym[256];
-    int sgrid[256];
+    unsigned char sgrid[256];          // slice6's byte grid [iI][iQ], row stride 16
     double2 twa[2][4][6];
     double2 amt[2][6][16];            // NM network: A_m[i][k] at [dir][m][i + 4 k] (k_pic_fft's)
 };
@@ -2073,15 +2131,19 @@ struct Mic2Tables {
 // One-tap + detection of the lane's six rows with diag(D_hat) = hd[a]; returns
 // the decided symbol indices (first-minimum tie rule, SignalConstellation.m:88)
 __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6], const double2 (&hd)[6],
-                                           const StorePerfectDetect& o, const int* sgrid) {
+                                           const StorePerfectDetect& o, const unsigned char* sgrid) {
+    // z = ye / hd with the slicer scale folded into the reciprocal (r05: 15 FP64
+    // operations per row instead of c_div_fast's 16 and the two scale FMAs)
     double fI[6], fQ[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-        const double2 z = c_div_fast(ye[a], hd[a]);
-        fI[a] = fma(z.x, o.scI, o.ofI);
-        fQ[a] = fma(z.y, o.scQ, o.ofQ);
+        const double2 b = hd[a], y = ye[a];
+        const double id = recip_fast(fma(b.x, b.x, b.y * b.y));
+        const double nx = fma(y.x, b.x, y.y * b.y), ny = fma(y.y, b.x, -(y.x * b.y));
+        fI[a] = fma(nx, id * o.scI, o.ofI);
+        fQ[a] = fma(ny, id * o.scQ, o.ofQ);
     }
-    slice6(dp, fI, fQ, o.topI, o.topQ, o.nQ, sgrid);
+    slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
 }
 
 // Stages 0..niter of the MMSE branch for one symbol of a unit (the common body of
@@ -2102,7 +2164,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                                             int row0, int unit, int unit_mf, int ul, int l, int r, int U, int R, int rl,
                                             int snr, const double* twl = nullptr, const double* tsl = nullptr,
                                             double2 (*szz)[NT * MIC_NB][17] = nullptr, int unit0 = 0,
-                                            const double2* bzl = nullptr) {
+                                            const double2* bzl = nullptr, double2 (*vcst)[256] = nullptr) {
     constexpr int NZ = NT * MIC_NB;
     const int cq = NM ? r : (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
@@ -2128,6 +2190,17 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         dmask |= dc >= 0 ? 1u << a : 0u;
         emask |= dc >= 0 && (dc & 1) ? 1u << a : 0u;
     }
+    // the data kernel (vcst): the constant rows of v in the lane's own LDS slots
+    // (written for every row, read only for the constant ones; no barrier, no
+    // other lane reads them), so a re-precoded row is one LDS read behind one
+    // address select (k_pic_fft's reprecode, r05)
+    if (!PIL)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) vcst[a][threadIdx.x] = v[a];
+    // error-count weight of row a: data rows count 1, no-edge rows also 1 << 16
+    auto cweight = [&](int a) -> int {
+        return ((dmask >> a) & 1) ? (((emask >> a) & 1) ? 0x10001 : 1) : 0;
+    };
     // window sums of the previous stage's estimated taps: diag(D_hat_{s-1}) of the
     // y_ic correction.  They equal Bs hP_{s-1} (Bs = Bv summed over the window),
     // i.e. the previous stage's own diag sums sn, which are kept instead of
@@ -2310,8 +2383,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
-            const int ne = data ? __popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))) : 0;
-            ncnt += ne + (((emask >> a) & 1) ? ne << 16 : 0);
+            ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && unit == o.tr->unit) {
                 const int row = row0 + 4 * a + r;
                 o.tr->yest[(size_t)s * o.tr->LK + row] = ye[a];
@@ -2319,7 +2391,23 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 if (data) o.tr->dec_e[(size_t)s * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
             }
         }
-        reprecode6(v, dp, dmask, rpv, r, tb.sym, o.pv_uni);
+        if (PIL) {
+            reprecode6(v, dp, dmask, rpv, r, tb.sym, o.pv_uni);
+        } else {
+            double2 nv[6];
+            if (o.pv_uni) {
+#pragma unroll
+                for (int a = 0; a < 6; ++a) nv[a] = ((dmask >> a) & 1) ? tb.sym[dp[a]] : vcst[a][threadIdx.x];
+            } else {
+#pragma unroll
+                for (int a = 0; a < 6; ++a) {
+                    const double2 pr = c_mulf(rpv[4 * a + r], tb.sym[dp[a]]), cv = vcst[a][threadIdx.x];
+                    nv[a] = ((dmask >> a) & 1) ? pr : cv;
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) v[a] = nv[a];
+        }
         cntl[s] = wave_sum_dpp(valid ? ncnt : 0);  // uniform: every lane writes the same word
         if (!LR && !PIL && s < ma.niter) {
             // stage s + 1's operands: hP_s (tap GEMM) and hP_{s+1} (diag)
@@ -2345,9 +2433,10 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDetect& o, int tid, int nth) {
     for (int i = tid; i < 256; i += nth) {
         const double2 a = o.symbols[min(i, o.M - 1)];
-        const int g = o.grid_sym[min(i, o.nI * o.nQ - 1)];
+        const int gi = i >> 4, gq = i & 15;
+        const int g = o.grid_sym[min(gi * o.nQ + gq, o.nI * o.nQ - 1)];
         tb.sym[i] = stage_sym(make_double2(i < o.M ? a.x : 0.0, i < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
-        tb.sgrid[i] = i < o.nI * o.nQ ? g : 0;
+        tb.sgrid[i] = (unsigned char)(gi < o.nI && gq < o.nQ ? g : 0);
     }
     if (tid < 48) {
         const int e = ((tid / 6) % 4) * (tid % 6);
@@ -2459,6 +2548,7 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __shared__ double2 bss[2][NT][NP];
     __shared__ double twd[MIC_NB * 24 + MIC_NB];            // LR: T_k over the symbol's window + sums
     __shared__ int cntl[4][PM_MAXIT + 1];
+    __shared__ double2 vcst[6][256];                        // each lane's constant rows of v
     int ug, bi;
     band_block(ord, ma.nb, ug, bi);
     const int blk = ma.blks[bi];
@@ -2504,7 +2594,7 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
     mic2_stages<NT, SH, NP, TRACE, false, NM, LR>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
                                                   row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twd,
-                                                  twd + MIC_NB * 24);
+                                                  twd + MIC_NB * 24, nullptr, 0, nullptr, vcst);
     __syncthreads();
     for (int i = tid; i < 2 * (ma.niter + 1); i += 256) {
         const int s = i >> 1, edge = i & 1;
@@ -2736,7 +2826,9 @@ static unsigned launch_txrx(hipStream_t s, const Opts& op, const SchemeK& sk, co
 static bool pic_fft_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
     const bool fits = (long long)24 * b.U * 16 < (1ll << 32) && (long long)ch.ntap * ch.N * b.R * 16 < (1ll << 32) &&
                       (long long)sk.LK * b.U < (1ll << 62);
-    return sk.pf_ok && op.pic_chain == 3 && pic_fft_shift(ch) >= 0 && fits && niter >= 1 && niter <= PM_MAXIT;
+    // slice6's byte grid: nI, nQ <= 16 levels, M <= 256 symbols
+    return sk.pf_ok && op.pic_chain == 3 && pic_fft_shift(ch) >= 0 && fits && niter >= 1 && niter <= PM_MAXIT &&
+           sk.M <= 256 && sk.nI <= 16 && sk.nQ <= 16;
 }
 
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter) {
@@ -2784,6 +2876,7 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
     o.scQ = sk.real_detect ? 0.0 : o.idd * o.sQ;
     o.ofQ = 0.5 - sk.lv0Q * o.sQ;
     o.topQ = sk.nQ - 1;
+    o.rQ = o.scI != 0.0 ? o.scQ / o.scI : 0.0;
     o.pf_scale_re = sk.pf_scale.x;
     o.pf_scale_im = sk.pf_scale.y;
     o.pv_uni = sk.pv_uni;
@@ -2883,9 +2976,20 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
     // stage0: the chain also runs stage 0 of the branch (with k_mic_pilot /
     // k_mic_data); otherwise stage 0 came from the stage kernel (u in HBM)
+    // the fixed-point exit (Opts::pic_skip) is its own variant (its loop state
+    // costs the plain chain ~40 register copies per iteration), matrix-core
+    // network only
+    if (op.pic_skip && !op.pic_net)
+        throw std::invalid_argument("launch_perfect_chain: pic_skip needs pic_net 1");
+    if (!(o.scI != 0.0))
+        throw std::logic_error("launch_perfect_chain: the chain's slicer scale is zero");
 #define LAUNCH_PF(NTV, SHV, S0V, NMV)                                                                               \
     do {                                                                                                             \
-        if (b.tr)                                                                                                    \
+        if (NMV && op.pic_skip && b.tr)                                                                              \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V, NMV, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+        else if (NMV && op.pic_skip)                                                                                 \
+            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V, NMV, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
+        else if (b.tr)                                                                                               \
             hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);  \
         else                                                                                                         \
             hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
