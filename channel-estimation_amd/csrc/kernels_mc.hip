@@ -2169,11 +2169,10 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     const int cq = NM ? r : (r >> 1) + 2 * (r & 1);
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    const double isqk = sk.inv_sqrt_kappa;
     const bool valid = rl < o.rvalid;
     // per-unit operands, read once: y, transmitted indices, the rows' constant
-    // part of v (precoded pilots / zero rows); PIL: the transmitted pilots come
-    // from the block's LDS table xpb[pilot][unit]
+    // part of v (precoded pilots / zero rows); PIL: the LS factors isqk / x_p
+    // come from the block's LDS table xpb[pilot][unit]
     double2 yv[6], v[6];
     unsigned txp[2] = {0u, 0u};
 #pragma unroll
@@ -2338,8 +2337,8 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             for (int a = 0; a < 6; ++a) {
                 const int pc = rpc[4 * a + r];
                 if (pc >= 0) {
-                    const double2 q = c_div_fast(ye[a], xpb[pc][ul]);
-                    const double2 h = make_double2(q.x * isqk, q.y * isqk);
+                    // xpb holds isqk / x_p (k_mic_pilot's table fill): one product
+                    const double2 h = c_mulf(ye[a], xpb[pc][ul]);
                     hx[pc * 17 + ul] = h;
                     if (!LR || TRACE) ma.hpa[((size_t)s * NP + pc) * U + unit] = h;
                 }
@@ -2483,7 +2482,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     __shared__ int rdc[4][24], rpc[4][24];
     __shared__ double2 bss[LR ? 1 : 4][2][NT][NP];          // Bs of each wave's symbol, both variants
     __shared__ double2 shp[2][NP][17];                      // hP of the block's 16 units, double-buffered
-    __shared__ double2 xpb[NP][17];                         // transmitted pilots of the block's 16 units
+    __shared__ double2 xpb[NP][17];                         // isqk / transmitted pilot of the block's 16 units
     __shared__ double2 szz[LR ? 2 : 1][NZ][17];             // LR: Z of the block's 16 units, double-buffered
     __shared__ double twp[LR ? 4 : 1][MIC_NB * 24 + MIC_NB];   // LR: each wave's T_k window + sums
     __shared__ double2 bzl[LR ? 2 * NZ * NP : 1];           // LR: Bz of both variants at this SNR
@@ -2511,9 +2510,14 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
         const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
         bss[LR ? 0 : w][var][q][p] = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
     }
+    // the LS divisor of every pilot of the block's units as isqk / x_p (r05: the
+    // per-stage LS of a pilot row is one complex product instead of a division)
+    const double isqk0 = sk.inv_sqrt_kappa;
     for (int i = tid; i < NP * 16; i += blockDim.x) {
         const int u16 = ug16 * 16 + (i & 15);
-        xpb[i >> 4][i & 15] = o.xp[(size_t)(i >> 4) * R + u16 % R];
+        const double2 xv = o.xp[(size_t)(i >> 4) * R + u16 % R];
+        const double id = isqk0 / (xv.x * xv.x + xv.y * xv.y);
+        xpb[i >> 4][i & 15] = make_double2(xv.x * id, -xv.y * id);
     }
     __syncthreads();
     const double2* __restrict__ bvb = ma.bv + ((size_t)snr * NT * ma.N + klo) * NP;
