@@ -2618,8 +2618,12 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
 // chunk y = qs DFT24(r0 + sqrt(Pn/2) z) with z the noise stream of LoadNoisy
 // (identical draws); the perfect-CSI diag(D) = qs gs sum_q w^(-l d_q) S_q(IR)
 // (S_q = the window sum of tap q).  Replaces the G band, k_channel_apply, the
-// diag(D) band and the noisy Q^H band: s and r0 never reach memory.  Lane quad
-// = realisation (k_pic_fft's layout), block = 64 realisations x one symbol.
+// diag(D) band and the noisy Q^H band: s and r0 never reach memory.  A
+// realisation's four time quarters sit on the four 16-lane rows (lane = 16 r +
+// realisation, k_pic_fft's NM layout), block = 64 realisations x one symbol; the
+// 4-point network of both transforms is one complex 4 x 4 product per sample
+// on the matrix cores (r05: the DPP network cost 100 cycles per sample and
+// wave against 72, and the quad sums of diag(D) are one ones-MFMA each).
 // ---------------------------------------------------------------------------
 constexpr int TXRX_MAXSNR = 64;      // SNR points per k_txrx_fft launch (the launcher checks)
 
@@ -2640,12 +2644,12 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     int L = blockIdx.x;
     if (xcd) L = xcd_remap(L, gridDim.x);
     const int blk = L % sk.QH.nblk, rg = L / sk.QH.nblk;
-    const int tid = threadIdx.x, l = tid & 63, r = l & 3, w = tid >> 6;
-    const int rl = rg * WAVE + w * 16 + (l >> 2);
+    const int tid = threadIdx.x, l = tid & 63, r = l >> 4, w = tid >> 6;
+    const int rl = rg * WAVE + w * 16 + (l & 15);
     const int R = ta.R;
-    const int cq = (r >> 1) + 2 * (r & 1);
+    const int cq = r;                                           // time quarter of this lane
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
-    __shared__ double2 twa[2][4][6];
+    __shared__ double2 amt[2][6][16];                          // A_m[i][k] at [dir][m][i + 4 k]
     __shared__ double2 wrow[24];
     __shared__ double ssc[TXRX_MAXSNR];                        // sqrt(Pn / 2) of the chunk's SNR points
     __shared__ double2 slt[128], sct[256];                     // the Box-Muller tables (bm_tables.h)
@@ -2655,9 +2659,11 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         // table loads (twiddles, noise powers), then the per-unit loads, then
         // the LDS writes (unconditional, clamped: a write under a branch lets
         // the compiler sink its load there, behind a vmcnt(0))
-        const int tc = min(tid, 47);
-        const int e = ((tc / 6) % 4) * (tc % 6);
-        const double2 tw = kW24[e % 12];
+        // A_m[i][k]: inverse gs w24^(6 i k + k m), forward qs w24^-(6 i k + i m)
+        const int tc = min(tid, 191);
+        const int dir = tc / 96, mm = (tc / 16) % 6, ii = tc & 3, kk = (tc >> 2) & 3;
+        const int ea = (6 * ii * kk + (dir ? ii : kk) * mm) % 24;
+        const double2 tw = kW24[ea % 12];
         const int lr0 = min(max(tid - 64, 0), 23);
         const double2 t0 = kW24[lr0 % 12];
         const int kc = min(tid, ta.nchunk - 1);
@@ -2669,9 +2675,8 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         for (int m = 0; m < 6; ++m)
 #pragma unroll
             for (int q = 0; q < NT; ++q) taps[m][q] = ta.ir[((size_t)q * ta.N + klo + 6 * cq + m) * R + rl];
-        const int dir = tc / 24;
-        const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-        twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
+        const double2 v = ea >= 12 ? make_double2(-tw.x, -tw.y) : tw;
+        amt[dir][mm][ii + 4 * kk] = dir ? c_mul(qs, make_double2(v.x, -v.y)) : c_mul(gs, v);
         const double2 wl = lr0 >= 12 ? make_double2(-t0.x, -t0.y) : t0;
         wrow[lr0] = c_mul(ps, make_double2(wl.x, -wl.y));
         ssc[kc] = sqrt(pnv / 2.0);
@@ -2679,7 +2684,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
         slt[tid & 127] = lv;
     }
     __syncthreads();
-    const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
+    const int ai = (l & 3) + 4 * (l >> 4);                    // this lane's A entry
     // perfect-CSI diag(D) of the symbol's rows from the window sums of the taps
     {
         double2 s0 = make_double2(0.0, 0.0), s1 = s0;
@@ -2688,8 +2693,9 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
             double2 sq = make_double2(0.0, 0.0);
 #pragma unroll
             for (int m = 0; m < 6; ++m) sq = c_add(sq, taps[m][q]);
-            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
-            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+            // sum over the realisation's four quarters (rows): ones(4 x 4) x B
+            sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.x, 0.0, 0, 0, 0),
+                              __builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.y, 0.0, 0, 0, 0));
             if ((SH >> q) & 1) s1 = c_add(s1, sq);
             else s0 = c_add(s0, sq);
         }
@@ -2705,19 +2711,12 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
     dft6<1>(x);
     double2 t[6];
 #pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const double2 p = c_mulf(x[p6(m)], twa[0][r][m]);
-        const double2 pv = dpp_c<QP_XOR2>(p);
-        double2 e = make_double2(fma(sg1, p.x, pv.x), fma(sg1, p.y, pv.y));
-        e = quad_tw<1>(e, r == 3);
-        const double2 qv = dpp_c<QP_XOR1>(e);
-        t[m] = make_double2(fma(sg2, e.x, qv.x), fma(sg2, e.y, qv.y));
-    }
+    for (int m = 0; m < 6; ++m) t[m] = mfma4_cmul(amt[0][m][ai], x[p6(m)]);
     // r0 = H s over the window (the delayed tap reads the cyclic prefix for m = 0
     // of quarter 0: sample 5 of quarter 3)
     double2 r0[6];
     {
-        const double2 tprev = dpp_c<QP_PREV>(t[5]);
+        const double2 tprev = bperm_c(((l + 48) & 63) * 4, t[5]);
 #pragma unroll
         for (int m = 5; m >= 0; --m) {
             const double2 tp = m ? t[m - 1] : tprev;
@@ -2739,12 +2738,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
 #pragma unroll
         for (int m = 0; m < 6; ++m) {
             const uint4 wr = stream_sub(phs[m], STREAM_NOISE, (uint32_t)(ta.base + snr + 256 * ta.slot));
-            const double2 rv = noise_add(r0[m], sc, wr, slt, sct);
-            const double2 pv = dpp_c<QP_XOR1>(rv);
-            double2 g = make_double2(fma(sg2, rv.x, pv.x), fma(sg2, rv.y, pv.y));
-            g = quad_tw<-1>(g, r == 3);
-            const double2 qv = dpp_c<QP_XOR2>(g);
-            f[m] = c_mulf(make_double2(fma(sg1, g.x, qv.x), fma(sg1, g.y, qv.y)), twa[1][r][m]);
+            f[m] = mfma4_cmul(amt[1][m][ai], noise_add(r0[m], sc, wr, slt, sct));
         }
         dft6<-1>(f);
         const size_t u0 = (size_t)k * R + rl;
