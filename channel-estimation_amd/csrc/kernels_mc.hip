@@ -1396,6 +1396,25 @@ __device__ __forceinline__ double2 buf_ld2(__amdgpu_buffer_rsrc_t r, unsigned vo
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
     return make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
 }
+__device__ __forceinline__ unsigned buf_ldu16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    return (unsigned)__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
+}
+// The per-unit rows 4 a + r (a = 0..5) of one 24-row symbol block of a [LK][ld]
+// array: a buffer view from the block's first row, the lane's byte offset
+// (r ld + col) esz, and row a at the wave-uniform offset 4 a ld esz (SGPR): no
+// 64-bit address arithmetic per load (r05; the chain kernels' prologues spent
+// ~3 VALU per row and array on it).  Callers: 24 ld esz < 2^32 (pic_fft_ok).
+struct RowView {
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff, step;
+    __device__ __forceinline__ RowView(const void* base, int row0, int ld, int r, int col, int esz) {
+        rs = buf_rsrc((const char*)base + (size_t)row0 * ld * esz, (size_t)24 * ld * esz);
+        voff = (unsigned)(r * ld + col) * (unsigned)esz;
+        step = 4u * (unsigned)ld * (unsigned)esz;
+    }
+    __device__ __forceinline__ double2 ld2(int a) const { return buf_ld2(rs, voff, (unsigned)a * step); }
+    __device__ __forceinline__ unsigned ldu16(int a) const { return buf_ldu16(rs, voff, (unsigned)a * step); }
+};
 
 // Nearest level of a uniform level grid lv0 + i step (i < n) by rounding
 // f = (x - lv0) / step + 0.5, folded into one FMA.  An exact mid-point (f
@@ -1706,14 +1725,21 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);   // twa: w24^(r m')
         const double2 tw = kW24[e % 12];
         const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+        // NM: A_m[i][k], inverse w24^(6 i k + k m), forward qs gs w24^-(6 i k + i m);
+        // its constant read issued here with the other table reads (inside the
+        // tid < 192 branch it came after the per-unit loads, and its vmcnt(0)
+        // made the table writes wait for all of them)
+        const int tn = min(tid, 191), ndir = tn / 96, nm_ = (tn / 16) % 6, nii = tn & 3, nkk = (tn >> 2) & 3;
+        const int nea = (6 * nii * nkk + (ndir ? nii : nkk) * nm_) % 24;
+        const double2 nt0 = kW24[nea % 12];
+        const RowView vu = S0 ? RowView(o.xs, row0, R, r, rl, 16) : RowView(o.u, row0, U, r, unit, 16);
+        const RowView vs(o.sidr, row0, R, r, rl, 2), vy(o.y, row0, U, r, unit, 16), vh(o.h, row0, R, r, rl, 16);
 #pragma unroll
         for (int b = 0; b < 6; ++b) {
-            const int row = row0 + 4 * b + r;
-            if (S0) u[b] = o.xs[(size_t)row * R + rl];
-            else u[b] = o.u[(size_t)row * U + unit];
-            txp[b >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (b & 3));
-            yh[b] = o.y[(size_t)row * U + unit];
-            hc[b] = o.h[(size_t)row * R + rl];
+            u[b] = vu.ld2(b);
+            txp[b >> 2] |= (vs.ldu16(b) & 0xffu) << (8 * (b & 3));
+            yh[b] = vy.ld2(b);
+            hc[b] = vh.ld2(b);
         }
 #pragma unroll
         for (int m = 0; m < 6; ++m)
@@ -1727,19 +1753,15 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         // vmcnt(0) that also waits for every per-unit load
         rpv[rt] = pv;
         rdc[rt] = dr >= 0 ? (dr << 1) | (cns ? 1 : 0) : -1;    // data index << 1 | no-edge, or -1
-        {
+        if (!NM) {
             // IFFT w24^(r m'); FFT qs gs w24^-(r m') (the output scale of Q' H G)
             const int tc = min(tid, 47), dir = tc / 24;
             const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
             twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        }
-        if (NM && tid < 192) {
-            // A_m[i][k]: inverse w24^(6 i k + k m), forward qs gs w24^-(6 i k + i m)
-            const int dir = tid / 96, m = (tid / 16) % 6, ii = tid & 3, kk = (tid >> 2) & 3;
-            const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
-            const double2 t0 = kW24[ea % 12];
-            const double2 v = ea >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-            amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+        } else {
+            // unconditional (clamped: threads 192.. rewrite entry 191's value)
+            const double2 v = nea >= 12 ? make_double2(-nt0.x, -nt0.y) : nt0;
+            amt[ndir][nm_][nii + 4 * nkk] = ndir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
         }
     }
     __syncthreads();
@@ -2146,6 +2168,25 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
     slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
 }
 
+// The per-unit operands of a symbol, read once (rows 4 a + r): y, the rows'
+// constant part of v (precoded pilots / zero rows), transmitted indices; loaded
+// by the kernels before their table barrier (r05: after it, the first stage
+// waited for them with the barrier's latency behind it)
+struct Mic2Unit {
+    double2 yv[6], v[6];
+    unsigned txp[2];
+    __device__ __forceinline__ void load(const StorePerfectDetect& o, int row0, int r, int unit, int rl) {
+        const RowView vy(o.y, row0, o.U, r, unit, 16), vx(o.xs, row0, o.R, r, rl, 16), vs(o.sidr, row0, o.R, r, rl, 2);
+        txp[0] = txp[1] = 0u;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            yv[a] = vy.ld2(a);
+            v[a] = vx.ld2(a);
+            txp[a >> 2] |= (vs.ldu16(a) & 0xffu) << (8 * (a & 3));
+        }
+    }
+};
+
 // Stages 0..niter of the MMSE branch for one symbol of a unit (the common body of
 // k_mic_pilot and k_mic_data).  PIL: a pilot symbol (LS of every stage into the
 // block's LDS exchange + hpa, one barrier per stage); otherwise hP_s comes from
@@ -2158,6 +2199,7 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
 // MACs per symbol and unit); diag(D_hat_s) from S_q = sum_k tsl[k] Z_s[q k].
 template <int NT, int SH, int NP, bool TRACE, bool PIL, bool NM, bool LR, class ALoad, class BsLoad>
 __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o,
+                                            const Mic2Unit& mu,
                                             const Mic2Tables& tb, const double2* rpv, const int* rdc, const int* rpc,
                                             const double2* wrow, double2 (*shp)[NP][17],
                                             const double2 (*xpb)[17], int (*cntl), const ALoad& A, const BsLoad& Bs,
@@ -2170,18 +2212,18 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
     const bool valid = rl < o.rvalid;
-    // per-unit operands, read once: y, transmitted indices, the rows' constant
-    // part of v (precoded pilots / zero rows); PIL: the LS factors isqk / x_p
+    // per-unit operands (mu, loaded by the kernel); PIL: the LS factors isqk / x_p
     // come from the block's LDS table xpb[pilot][unit]
     double2 yv[6], v[6];
-    unsigned txp[2] = {0u, 0u};
+    unsigned txp[2] = {mu.txp[0], mu.txp[1]};
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-        const int row = row0 + 4 * a + r;
-        yv[a] = o.y[(size_t)row * U + unit];
-        v[a] = o.xs[(size_t)row * R + rl];
-        txp[a >> 2] |= ((unsigned)o.sidr[(size_t)row * R + rl] & 0xffu) << (8 * (a & 3));
+        yv[a] = mu.yv[a];
+        v[a] = mu.v[a];
     }
+    // this launch's Z of every stage (LR data kernel): [stage][NZ][U] by a buffer view
+    const __amdgpu_buffer_rsrc_t rza =
+        buf_rsrc(ma.za, LR && !PIL ? (size_t)(ma.niter + 1) * NZ * U * sizeof(double2) : 0);
     unsigned dmask = 0u, emask = 0u;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -2275,7 +2317,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 #pragma unroll
             for (int j = 0; j < NZR; ++j) zp[j] = zc[j];
 #pragma unroll
-            for (int j = 0; j < NZR; ++j) zc[j] = ma.za[((size_t)s * NZ + j) * U + unit];     // this stage's Z
+            for (int j = 0; j < NZR; ++j) zc[j] = buf_ld2(rza, (unsigned)unit * 16u, (unsigned)((s * NZ + j) * U) * 16u);
         } else if (!LR && !PIL) {
 #pragma unroll
             for (int k = 0; k < NP / 4; ++k) hn4[k] = ma.hpa[(size_t)s * NP * U + (size_t)(r * (NP / 4) + k) * U + unit];
@@ -2429,7 +2471,57 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 }
 
 // LDS tables of a block: constellation / slicer grid (256 entries), lane twiddles
+// Two-phase table staging for 256-thread blocks (r05): mic2_tab_load issues
+// every global read of the block tables (one entry of each per thread, clamped,
+// unconditional) and of the symbol's row tables (thread rt = min(t, 23)), the
+// caller then issues its per-unit reads, and mic2_tab_store writes LDS waiting
+// only for the table reads (vmcnt retires in order).  A read under a branch
+// waited with vmcnt(0) for everything issued before it.
+struct Mic2TabLoad {
+    double2 a, tw, t0, pv, tr;
+    int g, dr, cs, pcr;
+};
+__device__ __forceinline__ void mic2_tab_load(Mic2TabLoad& L, const StorePerfectDetect& o, const SchemeK& sk, int row0,
+                                              int tid, int t) {
+    const int gi = tid >> 4, gq = tid & 15;
+    L.a = o.symbols[min(tid, o.M - 1)];
+    L.g = o.grid_sym[min(gi * o.nQ + gq, o.nI * o.nQ - 1)];
+    const int tc = min(tid, 47), e = ((tc / 6) % 4) * (tc % 6);
+    L.tw = kW24[e % 12];
+    const int tn = min(tid, 191), dir = tn / 96, m = (tn / 16) % 6, ii = tn & 3, kk = (tn >> 2) & 3;
+    L.t0 = kW24[((6 * ii * kk + (dir ? ii : kk) * m) % 24) % 12];
+    const int rt = min(t, 23);
+    L.pv = o.row_pval[row0 + rt];
+    L.dr = o.row_data[row0 + rt];
+    L.cs = o.row_cons[row0 + rt];
+    L.pcr = sk.row_pcol[row0 + rt];
+    L.tr = kW24[rt % 12];
+}
+__device__ __forceinline__ void mic2_tab_store(const Mic2TabLoad& L, Mic2Tables& tb, double2* rpv, int* rdc, int* rpc,
+                                               double2* wrow, const StorePerfectDetect& o, const SchemeK& sk, int tid,
+                                               int t) {
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
+    const int gi = tid >> 4, gq = tid & 15;
+    tb.sym[tid] = stage_sym(make_double2(tid < o.M ? L.a.x : 0.0, tid < o.M ? L.a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
+    tb.sgrid[tid] = (unsigned char)(gi < o.nI && gq < o.nQ ? L.g : 0);
+    const int tc = min(tid, 47), e = ((tc / 6) % 4) * (tc % 6);
+    const double2 v = e >= 12 ? make_double2(-L.tw.x, -L.tw.y) : L.tw;
+    tb.twa[tc / 24][(tc / 6) % 4][tc % 6] = tc >= 24 ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+    const int tn = min(tid, 191), dir = tn / 96, m = (tn / 16) % 6, ii = tn & 3, kk = (tn >> 2) & 3;
+    const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
+    const double2 vn = ea >= 12 ? make_double2(-L.t0.x, -L.t0.y) : L.t0;
+    tb.amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(vn.x, -vn.y)) : vn;
+    // row tables (threads t >= 24 rewrite row 23's entries)
+    const int rt = min(t, 23);
+    rpv[rt] = L.pv;
+    rdc[rt] = L.dr >= 0 ? (L.dr << 1) | (L.cs ? 1 : 0) : -1;
+    rpc[rt] = L.dr < 0 && L.pcr >= 0 && L.pcr < sk.NP ? L.pcr : -1;
+    const double2 wl = rt >= 12 ? make_double2(-L.tr.x, -L.tr.y) : L.tr;
+    wrow[rt] = c_mul(scale, make_double2(wl.x, -wl.y));
+}
+
 __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDetect& o, int tid, int nth) {
+    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
     for (int i = tid; i < 256; i += nth) {
         const double2 a = o.symbols[min(i, o.M - 1)];
         const int gi = i >> 4, gq = i & 15;
@@ -2440,7 +2532,6 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
     if (tid < 48) {
         const int e = ((tid / 6) % 4) * (tid % 6);
         const double2 tw = kW24[e % 12];
-        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
         const int dir = tid / 24;
         const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
         tb.twa[dir][(tid / 6) % 4][tid % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
@@ -2450,7 +2541,6 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
         const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
         const double2 t0 = kW24[ea % 12];
         const double2 v = ea >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
         tb.amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
     }
 }
@@ -2460,17 +2550,18 @@ __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDe
 // (-1: not a pilot row), diag(D_hat) weight qs gs w^(-l) of a delayed tap
 __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, double2* wrow, const SchemeK& sk,
                                           const StorePerfectDetect& o, int row0, int t) {
-    if (t < 24) {
-        const double2 pv = o.row_pval[row0 + t];
-        const int dr = o.row_data[row0 + t], cs = o.row_cons[row0 + t];
-        const int pcr = sk.row_pcol[row0 + t];
-        rpv[t] = pv;
-        rdc[t] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
-        rpc[t] = dr < 0 && pcr >= 0 && pcr < sk.NP ? pcr : -1;
-        const double2 t0 = kW24[t % 12];
-        const double2 wl = t >= 12 ? make_double2(-t0.x, -t0.y) : t0;
-        wrow[t] = c_mul(make_double2(o.pf_scale_re, o.pf_scale_im), make_double2(wl.x, -wl.y));
-    }
+    // clamped, unconditional (threads t >= 24 rewrite row 23's entries): no
+    // branch around the reads (r05)
+    const int rt = min(t, 23);
+    const double2 pv = o.row_pval[row0 + rt];
+    const int dr = o.row_data[row0 + rt], cs = o.row_cons[row0 + rt];
+    const int pcr = sk.row_pcol[row0 + rt];
+    const double2 t0 = kW24[rt % 12];
+    rpv[rt] = pv;
+    rdc[rt] = dr >= 0 ? (dr << 1) | (cs ? 1 : 0) : -1;
+    rpc[rt] = dr < 0 && pcr >= 0 && pcr < sk.NP ? pcr : -1;
+    const double2 wl = rt >= 12 ? make_double2(-t0.x, -t0.y) : t0;
+    wrow[rt] = c_mul(make_double2(o.pf_scale_re, o.pf_scale_im), make_double2(wl.x, -wl.y));
 }
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
@@ -2490,15 +2581,32 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
     const int U = o.U, R = o.R;
-    const int ug16 = xcd_remap(blockIdx.x, gridDim.x);     // 16-unit group
+    // 16-unit group, SNR-fastest inside each XCD's contiguous range (r05): the
+    // SNR points of a realisation share its per-realisation reads (xs, sidr, x_p)
+    // in one L2 (unit-major, they sat on different XCDs: 1.72x the algorithmic
+    // HBM bytes per launch)
+    int ug16;
+    {
+        const int L = xcd_remap(blockIdx.x, gridDim.x), nch = o.U / o.R;
+        ug16 = (L % nch) * (o.R / 16) + L / nch;
+    }
     const int ul = NM ? l & 15 : l >> 2;
     const int unit = ug16 * 16 + ul, unit_mf = ug16 * 16 + (l & 15);
     const int rl = unit % R;
     const int snr = o.snr0 + (ug16 * 16) / R;
     const int blk = ma.blks[w];
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
-    mic2_tables(tb, o, tid, blockDim.x);
-    mic2_rows(rpv[w], rdc[w], rpc[w], wrow[w], sk, o, row0, l);
+    Mic2Unit mu;
+    if (blockDim.x == 256) {
+        Mic2TabLoad tl;
+        mic2_tab_load(tl, o, sk, row0, tid, l);
+        mu.load(o, row0, r, unit, rl);
+        mic2_tab_store(tl, tb, rpv[w], rdc[w], rpc[w], wrow[w], o, sk, tid, l);
+    } else {
+        mu.load(o, row0, r, unit, rl);
+        mic2_tables(tb, o, tid, blockDim.x);
+        mic2_rows(rpv[w], rdc[w], rpc[w], wrow[w], sk, o, row0, l);
+    }
     if (LR) {
         for (int i = l; i < MIC_NB * 25; i += 64)
             twp[w][i] = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
@@ -2526,7 +2634,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     // reloaded at the W -> W0 switch: 40 more VGPRs, 1.97 -> 2.28 ms per step)
     auto A = [&](int var, int q, int j, int p) { return bvb[var * vstride + ((size_t)q * ma.N + j) * NP + p]; };
     auto Bs = [&](int var, int q, int p) { return bss[LR ? 0 : w][var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, true, NM, LR>(sk, ma, o, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
+    mic2_stages<NT, SH, NP, TRACE, true, NM, LR>(sk, ma, o, mu, tb, rpv[w], rdc[w], rpc[w], wrow[w], shp, xpb, cntl[w], A,
                                                  Bs, row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twp[LR ? w : 0],
                                                  twp[LR ? w : 0] + MIC_NB * 24, szz, ug16 * 16, bzl);
     __syncthreads();
@@ -2564,13 +2672,16 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     const int unit = ug * WAVE + w * 16 + ul, unit_mf = ug * WAVE + w * 16 + (l & 15);
     const int rl = unit % R;
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
+    Mic2Unit mu;
     if constexpr (LR) {
         // the load clamped and issued first; only the threads with an entry store
         // (156 threads re-stored entry 99)
         const int i = min(tid, MIC_NB * 25 - 1);
         const double t = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
-        mic2_tables(tb, o, tid, 256);
-        mic2_rows(rpv, rdc, rpc, wrow, sk, o, row0, tid);
+        Mic2TabLoad tl;
+        mic2_tab_load(tl, o, sk, row0, tid, tid);
+        mu.load(o, row0, r, unit, rl);
+        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, o, sk, tid, tid);
         if (tid < MIC_NB * 25) twd[tid] = t;
     } else {
         // every global load before the first LDS write (clamped, unconditional)
@@ -2584,8 +2695,10 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
         }
         const int ib = min(tid, 2 * NT * NP - 1), var = ib / (NT * NP), q = (ib / NP) % NT, p = ib % NP;
         const double2 bsv = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
-        mic2_tables(tb, o, tid, 256);
-        mic2_rows(rpv, rdc, rpc, wrow, sk, o, row0, tid);
+        Mic2TabLoad tl;
+        mic2_tab_load(tl, o, sk, row0, tid, tid);
+        mu.load(o, row0, r, unit, rl);
+        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, o, sk, tid, tid);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = min(tid + 256 * k, NBV - 1);
@@ -2596,7 +2709,7 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
     __syncthreads();
     auto A = [&](int var, int q, int j, int p) { return sbv[LR ? 0 : var][q][LR ? 0 : j][p]; };
     auto Bs = [&](int var, int q, int p) { return bss[var][q][p]; };
-    mic2_stages<NT, SH, NP, TRACE, false, NM, LR>(sk, ma, o, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
+    mic2_stages<NT, SH, NP, TRACE, false, NM, LR>(sk, ma, o, mu, tb, rpv, rdc, rpc, wrow, nullptr, nullptr, cntl[w], A, Bs,
                                                   row0, unit, unit_mf, ul, l, r, U, R, rl, snr, twd,
                                                   twd + MIC_NB * 24, nullptr, 0, nullptr, vcst);
     __syncthreads();
@@ -2887,7 +3000,9 @@ static StorePerfectDetect chain_detect(const SchemeK& sk, const McBuffers& b, co
 // pilot symbols, then k_mic_data over the others; see Mic2Args).
 bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
                     int niter) {
-    const bool fits = (long long)ch.ntap * ch.N * 16 < (1ll << 31) && (long long)sk.LK * b.U < (1ll << 62);
+    // (the data kernel's buffer view of Z: every stage's NT MIC_NB x U entries < 4 GB)
+    const bool fits = (long long)ch.ntap * ch.N * 16 < (1ll << 31) && (long long)sk.LK * b.U < (1ll << 62) &&
+                      (long long)(niter + 1) * 2 * MIC_NB * b.U * 16 < (1ll << 32);
     return op.mmse_ic == 1 && mm.Bv && mm.Bs && sk.pf_ok && sk.NP == 16 && pic_fft_shift(ch) >= 0 &&
            (b.U % 64) == 0 && (b.R % 64) == 0 && fits && mm.npb >= 1 && mm.npb <= 4 && mm.ndb >= 1 && b.hpa &&
            niter >= 1 && niter <= PM_MAXIT && b.hpa_stages >= niter + 1 && op.pic_chain == 3 &&
