@@ -12,7 +12,7 @@ for i in 0 1; do
   for v in base alt; do
     if [ $v = base ]; then cp /tmp/libdsce_base.so $lib; else cp ab/libdsce_alt.so $lib; fi
     timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/ab_${tag}_${v}_$i.log 2>&1 || { echo "fail $v"; tail -5 gpurun_out/ab_${tag}_${v}_$i.log; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernels_ms']; print(sys.argv[2], round(d['value']), {n: round(v['ms']/max(1,v['launches']),3) for n,v in k.items() if v['launches']})" gpurun_out/ab_${tag}_${v}_$i.log $v
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernels']; print(sys.argv[2], round(d['value']), {n: v['ms_per_step'] for n,v in k.items() if v.get('launches')})" gpurun_out/ab_${tag}_${v}_$i.log $v
   done
 done
 cp /tmp/libdsce_base.so $lib
