@@ -2251,10 +2251,38 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     // per lane, for diag(D_hat_s)); the data kernel prefetches both for stage
     // s + 1 at the end of stage s and folds hn4 into the window sums sn at once
     double2 hb[LR ? 1 : NP / 4], hn4[LR ? 1 : NP / 4];
-    // LR: Z of the previous stage (the taps) and of this stage (diag), whole unit per
-    // lane (the data kernel; the pilot kernel reads them from its LDS szz instead)
+    // LR: Z of this stage (diag, then the next stage's taps), whole unit per lane
+    // (the data kernel; the pilot kernel reads them from its LDS szz instead)
     constexpr int NZR = LR && !PIL ? NZ : 1;
-    double2 zp[NZR], zc[NZR];
+    double2 zc[NZR];
+    // LR data kernel: the next stage's estimated taps, formed at the end of a stage
+    // from its Z (r05: carrying the previous stage's Z instead cost 16 register
+    // copies per stage; the taps' live range ends in the chain, so the next
+    // stage's land in the same registers)
+    constexpr int NTL = LR && !PIL ? 6 : 1;
+    double2 ltp[NTL][NT];
+    auto lr_taps = [&](double2 (&tp)[6][NT], int sp, int ozz) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+            double tk[MIC_NB];
+#pragma unroll
+            for (int k = 0; k < MIC_NB; ++k) tk[k] = twl[k * 24 + 6 * cq + a + ozz];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                double2 zk[MIC_NB];
+#pragma unroll
+                for (int k = 0; k < MIC_NB; ++k)
+                    zk[k] = PIL ? szz[sp & 1][q * MIC_NB + k][ul] : zc[(q * MIC_NB + k) % NZR];
+                double2 t = make_double2(tk[0] * zk[0].x, tk[0] * zk[0].y);
+#pragma unroll
+                for (int k = 1; k < MIC_NB; ++k) {
+                    t.x = fma(tk[k], zk[k].x, t.x);
+                    t.y = fma(tk[k], zk[k].y, t.y);
+                }
+                tp[a][q] = t;
+            }
+        }
+    };
     // diag(D_hat_s) = qs gs sum_q w^(-l d_q) Bs_q(var_s) hP_s: window sums sn0 / sn1
     auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
         sn0 = sn1 = make_double2(0.0, 0.0);
@@ -2315,8 +2343,6 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         double2 sn0, sn1;
         if (LR && !PIL) {
 #pragma unroll
-            for (int j = 0; j < NZR; ++j) zp[j] = zc[j];
-#pragma unroll
             for (int j = 0; j < NZR; ++j) zc[j] = buf_ld2(rza, (unsigned)unit * 16u, (unsigned)((s * NZ + j) * U) * 16u);
         } else if (!LR && !PIL) {
 #pragma unroll
@@ -2329,28 +2355,11 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         } else {
             // the previous stage's estimated taps and their window sums
             double2 taps[6][NT];
-            if constexpr (LR) {
+            if constexpr (LR && !PIL) {
+                // formed at the end of stage s - 1 (ltp)
+            } else if constexpr (LR) {
                 // T_k of the lane's six samples (this symbol's window, quarter cq)
-#pragma unroll
-                for (int a = 0; a < 6; ++a) {
-                    double tk[MIC_NB];
-#pragma unroll
-                    for (int k = 0; k < MIC_NB; ++k) tk[k] = twl[k * 24 + 6 * cq + a + oz];
-#pragma unroll
-                    for (int q = 0; q < NT; ++q) {
-                        double2 zk[MIC_NB];
-#pragma unroll
-                        for (int k = 0; k < MIC_NB; ++k)
-                            zk[k] = PIL ? szz[(s - 1) & 1][q * MIC_NB + k][ul] : zp[(q * MIC_NB + k) % NZR];
-                        double2 t = make_double2(tk[0] * zk[0].x, tk[0] * zk[0].y);
-#pragma unroll
-                        for (int k = 1; k < MIC_NB; ++k) {
-                            t.x = fma(tk[k], zk[k].x, t.x);
-                            t.y = fma(tk[k], zk[k].y, t.y);
-                        }
-                        taps[a][q] = t;
-                    }
-                }
+                lr_taps(taps, s - 1, oz);
             } else {
                 if (PIL)
 #pragma unroll
@@ -2361,12 +2370,15 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             double2 x[6];
 #pragma unroll
             for (int a = 0; a < 6; ++a) x[a] = v[a];
-            mic_chain<NT, SH, NM>(x, taps, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
+            if constexpr (LR && !PIL)
+                mic_chain<NT, SH, NM>(x, ltp, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
+            else
+                mic_chain<NT, SH, NM>(x, taps, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
             // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
                 double2 hpv = sp0;
-                c_fma(hpv, wrow[4 * a + ro], sp1);
+                c_fma(hpv, sp1, wrow[4 * a + ro]);
                 ye[a] = c_sub(yv[a], x[p6(a)]);
                 c_fma(ye[a], hpv, v[a]);
             }
@@ -2414,7 +2426,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             hd[a] = sn0;
-            c_fma(hd[a], wrow[4 * a + ro], sn1);
+            c_fma(hd[a], sn1, wrow[4 * a + ro]);
         }
         sp0 = sn0;
         sp1 = sn1;
@@ -2450,6 +2462,13 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
             for (int a = 0; a < 6; ++a) v[a] = nv[a];
         }
         cntl[s] = wave_sum_dpp(valid ? ncnt : 0);  // uniform: every lane writes the same word
+        if constexpr (LR && !PIL) {
+            if (s < ma.niter) {
+                int oz2 = 0;
+                asm volatile("" : "+v"(oz2));
+                lr_taps(ltp, s, oz2);                // stage s + 1's taps from Z_s
+            }
+        }
         if (!LR && !PIL && s < ma.niter) {
             // stage s + 1's operands: hP_s (tap GEMM) and hP_{s+1} (diag)
             const double2* __restrict__ hs = ma.hpa + (size_t)s * NP * U;
@@ -2816,7 +2835,7 @@ k_txrx_fft(SchemeK sk, TxrxArgs ta, int xcd) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             double2 hv = s0;
-            c_fma(hv, wrow[4 * a + r], s1);
+            c_fma(hv, s1, wrow[4 * a + r]);
             if (ta.snr0 == 0) ta.h[(size_t)(row0 + 4 * a + r) * R + rl] = hv;
         }
     }
