@@ -2154,16 +2154,36 @@ struct Mic2Tables {
 // the decided symbol indices (first-minimum tie rule, SignalConstellation.m:88)
 __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6], const double2 (&hd)[6],
                                            const StorePerfectDetect& o, const unsigned char* sgrid) {
-    // z = ye / hd with the slicer scale folded into the reciprocal (r05: 15 FP64
-    // operations per row instead of c_div_fast's 16 and the two scale FMAs)
+    // z = ye / hd with the slicer scale folded into the reciprocals, and the six
+    // rows' 1 / |hd|^2 from ONE reciprocal (r05, batch inversion: prefix
+    // products, one recip_fast, two products per row back; 20 FP64 operations
+    // instead of 30).  A product outside [2^-1000, 2^1000] (a zero or vanishing
+    // estimate somewhere in the lane's rows) takes the per-row reciprocals.
+    double nn[6], pp[6], id[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) nn[a] = fma(hd[a].x, hd[a].x, hd[a].y * hd[a].y);
+    pp[0] = nn[0];
+#pragma unroll
+    for (int a = 1; a < 6; ++a) pp[a] = pp[a - 1] * nn[a];
+    double inv = recip_fast(pp[5]) * o.scI;                  // scI / prod
+#pragma unroll
+    for (int a = 5; a > 0; --a) {
+        id[a] = inv * pp[a - 1];                              // scI / nn[a]
+        inv *= nn[a];
+    }
+    id[0] = inv;
+    const bool ok = pp[5] > 0x1p-1000 && pp[5] < 0x1p1000;
+    if (__ballot(!ok)) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a) id[a] = ok ? id[a] : recip_fast(nn[a]) * o.scI;
+    }
     double fI[6], fQ[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
         const double2 b = hd[a], y = ye[a];
-        const double id = recip_fast(fma(b.x, b.x, b.y * b.y));
         const double nx = fma(y.x, b.x, y.y * b.y), ny = fma(y.y, b.x, -(y.x * b.y));
-        fI[a] = fma(nx, id * o.scI, o.ofI);
-        fQ[a] = fma(ny, id * o.scQ, o.ofQ);
+        fI[a] = fma(nx, id[a], o.ofI);
+        fQ[a] = fma(ny, id[a] * o.rQ, o.ofQ);
     }
     slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
 }
