@@ -168,6 +168,35 @@ def test_bench_kernels_trace_matches_oracle(ofdm):
     eng.set_option("mmse_ic", 1)
 
 
+def test_nonuniform_row_precoder_matches_oracle():
+    """A row-local precoder whose data rows carry different unit-modulus
+    factors (SchemeK::pv_uni 0): the non-uniform re-precode branch of k_pic_fft
+    and k_mic_data (row value x the staged constellation, the constant rows
+    from the lane's LDS slot, r05) against the oracle on the same P: counts
+    within the borderline bar, the FFT-form kernels ran (asserted)."""
+    import copy
+    from types import SimpleNamespace
+    S0 = harness.setup("default", schemes=("ofdm",))
+    S = SimpleNamespace(**vars(S0))
+    S.name = "default_pv_rotated"          # its own oracle_mmse cache entry
+    S.schemes = copy.deepcopy(S0.schemes)
+    sc = S.schemes["ofdm"]
+    NP = len(sc["pilot_pos"])
+    P = sc["P"].copy()
+    ph = np.exp(1j * np.pi / 4 * (np.arange(P.shape[1] - NP) % 3))
+    P[:, NP:] = P[:, NP:] * ph[None, :]
+    sc["P"] = P
+    eng = harness.engine(S, batch=256)
+    try:
+        cg = eng.run(SEED, 0, 64)
+        assert {"pic_fft", "mic_stages"} <= eng.path_info(0), eng.path_info(0)
+        res = harness.simulate(S, SEED, 0, 64, ["ofdm"])
+        assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
+        assert res["err"].sum() > 0
+    finally:
+        eng.close()
+
+
 def test_error_counts_match_oracle(ofdm):
     """Error counts and MSE sums through the bench path, 64 realisations x 7 SNR
     points (7 x 14 perfect-CSI chain blocks: not a multiple of the 8 XCDs) and
