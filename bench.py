@@ -73,6 +73,12 @@ KERNEL_DESC = {
                    "from k_mic_pilot), y - Q'(H_hat (G v)) + diag(D_hat) v by the DFT-24 chain, one-tap + detection; "
                    "FP64 roofline (VALU and MFMA share the issue)"),
     "k_mic_pilot": "k_mic_pilot: every MMSE stage of the pilot symbols, LS pilots and Z = Bz hP per stage",
+    "ic_stages": ("the IC group of every FFT-form OFDM symbol (stage 0 + 4 IC iterations, both CSI branches): "
+                  "k_pic_fft (perfect CSI, script:428-466 / :541-561) on a second stream beside k_mic_pilot -> "
+                  "k_mic_data (MMSE, script:417-537); per stage and symbol the DFT-24 chain (prime-factor DFT-6 "
+                  "per lane + the 4-point network on v_mfma_f64_4x4x4f64) with the true or the low-rank estimated "
+                  "taps, one-tap, slicer, counts; FP64 roofline (f64 VALU and MFMA share the SIMD's issue, 78.6 TF); "
+                  "time = the group's span on the engine's main stream (HIP events: fork before, join after)"),
     "rx_front": ("k_txrx_fft: TX IDFT-24, the doubly-selective channel, and per SNR point the AWGN draw (Philox4x32-10 "
                  "+ table-driven Box-Muller) and the receiver DFT-24"),
     "k_jakes": "k_jakes_grp: the Jakes sum-of-sinusoids taps at the samples the receiver windows read",
@@ -523,7 +529,7 @@ def main():
     step_flops = 0.0
     modelled_ms = 0.0
     for k in ("k_jakes", "tx", "rx_front", "k_pilot_pre", "k_wcontract", "k_mic_pilot", "k_mic_data",
-              "perfect_ic", "k_stage"):
+              "perfect_ic", "k_stage", "ic_stages"):
         n, ms = eng.kernel_time(k)
         if not n:
             continue
@@ -551,7 +557,26 @@ def main():
                 if lk:
                     ent["valu_issue"], ent["mfma_busy"], ent["limiter"] = lk["valu_issue"], lk["mfma_busy"], lk["limiter"]
         kernels[k] = ent
-    tot_ms = sum(eng.kernel_time(k)[1] for k in kernels)
+    # the FFT-form OFDM IC group (dsce option ic_streams): "ic_stages" spans
+    # k_pic_fft (second stream) beside k_mic_pilot -> k_mic_data; its members'
+    # own spans then overlap, so the step sums and the dominant-group choice use
+    # the group and the members are reported for the record only
+    members = ()
+    if kernels.get("ic_stages", {}).get("flops_per_rep") and eng.get_option("ic_streams") == 2:
+        members = ("perfect_ic", "k_mic_pilot", "k_mic_data")
+        for m in members:
+            if m in kernels:
+                kernels[m]["in_group"] = "ic_stages (overlapped: ic_streams 2)"
+        step_flops -= sum(kernels[m]["flops_per_rep"] * B for m in members if kernels.get(m, {}).get("flops_per_rep"))
+        modelled_ms -= sum(eng.kernel_time(m)[1] for m in members if kernels.get(m, {}).get("flops_per_rep"))
+    elif "ic_stages" in kernels:
+        # one stream: the members are the measured kernels, the group span only
+        # repeats their sum (not counted twice)
+        ent = kernels.pop("ic_stages")
+        if ent.get("flops_per_rep"):
+            step_flops -= ent["flops_per_rep"] * B
+            modelled_ms -= eng.kernel_time("ic_stages")[1]
+    tot_ms = sum(eng.kernel_time(k)[1] for k in kernels if k not in members)
     for k in kernels:
         kernels[k]["share"] = round(eng.kernel_time(k)[1] / tot_ms, 4) if tot_ms else None
     step_ms = el / args.steps * 1e3
@@ -564,7 +589,8 @@ def main():
     # on the engine's stream) among those with a work model (C2's
     # perfect-CSI chain k_pic_fft became the largest in r04)
     paths = [eng.path_info(sid) for sid in range(len(schemes))]
-    kname = max((k for k in kernels if kernels[k].get("flops_per_rep")), key=lambda k: kernels[k]["ms_per_step"])
+    kname = max((k for k in kernels if kernels[k].get("flops_per_rep") and k not in members),
+                key=lambda k: kernels[k]["ms_per_step"])
     launches, k_ms = eng.kernel_time(kname)
     avg_ms = k_ms / launches if launches else None
     peak_meas = eng.fp64_mfma_peak()
@@ -594,6 +620,11 @@ def main():
         kp = (pmc_all or {}).get(kname)
         pmc = {"sq_per_launch": kp.get("sq_per_launch"), "hbm_bytes_per_launch": kp.get("hbm_bytes_per_launch"),
                "avg_duration_ns_rocprof": kp.get("avg_duration_ns_rocprof")} if kp else None
+        if pmc and kname == "ic_stages":
+            # a concurrent group: its counters are the members' isolated counts
+            # (the --pmc passes serialise dispatches), so the limiter describes
+            # the members' mix; the profiler's wall span is the trace's
+            pmc["avg_duration_ns_rocprof"] = None
         traffic_src = pmc_all_src
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     lim = derive_limiter(pmc, roof_tf, avg_ms)
@@ -673,7 +704,10 @@ def main():
                      "limiter": lim["limiter"] if lim else None,
                      "counters": lim,
                      # the next largest kernel group, for the record
-                     "next_by_time": dominant_by_time({k: v for k, v in kernels.items() if k != kname}, None)},
+                     "next_by_time": dominant_by_time({k: v for k, v in kernels.items() if k != kname and k not in members},
+                                                      None),
+                     "group_members": {m: kernels[m] for m in members if m in kernels} if kname == "ic_stages" else None,
+                     "rocprof_span_ms": ((pmc_all or {}).get(kname, {}).get("span_ns_rocprof_trace") or 0) / 1e6 or None},
         "cpu_baseline": cpu,
         "allreduce": allreduce,
         "setup_s": setup_s,

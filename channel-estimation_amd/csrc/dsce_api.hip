@@ -147,6 +147,10 @@ using namespace dsce;
 struct dsce_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // Opts::ic_streams 2: the perfect-CSI chain runs on stream2 beside the MMSE
+    // kernels (fork / join events on the main stream), created on first use
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool chan_set = false;
     ChannelK ch{};
@@ -1490,19 +1494,42 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 // the low-rank tap operator (both passes or neither: the data pass
                 // reads the pilot pass's Z instead of its LS pilots)
                 const bool lr = op.mic_lr && (op.mic_net & 1) && s.Bz;
+                // Opts::ic_streams 2 (r05): the perfect-CSI chain (issue-bound)
+                // on the second stream beside the MMSE pilot pass (latency-bound,
+                // 0.65 issue) and data pass; "ic_stages" spans the group on the
+                // main stream (fork before, join after), the per-kernel spans of
+                // the three then include their contention
+                const bool two = op.ic_streams == 2;
                 {
-                    Timed t(c, "perfect_ic");
-                    s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, true);
-                }
-                {
-                    Timed t(c, "k_mic_pilot");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1, (op.mic_net & 2) != 0,
-                                                 lr);
-                }
-                {
-                    Timed t(c, "k_mic_data");
-                    s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2, (op.mic_net & 1) != 0,
-                                                 lr);
+                    Timed tg(c, "ic_stages");
+                    if (two) {
+                        if (!c->stream2) {
+                            DSCE_HIP_CHECK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+                            DSCE_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+                            DSCE_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+                        }
+                        DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
+                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+                    }
+                    {
+                        Timed t(c, "perfect_ic", two ? c->stream2 : nullptr);
+                        s.path |= launch_perfect_chain(two ? c->stream2 : c->stream, op, s.k, c->ch, b, &pd, c->niter,
+                                                       true);
+                    }
+                    {
+                        Timed t(c, "k_mic_pilot");
+                        s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1,
+                                                     (op.mic_net & 2) != 0, lr);
+                    }
+                    {
+                        Timed t(c, "k_mic_data");
+                        s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2,
+                                                     (op.mic_net & 1) != 0, lr);
+                    }
+                    if (two) {
+                        DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
+                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
+                    }
                 }
                 if (to && to->hp_stages)
                     for (int st = 0; st <= c->niter; ++st)
@@ -1628,6 +1655,17 @@ struct KWork {
 
 KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
     KWork w;
+    if (name == "ic_stages") {
+        // the concurrent group of the FFT-form OFDM path (Opts::ic_streams 2):
+        // k_pic_fft on the second stream beside k_mic_pilot -> k_mic_data
+        if (!(s.path & PATH_MIC_STAGES)) return w;
+        for (const char* g : {"perfect_ic", "k_mic_pilot", "k_mic_data"}) {
+            const KWork x = kernel_work(c, s, g);
+            w.flops += x.flops;
+            w.bytes += x.bytes;
+        }
+        return w;
+    }
     const double nt = c->ch.ntap, NP = s.d.n_pilots, ns = c->nsnr, it = c->niter, LK = s.LK;
     const double DFT = 5.0 * 24.0 * std::log2(24.0);
     const bool fft = (s.path & PATH_MIC_STAGES) != 0;
@@ -1761,6 +1799,7 @@ int dsce_destroy(dsce_ctx* ctx) {
     };
     note(hipSetDevice(ctx->device), "hipSetDevice");
     if (ctx->stream) note(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (ctx->stream2) note(hipStreamSynchronize(ctx->stream2), "hipStreamSynchronize (stream2)");
     for (void* p : ctx->buf_allocs) note(hipFree(p), "hipFree (batch buffers)");
     for (void* p : ctx->allocs) note(hipFree(p), "hipFree (operators)");
     for (auto& e : ctx->pending) {
@@ -1768,6 +1807,9 @@ int dsce_destroy(dsce_ctx* ctx) {
         note(hipEventDestroy(e.b), "hipEventDestroy");
     }
     for (auto e : ctx->event_pool) note(hipEventDestroy(e), "hipEventDestroy (pool)");
+    if (ctx->ev_fork) note(hipEventDestroy(ctx->ev_fork), "hipEventDestroy (fork)");
+    if (ctx->ev_join) note(hipEventDestroy(ctx->ev_join), "hipEventDestroy (join)");
+    if (ctx->stream2) note(hipStreamDestroy(ctx->stream2), "hipStreamDestroy (stream2)");
     if (ctx->stream) note(hipStreamDestroy(ctx->stream), "hipStreamDestroy");
     delete ctx;
     if (first) fprintf(stderr, "dsce_destroy: %s failed: %s\n", first, hipGetErrorString(ferr));
@@ -2419,7 +2461,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr) X(pic_poly) X(wrow)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr) X(pic_poly) X(wrow) X(ic_streams)
 
 int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN
@@ -2437,6 +2479,7 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
         throw ApiError(DSCE_EINVAL, "pic_chain: 0 (per-iteration passes) | 3 (k_pic_fft); the r01 chains 1 / 2 "
                                     "(k_pic_chain, k_pic_mfma) were retired in r03");
     if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
+    if (n == "ic_streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "ic_streams: 1 | 2");
     if (n == "snr_base") check_noise_streams(ctx, value, ctx->nsnr, max_noise_slot(ctx));
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;

@@ -40,6 +40,9 @@ struct Opts {
                               // L != 24) as IDFT-L per symbol + window sums per residue + DFT-L per symbol
                               // (k_poly_syn / k_poly_chan / k_poly_ana) instead of the two banded passes
                               // (r04 box, C3: 14.3 -> 8.7 ms per iteration); 0 = the banded passes
+    int ic_streams = 1;       // FFT-form OFDM: 2 = k_pic_fft on a second stream beside k_mic_pilot / k_mic_data
+                              // (r05 same-box A/Bs: 7.06-7.20 -> 6.87-6.90 ms per C2 step on one box, 6.77 ->
+                              // 6.83 on another: box-dependent, and it blurs the per-kernel spans); 1 = one stream
     int wrow = 1;             // unfused W contraction of 32-row blocks (FBMC, C5) as one GEMM per row tile
                               // (k_wrow3: X = hP v_c as the B operand, no per-tile epilogue); 0 = k_wpair3
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows

@@ -337,7 +337,12 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes),
  *   wrow (1: the unfused W contraction of 32-row blocks — FBMC, C5 — as one
  *   GEMM per 16-row tile over (column, pilot) with B = hP v_c, no per-tile
- *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles).
+ *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles), ic_streams (2: on
+ *   the FFT-form OFDM path the perfect-CSI chain k_pic_fft runs on the
+ *   context's second stream beside k_mic_pilot -> k_mic_data, forked after the
+ *   receiver front and joined before the counters, the per-kernel spans then
+ *   overlap; 1, the default: one stream, the three in sequence; either way
+ *   dsce_kernel_time's "ic_stages" spans the group).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */
@@ -346,7 +351,9 @@ int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, dsce_run records HIP events around every launch of each kernel
- * on the context's stream; dsce_kernel_time returns (launches, total ms). */
+ * on the stream it runs on; dsce_kernel_time returns (launches, total ms).
+ * "ic_stages" is the span of the FFT-form OFDM IC group on the main stream
+ * (k_pic_fft with ic_streams 2 on the second stream, k_mic_pilot, k_mic_data). */
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
 /* Algorithmic work of one realisation of a scheme (support-aware): complex
@@ -361,7 +368,8 @@ int dsce_work_model(dsce_ctx* ctx, int32_t scheme_id, double* wcontract_cmac_per
  * n-point DFT; transcendentals and RNG integer work not counted) and the
  * compulsory HBM bytes (each operand read once per realisation / unit, each
  * result written once).  Modelled: the FFT-form OFDM chain (k_jakes, tx,
- * rx_front, perfect_ic, k_mic_pilot, k_mic_data), the polyphase perfect-CSI
+ * rx_front, perfect_ic, k_mic_pilot, k_mic_data, and ic_stages = the sum of the
+ * last three), the polyphase perfect-CSI
  * passes (perfect_ic of FBMC / L = 48 OFDM) and the W contraction (k_wcontract);
  * 0 = not modelled for the path that ran.  DESIGN.md section 4
  * lists the per-unit formulas. */

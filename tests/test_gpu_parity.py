@@ -500,7 +500,7 @@ def test_stage_variants_agree(name):
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
                 {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 1},
-                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0})
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0}, {"ic_streams": 1})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():

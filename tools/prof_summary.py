@@ -66,6 +66,26 @@ def short(name):
     return n[:n.index("(")] if "(" in n else n
 
 
+def group_span(sdir):
+    """Mean span (ns) of the i-th k_pic_fft / k_mic_pilot / k_mic_data dispatch
+    triple in the stats run's kernel trace: first start to last end."""
+    try:
+        tr = one(os.path.join(sdir, "**", "*_kernel_trace.csv"))
+    except Exception:
+        return None
+    seq = {"k_pic_fft": [], "k_mic_pilot": [], "k_mic_data": []}
+    for r in csv.DictReader(open(tr)):
+        n = r["Kernel_Name"]
+        for k in seq:
+            if k in n:
+                seq[k].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    m = min(len(v) for v in seq.values())
+    if not m:
+        return None
+    spans = [max(seq[k][i][1] for k in seq) - min(seq[k][i][0] for k in seq) for i in range(m)]
+    return sum(spans) / len(spans)
+
+
 def main_all(argv):
     tag, sdir, fdir, wdir, workload = argv[:5]
     sqdir = argv[5] if len(argv) > 5 else None
@@ -96,10 +116,23 @@ def main_all(argv):
         e["avg_duration_ns_rocprof"] += avg.get(k, 0.0)
         for c in sq:
             e["sq_per_launch"][c] += sq[c].get(k, 0.0)
+    # the concurrent IC group of the FFT-form OFDM path (ic_streams 2): its
+    # members' counters (the --pmc passes serialise the dispatches, so these are
+    # the kernels' isolated counts) and, from the stats run's kernel trace, the
+    # mean span first start -> last end of each (pic, pilot, data) triple
+    mem = [g for g in ("perfect_ic", "k_mic_pilot", "k_mic_data") if g in groups]
+    if len(mem) == 3 and any("k_pic_fft" in k for k in groups["perfect_ic"]["kernels"]):
+        e = {"kernels": sum((groups[g]["kernels"] for g in mem), []), "members": mem}
+        for key in ("fetch_size_kb_per_launch", "write_size_kb_per_launch", "avg_duration_ns_rocprof"):
+            e[key] = sum(groups[g][key] for g in mem)
+        if sq:
+            e["sq_per_launch"] = {c: sum(groups[g]["sq_per_launch"][c] for g in mem) for c in sq}
+        e["span_ns_rocprof_trace"] = group_span(sdir)
+        groups["ic_stages"] = e
     for e in groups.values():
         e["hbm_bytes_per_launch"] = (2 * e["fetch_size_kb_per_launch"] + e["write_size_kb_per_launch"]) * 1024
         if not sq:
-            del e["sq_per_launch"]
+            e.pop("sq_per_launch", None)
     res = {"workload": workload, "source_hash": source_hash(), "kernels": groups,
            "correction": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE reports half of "
                          "wide coalesced reads, MI355X_MICROARCH.md §HBM)"}
