@@ -562,11 +562,13 @@ def main():
     # own spans then overlap, so the step sums and the dominant-group choice use
     # the group and the members are reported for the record only
     members = ()
-    if kernels.get("ic_stages", {}).get("flops_per_rep") and eng.get_option("ic_streams") == 2:
+    ics = eng.get_option("ic_streams")
+    if kernels.get("ic_stages", {}).get("flops_per_rep") and ics in (2, 3):
         members = ("perfect_ic", "k_mic_pilot", "k_mic_data")
         for m in members:
             if m in kernels:
-                kernels[m]["in_group"] = "ic_stages (overlapped: ic_streams 2)"
+                kernels[m]["in_group"] = "ic_stages (ic_streams %d: %s)" % (
+                    ics, "overlapped" if ics == 2 else "chain + pilot pass in one launch, k_ic_pair")
         step_flops -= sum(kernels[m]["flops_per_rep"] * B for m in members if kernels.get(m, {}).get("flops_per_rep"))
         modelled_ms -= sum(eng.kernel_time(m)[1] for m in members if kernels.get(m, {}).get("flops_per_rep"))
     elif "ic_stages" in kernels:

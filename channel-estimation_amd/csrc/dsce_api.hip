@@ -1500,6 +1500,9 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 // main stream (fork before, join after), the per-kernel spans of
                 // the three then include their contention
                 const bool two = op.ic_streams == 2;
+                // Opts::ic_streams 3 (r05): the chain and the pilot pass in one
+                // launch (k_ic_pair, "ic_pair"), then the data pass
+                const bool pair = op.ic_streams == 3 && ic_pair_ok(op, s.k, mm, b, lr);
                 {
                     Timed tg(c, "ic_stages");
                     if (two) {
@@ -1511,12 +1514,15 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                         DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
                         DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
                     }
-                    {
-                        Timed t(c, "perfect_ic", two ? c->stream2 : nullptr);
-                        s.path |= launch_perfect_chain(two ? c->stream2 : c->stream, op, s.k, c->ch, b, &pd, c->niter,
-                                                       true);
-                    }
-                    {
+                    if (pair) {
+                        Timed t(c, "ic_pair");
+                        s.path |= launch_ic_pair(c->stream, op, s.k, mm, c->ch, b, &pd, c->niter, lr);
+                    } else {
+                        {
+                            Timed t(c, "perfect_ic", two ? c->stream2 : nullptr);
+                            s.path |= launch_perfect_chain(two ? c->stream2 : c->stream, op, s.k, c->ch, b, &pd,
+                                                           c->niter, true);
+                        }
                         Timed t(c, "k_mic_pilot");
                         s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1,
                                                      (op.mic_net & 2) != 0, lr);
@@ -2479,7 +2485,7 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
         throw ApiError(DSCE_EINVAL, "pic_chain: 0 (per-iteration passes) | 3 (k_pic_fft); the r01 chains 1 / 2 "
                                     "(k_pic_chain, k_pic_mfma) were retired in r03");
     if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
-    if (n == "ic_streams" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "ic_streams: 1 | 2");
+    if (n == "ic_streams" && (value < 1 || value > 3)) throw ApiError(DSCE_EINVAL, "ic_streams: 1 | 2 | 3");
     if (n == "snr_base") check_noise_streams(ctx, value, ctx->nsnr, max_noise_slot(ctx));
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;

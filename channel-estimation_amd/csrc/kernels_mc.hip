@@ -885,10 +885,9 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-__device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug, int& blk) {
-    int L = blockIdx.x;
+__device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug, int& blk, int L, int n) {
     if (o.xcd) {
-        L = xcd_remap(L, gridDim.x);
+        L = xcd_remap(L, n);
         const int sn = L % o.nchunk, rest = L / o.nchunk;
         blk = rest % nblk;
         ug = sn * o.rgs + rest / nblk;
@@ -896,6 +895,9 @@ __device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug
         ug = L % o.nug;
         blk = L / o.nug;
     }
+}
+__device__ __forceinline__ void band_block(const BandOrder& o, int nblk, int& ug, int& blk) {
+    band_block(o, nblk, ug, blk, blockIdx.x, gridDim.x);
 }
 
 template <class In, class Out>
@@ -1684,11 +1686,13 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // (7 FP64 operations per row).  Re-precoded decisions read the scaled
 // constellation; the constant rows of u (pilots) are per-lane LDS slots read
 // through the same address select, so a row's new u is one LDS read.
-template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false, bool SKIP = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
+// (the body of k_pic_fft and of k_ic_pair's chain blocks: vb / vn = the block's
+// index in the chain's own grid and that grid's size, vb % 8 = the XCD)
+template <int NT, int SH, bool TRACE, bool S0, bool NM, bool SKIP>
+__device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder& ord, const double2* __restrict__ ir, int N,
+                                             const StorePerfectDetect& o, int niter, int vb, int vn) {
     int ug, blk;
-    band_block(ord, sk.QH.nblk, ug, blk);
+    band_block(ord, sk.QH.nblk, ug, blk, vb, vn);
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, r = NM ? l >> 4 : l & 3;
     const int U = o.U, R = o.R;
     const int unit = ug * WAVE + w * 16 + (NM ? (l & 15) : (l >> 2));
@@ -1980,6 +1984,12 @@ k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, Stor
         const size_t i0 = o.cidx0 + (size_t)it + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
         if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
     }
+}
+
+template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false, bool SKIP = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
+    pic_fft_body<NT, SH, TRACE, S0, NM, SKIP>(sk, ord, ir, N, o, niter, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -2604,8 +2614,10 @@ __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, doub
 }
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
-template <int NT, int SH, int NP, bool TRACE, bool NM = false, bool LR = false>
-__global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
+// (the body of k_mic_pilot and of k_ic_pair's pilot blocks: vb / vn as pic_fft_body's)
+template <int NT, int SH, int NP, bool TRACE, bool NM, bool LR>
+__device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o, int vb,
+                                               int vn) {
     constexpr int NZ = NT * MIC_NB;
     __shared__ Mic2Tables tb;
     __shared__ double2 rpv[4][24], wrow[4][24];
@@ -2626,7 +2638,7 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
     // HBM bytes per launch)
     int ug16;
     {
-        const int L = xcd_remap(blockIdx.x, gridDim.x), nch = o.U / o.R;
+        const int L = xcd_remap(vb, vn), nch = o.U / o.R;
         ug16 = (L % nch) * (o.R / 16) + L / nch;
     }
     const int ul = NM ? l & 15 : l >> 2;
@@ -2685,6 +2697,32 @@ __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, Stor
         const size_t i0 = o.cidx0 + (size_t)s + (size_t)snr * o.cstride_snr + (edge ? (size_t)o.cstride_edge : 0);
         if (v) atomicAdd(&o.counters[i0], (unsigned long long)v);
     }
+}
+
+template <int NT, int SH, int NP, bool TRACE, bool NM = false, bool LR = false>
+__global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
+    mic_pilot_body<NT, SH, NP, TRACE, NM, LR>(sk, ma, o, blockIdx.x, gridDim.x);
+}
+
+// The perfect-CSI chain (k_pic_fft, stage 0 included, matrix-core network) and
+// the MMSE pilot pass (k_mic_pilot, 256 threads) in ONE launch (Opts::ic_streams
+// 3): the two are independent, the chain issue-bound (VALU + MFMA 0.86 busy), the
+// pilot pass latency-bound (two barriers per stage, 0.65 busy), so a CU holding
+// a block of each fills the pilot blocks' stalls with chain work.  The grid is
+// cut into groups of 8 blocks (one per XCD); the groups are dealt to the two
+// passes evenly (Bresenham), and inside each pass group g, block x has the
+// pass-local index 8 g + x: the same XCD as in the pass's own launch, so its
+// XCD-contiguous order (xcd_remap) holds.  LDS: both bodies' tables (static).
+template <int NT, int SH, bool PNM, bool LR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_ic_pair(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect op, int niter,
+          Mic2Args ma, StorePerfectDetect om, int npic8, int npil8) {
+    const int G = blockIdx.x >> 3, x = blockIdx.x & 7, ng = npic8 + npil8;
+    const int q0 = (int)((long long)G * npil8 / ng), q1 = (int)((long long)(G + 1) * npil8 / ng);
+    if (q1 > q0)
+        mic_pilot_body<NT, SH, 16, false, PNM, LR>(sk, ma, om, q0 * 8 + x, npil8 * 8);
+    else
+        pic_fft_body<NT, SH, false, true, true, false>(sk, ord, ir, N, op, niter, (G - q0) * 8 + x, npic8 * 8);
 }
 
 // 64 units x one data symbol per block (4 waves x 16 units)
@@ -3048,9 +3086,8 @@ bool mmse_stages_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const Ch
            pic_fft_ok(op, sk, ch, b, niter) && (long long)(niter + 1) * sk.NP * b.U < (1ll << 40);
 }
 
-unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
-                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm, bool lr) {
-    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
+static Mic2Args mic2_args(const SchemeK& sk, const MmseK& mm, const ChannelK& ch, const McBuffers& b,
+                          const PerfectDetectArgs* pd, int niter) {
     Mic2Args ma{};
     ma.bv = mm.Bv;
     ma.bs = mm.Bs;
@@ -3066,6 +3103,15 @@ unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, c
     ma.za = b.za;
     ma.tw = mm.Tw;
     ma.ts = mm.Ts;
+    ma.blks = mm.pblk;
+    ma.nb = mm.npb;
+    return ma;
+}
+
+unsigned launch_mmse_stages(hipStream_t s, const SchemeK& sk, const MmseK& mm, const ChannelK& ch, McBuffers& b,
+                            const PerfectDetectArgs* pd, int niter, int xcd, int part, bool nm, bool lr) {
+    StorePerfectDetect o = chain_detect(sk, b, pd, 0);
+    Mic2Args ma = mic2_args(sk, mm, ch, b, pd, niter);
     // the low-rank operator: built (build_mic_lr), MIC_NB pilot symbols, Z buffer;
     // the data pass on the matrix-core network (the caller requires mic_net bit 0)
     const bool use_lr = lr && mm.Bz && mm.Tw && mm.Ts && b.za && mm.npb == MIC_NB;
@@ -3161,6 +3207,38 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
 #undef LAUNCH_PF2
 #undef LAUNCH_PF
     return PATH_PIC_FFT;
+}
+
+// k_ic_pair (Opts::ic_streams 3): the perfect-CSI chain with its stage 0 and the
+// MMSE pilot pass in one launch; the variant the C2 path runs (matrix-core
+// networks, low-rank taps, 4 pilot symbols, no trace, no fixed-point exit) and
+// both grids in whole 8-block groups.  Otherwise the caller launches the two.
+bool ic_pair_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b, bool lr) {
+    const long long npic = (long long)(b.U / WAVE) * sk.QH.nblk, npil = b.U / 16;
+    return op.pic_net && !op.pic_skip && !b.tr && lr && (op.mic_net & 2) && mm.npb == 4 && mm.Bz && mm.Tw &&
+           mm.Ts && b.za && npic % 8 == 0 && npil % 8 == 0 && npic + npil < (1ll << 31);
+}
+
+unsigned launch_ic_pair(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch,
+                        McBuffers& b, const PerfectDetectArgs* pd, int niter, bool lr) {
+    if (!ic_pair_ok(op, sk, mm, b, lr) || !pic_fft_ok(op, sk, ch, b, niter))
+        throw std::logic_error("launch_ic_pair: not eligible (ic_pair_ok / pic_fft_ok)");
+    StorePerfectDetect op_ = chain_detect(sk, b, pd, 1);
+    op_.skip = 0;
+    if (!(op_.scI != 0.0)) throw std::logic_error("launch_ic_pair: the chain's slicer scale is zero");
+    const StorePerfectDetect om = chain_detect(sk, b, pd, 0);
+    const Mic2Args ma = mic2_args(sk, mm, ch, b, pd, niter);
+    const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
+    const int npic8 = (int)((long long)(b.U / WAVE) * sk.QH.nblk / 8), npil8 = (b.U / 16) / 8;
+    const dim3 grid(8 * (npic8 + npil8)), blk(256);
+    const int sh = pic_fft_shift(ch);
+    if (ch.ntap == 1)
+        hipLaunchKernelGGL((k_ic_pair<1, 0, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
+    else if (sh == 1)
+        hipLaunchKernelGGL((k_ic_pair<2, 1, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
+    else
+        hipLaunchKernelGGL((k_ic_pair<2, 2, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
+    return PATH_PIC_FFT | PATH_MIC_FFT | PATH_MIC_STAGES | PATH_MIC_LR;
 }
 
 // ---------------------------------------------------------------------------

@@ -341,8 +341,11 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   the FFT-form OFDM path the perfect-CSI chain k_pic_fft runs on the
  *   context's second stream beside k_mic_pilot -> k_mic_data, forked after the
  *   receiver front and joined before the counters, the per-kernel spans then
- *   overlap; 1, the default: one stream, the three in sequence; either way
- *   dsce_kernel_time's "ic_stages" spans the group).
+ *   overlap; 3: the chain and the pilot pass in one launch, k_ic_pair —
+ *   timed as "ic_pair" — then k_mic_data, where the variant exists (matrix-
+ *   core networks, low-rank taps, 4 pilot symbols, no trace, no pic_skip;
+ *   else as 1); 1, the default: one stream, the three in sequence; in every
+ *   case dsce_kernel_time's "ic_stages" spans the group).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */
@@ -353,7 +356,8 @@ int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 /* When enabled, dsce_run records HIP events around every launch of each kernel
  * on the stream it runs on; dsce_kernel_time returns (launches, total ms).
  * "ic_stages" is the span of the FFT-form OFDM IC group on the main stream
- * (k_pic_fft with ic_streams 2 on the second stream, k_mic_pilot, k_mic_data). */
+ * (k_pic_fft with ic_streams 2 on the second stream, k_mic_pilot, k_mic_data;
+ * with ic_streams 3 "ic_pair" = k_ic_pair, then k_mic_data). */
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
 /* Algorithmic work of one realisation of a scheme (support-aware): complex

@@ -482,7 +482,9 @@ def test_stage_variants_agree(name):
     perfect-CSI passes banded instead of polyphase (pic_poly 0; FBMC) and
     polyphase for OFDM too (pic_poly 1 with pic_chain 0: OFDM's chain is
     otherwise k_pic_fft), the FBMC contraction as k_wpair3's pair tiles instead
-    of k_wrow3's row-tile GEMM (wrow 0)."""
+    of k_wrow3's row-tile GEMM (wrow 0), the perfect-CSI chain on a second
+    stream (ic_streams 2) or in one launch with the MMSE pilot pass (k_ic_pair,
+    ic_streams 3; with mic_lr 0 it falls back to the two launches)."""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -500,7 +502,8 @@ def test_stage_variants_agree(name):
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
                 {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 1},
-                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0}, {"ic_streams": 1})
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0}, {"ic_streams": 2},
+                {"ic_streams": 3}, {"ic_streams": 3, "mic_lr": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
