@@ -557,23 +557,11 @@ def main():
                 if lk:
                     ent["valu_issue"], ent["mfma_busy"], ent["limiter"] = lk["valu_issue"], lk["mfma_busy"], lk["limiter"]
         kernels[k] = ent
-    # the FFT-form OFDM IC group (dsce option ic_streams): "ic_stages" spans
-    # k_pic_fft (second stream) beside k_mic_pilot -> k_mic_data; its members'
-    # own spans then overlap, so the step sums and the dominant-group choice use
-    # the group and the members are reported for the record only
+    # the FFT-form OFDM IC group: "ic_stages" spans k_pic_fft -> k_mic_pilot ->
+    # k_mic_data on the one stream, so it only repeats its members' sum (not
+    # counted twice; r06 retired the overlapping ic_streams variants)
     members = ()
-    ics = eng.get_option("ic_streams")
-    if kernels.get("ic_stages", {}).get("flops_per_rep") and ics in (2, 3):
-        members = ("perfect_ic", "k_mic_pilot", "k_mic_data")
-        for m in members:
-            if m in kernels:
-                kernels[m]["in_group"] = "ic_stages (ic_streams %d: %s)" % (
-                    ics, "overlapped" if ics == 2 else "chain + pilot pass in one launch, k_ic_pair")
-        step_flops -= sum(kernels[m]["flops_per_rep"] * B for m in members if kernels.get(m, {}).get("flops_per_rep"))
-        modelled_ms -= sum(eng.kernel_time(m)[1] for m in members if kernels.get(m, {}).get("flops_per_rep"))
-    elif "ic_stages" in kernels:
-        # one stream: the members are the measured kernels, the group span only
-        # repeats their sum (not counted twice)
+    if "ic_stages" in kernels:
         ent = kernels.pop("ic_stages")
         if ent.get("flops_per_rep"):
             step_flops -= ent["flops_per_rep"] * B

@@ -12,7 +12,10 @@
 #include <stdexcept>
 #include <string>
 #include <cstdio>
+#include <thread>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "dsce.h"
 #include "dsce_kernels.h"
@@ -147,10 +150,6 @@ using namespace dsce;
 struct dsce_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    // Opts::ic_streams 2: the perfect-CSI chain runs on stream2 beside the MMSE
-    // kernels (fork / join events on the main stream), created on first use
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string err;
     bool chan_set = false;
     ChannelK ch{};
@@ -184,6 +183,13 @@ struct dsce_ctx {
     };
     std::vector<Ev> pending;
     std::vector<hipEvent_t> event_pool;
+    // multi-device context (dsce_create_multi, ABI 7): this context is member 0,
+    // peers are members 1.. (one context each, configured identically); comms:
+    // one RCCL communicator per member (ncclCommInitAll) when the devices are
+    // distinct; reduce: DSCE_REDUCE_* (how dsce_run sums the members' counters)
+    std::vector<dsce_ctx*> peers;
+    std::vector<ncclComm_t> comms;
+    int reduce = DSCE_REDUCE_NONE;
 };
 
 namespace {
@@ -1494,35 +1500,16 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                 // the low-rank tap operator (both passes or neither: the data pass
                 // reads the pilot pass's Z instead of its LS pilots)
                 const bool lr = op.mic_lr && (op.mic_net & 1) && s.Bz;
-                // Opts::ic_streams 2 (r05): the perfect-CSI chain (issue-bound)
-                // on the second stream beside the MMSE pilot pass (latency-bound,
-                // 0.65 issue) and data pass; "ic_stages" spans the group on the
-                // main stream (fork before, join after), the per-kernel spans of
-                // the three then include their contention
-                const bool two = op.ic_streams == 2;
-                // Opts::ic_streams 3 (r05): the chain and the pilot pass in one
-                // launch (k_ic_pair, "ic_pair"), then the data pass
-                const bool pair = op.ic_streams == 3 && ic_pair_ok(op, s.k, mm, b, lr);
+                // (r06: the r05 options ic_streams 2 / 3 — the chain on a second
+                // stream, or beside the pilot pass in one launch, k_ic_pair — were
+                // within box noise and are retired; "ic_stages" spans the group)
                 {
                     Timed tg(c, "ic_stages");
-                    if (two) {
-                        if (!c->stream2) {
-                            DSCE_HIP_CHECK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-                            DSCE_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-                            DSCE_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-                        }
-                        DSCE_HIP_CHECK(hipEventRecord(c->ev_fork, c->stream));
-                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream2, c->ev_fork, 0));
+                    {
+                        Timed t(c, "perfect_ic");
+                        s.path |= launch_perfect_chain(c->stream, op, s.k, c->ch, b, &pd, c->niter, true);
                     }
-                    if (pair) {
-                        Timed t(c, "ic_pair");
-                        s.path |= launch_ic_pair(c->stream, op, s.k, mm, c->ch, b, &pd, c->niter, lr);
-                    } else {
-                        {
-                            Timed t(c, "perfect_ic", two ? c->stream2 : nullptr);
-                            s.path |= launch_perfect_chain(two ? c->stream2 : c->stream, op, s.k, c->ch, b, &pd,
-                                                           c->niter, true);
-                        }
+                    {
                         Timed t(c, "k_mic_pilot");
                         s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 1,
                                                      (op.mic_net & 2) != 0, lr);
@@ -1531,10 +1518,6 @@ void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Tra
                         Timed t(c, "k_mic_data");
                         s.path |= launch_mmse_stages(c->stream, s.k, mm, c->ch, b, &pd, c->niter, op.xcd, 2,
                                                      (op.mic_net & 1) != 0, lr);
-                    }
-                    if (two) {
-                        DSCE_HIP_CHECK(hipEventRecord(c->ev_join, c->stream2));
-                        DSCE_HIP_CHECK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
                     }
                 }
                 if (to && to->hp_stages)
@@ -1662,8 +1645,7 @@ struct KWork {
 KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
     KWork w;
     if (name == "ic_stages") {
-        // the concurrent group of the FFT-form OFDM path (Opts::ic_streams 2):
-        // k_pic_fft on the second stream beside k_mic_pilot -> k_mic_data
+        // the IC group of the FFT-form OFDM path: k_pic_fft, k_mic_pilot, k_mic_data
         if (!(s.path & PATH_MIC_STAGES)) return w;
         for (const char* g : {"perfect_ic", "k_mic_pilot", "k_mic_data"}) {
             const KWork x = kernel_work(c, s, g);
@@ -1761,6 +1743,67 @@ KWork kernel_work(const dsce_ctx* c, const Scheme& s, const std::string& name) {
 
 }  // namespace
 
+// ---- multi-device contexts (dsce_create_multi, ABI 7) -----------------------
+#define DSCE_NCCL_CHECK(x)                                                                             \
+    do {                                                                                               \
+        const ncclResult_t r_ = (x);                                                                   \
+        if (r_ != ncclSuccess)                                                                         \
+            throw ApiError(DSCE_EHIP, std::string("RCCL error '") + ncclGetErrorString(r_) + "' (" #x ")"); \
+    } while (0)
+
+static dsce_ctx* member(dsce_ctx* ctx, size_t m) { return m ? ctx->peers[m - 1] : ctx; }
+
+static std::string member_name(const dsce_ctx* ctx, size_t m) {
+    const dsce_ctx* c = m ? ctx->peers[m - 1] : ctx;
+    return "member " + std::to_string(m) + " (device " + std::to_string(c->device) + ")";
+}
+
+// A configuration call on a multi-device context runs on every member, member 0
+// first (it validates the arguments; the members are configured identically,
+// so a later member fails only on its own device's resources).
+template <class F>
+static int fanout(dsce_ctx* ctx, F&& f) {
+    const int rc = f(ctx);
+    if (rc != DSCE_OK || !ctx) return rc;
+    for (size_t m = 1; m <= ctx->peers.size(); ++m) {
+        const int r2 = f(member(ctx, m));
+        if (r2 != DSCE_OK) return api_fail(ctx, r2, member_name(ctx, m) + ": " + member(ctx, m)->err);
+    }
+    return DSCE_OK;
+}
+
+// The same with one host thread per member (dsce_build_mmse: the setup is
+// replicated per device, SURVEY §8e, and runs concurrently).
+template <class F>
+static int fanout_par(dsce_ctx* ctx, F&& f) {
+    if (!ctx || ctx->peers.empty()) return f(ctx);
+    const size_t n = ctx->peers.size() + 1;
+    std::vector<int> rc(n, DSCE_OK);
+    std::vector<std::thread> th;
+    try {
+        for (size_t m = 1; m < n; ++m) th.emplace_back([&, m] { rc[m] = f(member(ctx, m)); });
+    } catch (const std::exception& e) {
+        for (auto& t : th) t.join();
+        return api_fail(ctx, DSCE_ENOMEM, std::string("cannot start a member thread: ") + e.what());
+    }
+    rc[0] = f(ctx);
+    for (auto& t : th) t.join();
+    if (rc[0] != DSCE_OK) return rc[0];
+    for (size_t m = 1; m < n; ++m)
+        if (rc[m] != DSCE_OK) return api_fail(ctx, rc[m], member_name(ctx, m) + ": " + member(ctx, m)->err);
+    return DSCE_OK;
+}
+
+// Slice m of [first, first + n) over `world` members on multiples of 64
+// realisations (dsce/parallel.py shard_range, the torch.distributed twin)
+static void shard_slice(uint64_t first, uint64_t n, size_t world, size_t m, uint64_t& f, uint64_t& k) {
+    const uint64_t blocks = (n + 63) / 64;
+    const uint64_t lo = std::min<uint64_t>(blocks * m / world * 64, n);
+    const uint64_t hi = std::min<uint64_t>(blocks * (m + 1) / world * 64, n);
+    f = first + lo;
+    k = hi - lo;
+}
+
 extern "C" {
 
 int dsce_abi_version(void) { return DSCE_ABI_VERSION; }
@@ -1789,8 +1832,79 @@ int dsce_create(int hip_device, dsce_ctx** out) {
     return DSCE_OK;
 }
 
+int dsce_create_multi(const int32_t* devices, int32_t n_devices, dsce_ctx** out) {
+    if (!out) return DSCE_EINVAL;
+    *out = nullptr;
+    if (!devices || n_devices < 1 || n_devices > 64) {
+        fprintf(stderr, "dsce_create_multi: 1..64 devices expected\n");
+        return DSCE_EINVAL;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) count = 0;
+    bool distinct = true;
+    for (int i = 0; i < n_devices; ++i) {
+        if (devices[i] < 0 || devices[i] >= count) {
+            fprintf(stderr, "dsce_create_multi: device %d of %d is not a HIP device\n", (int)devices[i], count);
+            return DSCE_EINVAL;
+        }
+        for (int j = 0; j < i; ++j) distinct = distinct && devices[j] != devices[i];
+    }
+    dsce_ctx* ctx = nullptr;
+    int rc = dsce_create(devices[0], &ctx);
+    if (rc != DSCE_OK) return rc;
+    for (int i = 1; i < n_devices; ++i) {
+        dsce_ctx* p = nullptr;
+        rc = dsce_create(devices[i], &p);
+        if (rc != DSCE_OK) {
+            (void)dsce_destroy(ctx);
+            return rc;
+        }
+        ctx->peers.push_back(p);
+    }
+    if (distinct) {
+        // one communicator per member in this process (single-process multi-GPU
+        // RCCL); n_devices = 1 too, so the reduction path is the same at any size
+        ctx->comms.assign(n_devices, nullptr);
+        const ncclResult_t r = ncclCommInitAll(ctx->comms.data(), n_devices, devices);
+        if (r != ncclSuccess) {
+            fprintf(stderr, "dsce_create_multi: ncclCommInitAll failed: %s\n", ncclGetErrorString(r));
+            ctx->comms.clear();
+            (void)dsce_destroy(ctx);
+            return DSCE_EHIP;
+        }
+        ctx->reduce = DSCE_REDUCE_RCCL;
+    } else {
+        ctx->reduce = DSCE_REDUCE_HOST;
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = ctx;
+    return DSCE_OK;
+}
+
+int dsce_group_info(dsce_ctx* ctx, int32_t* n_devices, int32_t* devices, int32_t* reduce) {
+    if (!ctx) return DSCE_EINVAL;
+    const size_t n = ctx->peers.size() + 1;
+    if (n_devices) *n_devices = (int32_t)n;
+    if (devices)
+        for (size_t m = 0; m < n; ++m) devices[m] = member(ctx, m)->device;
+    if (reduce) *reduce = ctx->reduce;
+    return DSCE_OK;
+}
+
 int dsce_destroy(dsce_ctx* ctx) {
     if (!ctx) return DSCE_OK;
+    // a multi-device handle: its communicators, then its members (each reports
+    // its own failing call on stderr)
+    int member_rc = DSCE_OK;
+    for (ncclComm_t cm : ctx->comms)
+        if (cm && ncclCommDestroy(cm) != ncclSuccess) {
+            fprintf(stderr, "dsce_destroy: ncclCommDestroy failed\n");
+            member_rc = DSCE_EHIP;
+        }
+    ctx->comms.clear();
+    for (dsce_ctx* p : ctx->peers)
+        if (dsce_destroy(p) != DSCE_OK) member_rc = DSCE_EHIP;
+    ctx->peers.clear();
     // The context is freed whatever happens; a failing call is named (stderr),
     // its error cleared, so it does not surface in the next context's
     // hipGetLastError (r04: a stale 'invalid argument' met a later build_mmse),
@@ -1805,7 +1919,6 @@ int dsce_destroy(dsce_ctx* ctx) {
     };
     note(hipSetDevice(ctx->device), "hipSetDevice");
     if (ctx->stream) note(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-    if (ctx->stream2) note(hipStreamSynchronize(ctx->stream2), "hipStreamSynchronize (stream2)");
     for (void* p : ctx->buf_allocs) note(hipFree(p), "hipFree (batch buffers)");
     for (void* p : ctx->allocs) note(hipFree(p), "hipFree (operators)");
     for (auto& e : ctx->pending) {
@@ -1813,19 +1926,16 @@ int dsce_destroy(dsce_ctx* ctx) {
         note(hipEventDestroy(e.b), "hipEventDestroy");
     }
     for (auto e : ctx->event_pool) note(hipEventDestroy(e), "hipEventDestroy (pool)");
-    if (ctx->ev_fork) note(hipEventDestroy(ctx->ev_fork), "hipEventDestroy (fork)");
-    if (ctx->ev_join) note(hipEventDestroy(ctx->ev_join), "hipEventDestroy (join)");
-    if (ctx->stream2) note(hipStreamDestroy(ctx->stream2), "hipStreamDestroy (stream2)");
     if (ctx->stream) note(hipStreamDestroy(ctx->stream), "hipStreamDestroy");
     delete ctx;
     if (first) fprintf(stderr, "dsce_destroy: %s failed: %s\n", first, hipGetErrorString(ferr));
     (void)hipGetLastError();
-    return first ? DSCE_EHIP : DSCE_OK;
+    return first ? DSCE_EHIP : member_rc;
 }
 
 const char* dsce_last_error(const dsce_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
-int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
+static int set_channel_one(dsce_ctx* ctx, const dsce_channel_desc* d) {
     API_BEGIN
     check_ctx(ctx);
     if (!d || !d->pdp_norm || d->n_samples <= 1 || d->n_taps <= 0 || d->n_paths <= 0 || d->sampling_rate <= 0)
@@ -1881,7 +1991,11 @@ int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
     API_END
 }
 
-int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter) {
+int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* d) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_channel_one(c, d); });
+}
+
+static int set_snr_one(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter) {
     API_BEGIN
     check_ctx(ctx);
     if (!pn_time || n_snr <= 0 || n_iter < 0) throw ApiError(DSCE_EINVAL, "invalid SNR list");
@@ -1901,7 +2015,11 @@ int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_
     API_END
 }
 
-int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id) {
+int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_snr_one(c, pn_time, n_snr, n_iter); });
+}
+
+static int add_scheme_one(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id) {
     API_BEGIN
     check_ctx(ctx);
     if (!ctx->chan_set) throw ApiError(DSCE_ESTATE, "dsce_set_channel first");
@@ -1948,7 +2066,11 @@ int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id
     API_END
 }
 
-int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold) {
+int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id) {
+    return fanout(ctx, [&](dsce_ctx* c) { return add_scheme_one(c, d, scheme_id); });
+}
+
+static int build_mmse_one(dsce_ctx* ctx, double zero_threshold) {
     API_BEGIN
     check_ctx(ctx);
     if (ctx->nsnr <= 0) throw ApiError(DSCE_ESTATE, "dsce_set_snr first");
@@ -1958,12 +2080,20 @@ int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold) {
     API_END
 }
 
-int dsce_set_batch(dsce_ctx* ctx, int32_t reps) {
+int dsce_build_mmse(dsce_ctx* ctx, double zero_threshold) {
+    return fanout_par(ctx, [&](dsce_ctx* c) { return build_mmse_one(c, zero_threshold); });
+}
+
+static int set_batch_one(dsce_ctx* ctx, int32_t reps) {
     API_BEGIN
     check_ctx(ctx);
     if (reps < 64) throw ApiError(DSCE_EINVAL, "batch must be >= 64");
     ctx->batch = (reps + 63) / 64 * 64;
     API_END
+}
+
+int dsce_set_batch(dsce_ctx* ctx, int32_t reps) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_batch_one(c, reps); });
 }
 
 static void prepare_run(dsce_ctx* ctx) {
@@ -2000,18 +2130,19 @@ static void set_mse_buffers(dsce_ctx* ctx) {
     ctx->buf.mse_pow = ctx->d_mse + ne;
 }
 
-static void collect_mse(dsce_ctx* ctx) {
+// the member's device MSE sums added into dst (the handle's host totals)
+static void collect_mse(dsce_ctx* ctx, std::vector<double>& dst) {
     if (!ctx->mse) return;
     std::vector<double> h(ctx->mse_n);
     DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_mse, h.size() * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
-    for (size_t i = 0; i < h.size(); ++i) ctx->mse_host[i] += h[i];
+    if (dst.size() != h.size()) dst.assign(h.size(), 0.0);
+    for (size_t i = 0; i < h.size(); ++i) dst[i] += h[i];
 }
 
-int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
-    API_BEGIN
-    check_ctx(ctx);
-    if (!err_counts) throw ApiError(DSCE_EINVAL, "err_counts is null");
+// Realisations [first_rep, first_rep + n_rep) of one member into its device
+// counters (zeroed first); nothing is copied back
+static void run_reps(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep) {
     prepare_run(ctx);
     // any n_rep (the script's NrRepetitions, script:19 / :44): a tail that is no
     // multiple of 64 runs as a whole wave whose padding realisations count nothing
@@ -2025,13 +2156,108 @@ int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, i
         run_batch(ctx, seed, first_rep + done, R, nvalid, nullptr);
         done += (uint64_t)nvalid;
     }
-    std::vector<unsigned long long> h(ctx->counters_n);
-    DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(unsigned long long),
-                                  hipMemcpyDeviceToHost, ctx->stream));
+}
+
+// The member's device counters added into err_counts (null: none), its MSE sums
+// into *mse_dst (the handle's totals), its timing events collected
+static void finish_run(dsce_ctx* ctx, int64_t* err_counts, std::vector<double>* mse_dst) {
+    std::vector<unsigned long long> h(err_counts ? ctx->counters_n : 0);
+    if (err_counts)
+        DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->timing) collect_timing(ctx);
     for (size_t i = 0; i < h.size(); ++i) err_counts[i] += (int64_t)h[i];
-    collect_mse(ctx);
+    if (mse_dst) collect_mse(ctx, *mse_dst);
+}
+
+// dsce_run of a multi-device context: one host thread per member on its slice,
+// then one ncclAllReduce (sum) per buffer over the members' device counters /
+// MSE sums (DSCE_REDUCE_RCCL) or the host sum (DSCE_REDUCE_HOST), and the total
+// added into err_counts once
+static void run_multi(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
+    const size_t n = ctx->peers.size() + 1;
+    std::vector<int> code(n, DSCE_OK);
+    std::vector<std::string> msg(n);
+    auto work = [&](size_t m) {
+        dsce_ctx* c = member(ctx, m);
+        try {
+            check_ctx(c);
+            uint64_t f = 0, k = 0;
+            shard_slice(first_rep, n_rep, n, m, f, k);
+            run_reps(c, seed, f, k);
+            DSCE_HIP_CHECK(hipGetLastError());
+            return;
+        } catch (const ApiError& e) {
+            code[m] = e.code;
+            msg[m] = e.what();
+        } catch (const HipError& e) {
+            code[m] = DSCE_EHIP;
+            msg[m] = e.what();
+        } catch (const std::bad_alloc&) {
+            code[m] = DSCE_ENOMEM;
+            msg[m] = "host out of memory";
+        } catch (const std::exception& e) {
+            code[m] = DSCE_EINVAL;
+            msg[m] = e.what();
+        }
+    };
+    std::vector<std::thread> th;
+    try {
+        for (size_t m = 1; m < n; ++m) th.emplace_back(work, m);
+    } catch (...) {
+        for (auto& t : th) t.join();
+        throw ApiError(DSCE_ENOMEM, "cannot start a member thread");
+    }
+    work(0);
+    for (auto& t : th) t.join();
+    for (size_t m = 0; m < n; ++m)
+        if (code[m] != DSCE_OK) {
+            // drain every member before reporting (no member's launches outlive the call)
+            for (size_t j = 0; j < n; ++j) {
+                (void)hipSetDevice(member(ctx, j)->device);
+                (void)hipStreamSynchronize(member(ctx, j)->stream);
+            }
+            (void)hipSetDevice(ctx->device);
+            throw ApiError(code[m], member_name(ctx, m) + ": " + msg[m]);
+        }
+    if (ctx->reduce == DSCE_REDUCE_RCCL) {
+        // stream-ordered behind each member's kernels; one group = one collective
+        // launch per buffer and device
+        DSCE_NCCL_CHECK(ncclGroupStart());
+        for (size_t m = 0; m < n; ++m) {
+            dsce_ctx* c = member(ctx, m);
+            DSCE_NCCL_CHECK(ncclAllReduce(c->d_counters, c->d_counters, c->counters_n, ncclUint64, ncclSum,
+                                          ctx->comms[m], c->stream));
+            if (c->mse)
+                DSCE_NCCL_CHECK(ncclAllReduce(c->d_mse, c->d_mse, c->mse_n, ncclFloat64, ncclSum, ctx->comms[m], c->stream));
+        }
+        DSCE_NCCL_CHECK(ncclGroupEnd());
+        for (size_t m = 1; m < n; ++m) {
+            check_ctx(member(ctx, m));
+            finish_run(member(ctx, m), nullptr, nullptr);
+        }
+        check_ctx(ctx);
+        finish_run(ctx, err_counts, &ctx->mse_host);     // member 0 holds the sums
+    } else {
+        for (size_t m = 0; m < n; ++m) {
+            check_ctx(member(ctx, m));
+            finish_run(member(ctx, m), err_counts, &ctx->mse_host);
+        }
+        check_ctx(ctx);
+    }
+}
+
+int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
+    API_BEGIN
+    check_ctx(ctx);
+    if (!err_counts) throw ApiError(DSCE_EINVAL, "err_counts is null");
+    if (!ctx->peers.empty() || ctx->reduce != DSCE_REDUCE_NONE) {
+        run_multi(ctx, seed, first_rep, n_rep, err_counts);
+    } else {
+        run_reps(ctx, seed, first_rep, n_rep);
+        finish_run(ctx, err_counts, &ctx->mse_host);
+    }
     API_END
 }
 
@@ -2310,7 +2536,7 @@ int dsce_mmse_onetap(dsce_ctx* ctx, int32_t id, int32_t k, int32_t var, const do
     API_END
 }
 
-int dsce_set_noise_slot(dsce_ctx* ctx, int32_t id, int32_t slot) {
+static int set_noise_slot_one(dsce_ctx* ctx, int32_t id, int32_t slot) {
     API_BEGIN
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
@@ -2320,7 +2546,11 @@ int dsce_set_noise_slot(dsce_ctx* ctx, int32_t id, int32_t slot) {
     API_END
 }
 
-int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
+int dsce_set_noise_slot(dsce_ctx* ctx, int32_t id, int32_t slot) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_noise_slot_one(c, id, slot); });
+}
+
+static int set_interpolation_one(dsce_ctx* ctx, int32_t id, const double* I) {
     API_BEGIN
     check_ctx(ctx);
     Scheme& s = get_scheme(ctx, id);
@@ -2340,12 +2570,20 @@ int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
     API_END
 }
 
-int dsce_enable_mse(dsce_ctx* ctx, int32_t enable) {
+int dsce_set_interpolation(dsce_ctx* ctx, int32_t id, const double* I) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_interpolation_one(c, id, I); });
+}
+
+static int enable_mse_one(dsce_ctx* ctx, int32_t enable) {
     API_BEGIN
     check_ctx(ctx);
     ctx->mse = enable != 0;
     ctx->mse_host.clear();
     API_END
+}
+
+int dsce_enable_mse(dsce_ctx* ctx, int32_t enable) {
+    return fanout(ctx, [&](dsce_ctx* c) { return enable_mse_one(c, enable); });
 }
 
 int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum) {
@@ -2362,12 +2600,16 @@ int dsce_get_mse(dsce_ctx* ctx, double* err_sum, double* pow_sum) {
     API_END
 }
 
-int dsce_enable_timing(dsce_ctx* ctx, int32_t enable) {
+static int enable_timing_one(dsce_ctx* ctx, int32_t enable) {
     API_BEGIN
     check_ctx(ctx);
     ctx->timing = enable != 0;
     if (!ctx->timing) ctx->ktime.clear();
     API_END
+}
+
+int dsce_enable_timing(dsce_ctx* ctx, int32_t enable) {
+    return fanout(ctx, [&](dsce_ctx* c) { return enable_timing_one(c, enable); });
 }
 
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms) {
@@ -2467,9 +2709,9 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(pic_skip) X(mic_lr) X(pic_poly) X(wrow) X(ic_streams)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(mic_lr) X(pic_poly) X(wrow)
 
-int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
+static int set_option_one(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN
     check_ctx(ctx);
     if (!name) throw ApiError(DSCE_EINVAL, "null option name");
@@ -2478,6 +2720,8 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
 #define X(f) if (n == #f) slot = &ctx->op.f;
     DSCE_OPTIONS(X)
 #undef X
+    if (!slot && (n == "pic_skip" || n == "ic_streams"))
+        throw ApiError(DSCE_EINVAL, "option '" + n + "' was retired in r06 (measured neutral in r04 / r05; DESIGN.md 2.0d, 2.0f)");
     if (!slot) throw ApiError(DSCE_EINVAL, "unknown option '" + n + "'");
     if (n == "stage_rb" && value != 4 && value != 8 && value != 16) throw ApiError(DSCE_EINVAL, "stage_rb: 4 | 8 | 16");
     if (n == "jakes_rpw" && value != 1 && value != 2) throw ApiError(DSCE_EINVAL, "jakes_rpw: 1 | 2");
@@ -2485,11 +2729,14 @@ int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
         throw ApiError(DSCE_EINVAL, "pic_chain: 0 (per-iteration passes) | 3 (k_pic_fft); the r01 chains 1 / 2 "
                                     "(k_pic_chain, k_pic_mfma) were retired in r03");
     if (n == "snr_base" && (value < 0 || value > 255)) throw ApiError(DSCE_EINVAL, "snr_base: 0..255");
-    if (n == "ic_streams" && (value < 1 || value > 3)) throw ApiError(DSCE_EINVAL, "ic_streams: 1 | 2 | 3");
     if (n == "snr_base") check_noise_streams(ctx, value, ctx->nsnr, max_noise_slot(ctx));
     if (value < -1 || value > 1 << 20) throw ApiError(DSCE_EINVAL, "option value out of range");
     *slot = (int)value;
     API_END
+}
+
+int dsce_set_option(dsce_ctx* ctx, const char* name, int64_t value) {
+    return fanout(ctx, [&](dsce_ctx* c) { return set_option_one(c, name, value); });
 }
 
 int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value) {

@@ -84,8 +84,9 @@ __device__ __forceinline__ uint4 stream_block(uint64_t seed, uint64_t rep, uint3
 
 // stream_block of many sub-streams of one (seed, rep, stream, idx) (k_txrx_fft:
 // the SNR points): the first round does not depend on the sub-stream except
-// through one XOR (c2' = hi(M0 idx) ^ c3 ^ k0'), so its two products are formed
-// once (pre) and each block costs nine rounds
+// through one XOR (c2' = hi(M0 idx) ^ c3 ^ k1, with k1 = seed >> 32 the round-0
+// key, not yet incremented), so its two products are formed once (pre) and each
+// block costs nine rounds (tests/test_philox_sub.py restates the split)
 struct PhiloxSub {
     uint32_t n0, lo1, hk, lo0, k0, k1;
 };

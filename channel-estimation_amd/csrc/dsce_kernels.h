@@ -33,18 +33,10 @@ struct Opts {
     int realise_win = 0;      // dsce_channel_realise forms only the JakesChunks samples (tests the window kernels)
     int mic_lr = 1;           // MMSE IC taps in the low-rank form T_k Z (k_mic_pilot / k_mic_data) where
                               // build_mic_lr verified it; 0 = the tap GEMM Bv hP on the matrix cores
-    int pic_skip = 0;         // 1: k_pic_fft stops a wave at the IC's fixed point (decisions repeat: later
-                              // iterations are copies); exact, but rarely a whole wave converges and the
-                              // test costs more than it saves (r04 box: 2.626 -> 2.665 ms per step): 0
     int pic_poly = 1;         // perfect-CSI IC passes of polyphase schemes (SchemeK::poly_ok: FBMC, OFDM with
                               // L != 24) as IDFT-L per symbol + window sums per residue + DFT-L per symbol
                               // (k_poly_syn / k_poly_chan / k_poly_ana) instead of the two banded passes
                               // (r04 box, C3: 14.3 -> 8.7 ms per iteration); 0 = the banded passes
-    int ic_streams = 1;       // FFT-form OFDM: 2 = k_pic_fft on a second stream beside k_mic_pilot / k_mic_data
-                              // (r05 same-box A/Bs: 7.06-7.20 -> 6.87-6.90 ms per C2 step on one box, 6.77 ->
-                              // 6.83 on another: box-dependent, and it blurs the per-kernel spans); 3 = k_pic_fft
-                              // and k_mic_pilot in ONE launch (k_ic_pair, XCD-preserving 8-block groups dealt
-                              // evenly; two boxes: +1.4 % and +0.0 %, within box noise); 1 = one stream
     int wrow = 1;             // unfused W contraction of 32-row blocks (FBMC, C5) as one GEMM per row tile
                               // (k_wrow3: X = hP v_c as the B operand, no per-tile epilogue); 0 = k_wpair3
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
@@ -231,11 +223,6 @@ unsigned launch_perfect_ic(hipStream_t s, const Opts& op, const SchemeK& sk, con
 // registers (pic_ok schemes); perfect_chain_ok tells when it applies.
 bool perfect_chain_ok(const Opts& op, const SchemeK& sk, const ChannelK& ch, const McBuffers& b, int niter);
 // stage0: k_pic_fft also runs the perfect-CSI stage 0 (one-tap y ./ h) first
-// Opts::ic_streams 3: the perfect-CSI chain and the MMSE pilot pass in one
-// launch (k_ic_pair); ic_pair_ok: the variant exists for this scheme / batch
-bool ic_pair_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b, bool lr);
-unsigned launch_ic_pair(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch,
-                        McBuffers& b, const PerfectDetectArgs* pd, int niter, bool lr);
 unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, const ChannelK& ch, McBuffers& b,
                               const PerfectDetectArgs* pd, int niter, bool stage0 = false);
 void launch_mmse_onetap(hipStream_t s, int LK, int NP, const double2* wd, const double2* hp, int n, double2* h);

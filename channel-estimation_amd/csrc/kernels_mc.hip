@@ -1069,7 +1069,6 @@ struct StorePerfectDetect {
     const uint16_t* sidr;              // transmitted symbol index per data row [LK][R]
     const TraceK* tr;                  // null unless tracing (dsce_trace_unit_ex)
     int stage;                         // IC iteration of this pass (trace only)
-    int skip;                          // k_pic_fft: stop at the IC's fixed point (Opts::pic_skip)
     int pv_uni;                        // chain kernels: SchemeK::pv_uni (reprecode6 / stage_sym)
     double pv_re, pv_im;
     double2* sym;
@@ -1675,8 +1674,8 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // twiddle, 8 DPP moves, 4 FMAs and the +-i selects (100 cycles,
 // tools/ubench/net.hip).  The previous quarter's sample 5 comes by ds_bpermute.
 // r05 (the per-section census, profiles/r05_census_*): the iteration carried
-// ~40 register copies (the fixed-point exit's loop state, now the SKIP variant
-// only), the imaginary A parts were negated by VALU moves (now the f64 MFMA's
+// ~40 register copies (the loop state of the fixed-point exit, option pic_skip,
+// retired in r06), the imaginary A parts were negated by VALU moves (now the f64 MFMA's
 // neg modifier, mfma4_cmul), the tie candidates took ~35 instructions per
 // iteration (now one min3 chain), and the epilogue spent 10 FP64 operations
 // per row.  The chain now runs on u scaled by the slicer's scale c = scI: the
@@ -1686,9 +1685,8 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // (7 FP64 operations per row).  Re-precoded decisions read the scaled
 // constellation; the constant rows of u (pilots) are per-lane LDS slots read
 // through the same address select, so a row's new u is one LDS read.
-// (the body of k_pic_fft and of k_ic_pair's chain blocks: vb / vn = the block's
-// index in the chain's own grid and that grid's size, vb % 8 = the XCD)
-template <int NT, int SH, bool TRACE, bool S0, bool NM, bool SKIP>
+// (vb / vn = the block's index in the grid and the grid's size, vb % 8 = the XCD)
+template <int NT, int SH, bool TRACE, bool S0, bool NM>
 __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder& ord, const double2* __restrict__ ir, int N,
                                              const StorePerfectDetect& o, int niter, int vb, int vn) {
     int ug, blk;
@@ -1786,16 +1784,6 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
     }
     const double sg1 = (r >> 1) ? -1.0 : 1.0, sg2 = (r & 1) ? -1.0 : 1.0;
     int ncnt = 0;
-    // The IC's fixed point (SKIP, o.skip): D, h and y do not change between the
-    // iterations of the perfect-CSI branch (script:541-561), so an iteration
-    // whose decisions equal the previous iteration's for every data row of the
-    // wave's 16 units (the symbol blocks of OFDM are independent: D is block-
-    // diagonal) is reproduced exactly — same inputs, same instructions — by
-    // every later one: their counts (and traces) are copies.  pk: the last
-    // decisions, 8 bits per row; have: pk is valid (stage 0 ran here, or an
-    // iteration did).
-    unsigned pk[2] = {0u, 0u};
-    bool have = S0, conv = false;
     // error-count weight of row a: data rows count 1, no-edge rows also 1 << 16
     auto cweight = [&](int a) -> int {
         return ((dmask >> a) & 1) ? (((emask >> a) & 1) ? 0x10001 : 1) : 0;
@@ -1840,18 +1828,12 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
             const bool data = (dmask >> a) & 1;
             ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)(rdc[4 * a + r] >> 1)] = dp[a];
-            if (SKIP) pk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
         reprecode(dp);
         cntl[w][0] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);
         ncnt = 0;
     }
     for (int it = 1; it <= niter; ++it) {
-        if (SKIP && conv) {
-            // the fixed point (below): this iteration reproduces the previous one
-            cntl[w][it] = cntl[w][it - 1];
-            continue;
-        }
         // an opaque zero keeps the per-iteration LDS twiddle reads inside the loop
         // (hoisted, they would hold 56 more registers)
         int oz = 0;
@@ -1937,39 +1919,15 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
         // a decision exactly on a mid-point (measure zero): the smallest symbol
         // index among the tied grid points (one uniform branch inside)
         slice6(dp, fI, fQ, o.topI, o.topQ, sgrid);
-        unsigned npk[2] = {0u, 0u};
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const bool data = (dmask >> a) & 1;
             ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)it * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
-            if (SKIP) npk[a >> 2] |= (data ? (unsigned)dp[a] & 0xffu : 0u) << (8 * (a & 3));
         }
         reprecode(dp);
         cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
-        if (SKIP) {
-            const bool same = have && npk[0] == pk[0] && npk[1] == pk[1];
-            pk[0] = npk[0];
-            pk[1] = npk[1];
-            have = true;
-            if (o.skip && it < niter && __all(same)) {
-                conv = true;
-                if (TRACE)
-#pragma unroll
-                    for (int a = 0; a < 6; ++a)
-                        if (((dmask >> a) & 1) && unit == o.tr->unit) {
-                            const int row = row0 + 4 * a + r;
-                            const double2 yv = o.y[(size_t)row * U + unit], hv = o.h[(size_t)row * R + rl];
-                            const double2 yp = c_add(c_sub(yv, make_double2(x[p6(a)].x / cs, x[p6(a)].y / cs)),
-                                                     c_mul(hv, make_double2(u[a].x / cs, u[a].y / cs)));
-                            for (int i2 = it + 1; i2 <= niter; ++i2) {
-                                o.tr->yperf[(size_t)i2 * o.tr->LK + row] = yp;
-                                o.tr->dec_p[(size_t)i2 * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
-                            }
-                        }
-            }
-        }
     }
     // counters of every stage, summed over the block's 4 waves: thread
     // 2 (it - it0) + edge issues the block's one atomic per counter
@@ -1986,10 +1944,10 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
     }
 }
 
-template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false, bool SKIP = false>
+template <int NT, int SH, bool TRACE, bool S0 = false, bool NM = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_pic_fft(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect o, int niter) {
-    pic_fft_body<NT, SH, TRACE, S0, NM, SKIP>(sk, ord, ir, N, o, niter, blockIdx.x, gridDim.x);
+    pic_fft_body<NT, SH, TRACE, S0, NM>(sk, ord, ir, N, o, niter, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -2167,8 +2125,9 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
     // z = ye / hd with the slicer scale folded into the reciprocals, and the six
     // rows' 1 / |hd|^2 from ONE reciprocal (r05, batch inversion: prefix
     // products, one recip_fast, two products per row back; 20 FP64 operations
-    // instead of 30).  A product outside [2^-1000, 2^1000] (a zero or vanishing
-    // estimate somewhere in the lane's rows) takes the per-row reciprocals.
+    // instead of 30).  A factor |hd|^2 outside [2^-160, 2^160] (a zero or
+    // vanishing estimate somewhere in the lane's rows) takes the per-row
+    // reciprocals.
     double nn[6], pp[6], id[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) nn[a] = fma(hd[a].x, hd[a].x, hd[a].y * hd[a].y);
@@ -2182,7 +2141,14 @@ __device__ __forceinline__ void mic_detect(int (&dp)[6], const double2 (&ye)[6],
         inv *= nn[a];
     }
     id[0] = inv;
-    const bool ok = pp[5] > 0x1p-1000 && pp[5] < 0x1p1000;
+    // every factor in [2^-160, 2^160] (its exponent field, one unsigned compare
+    // per row): then every prefix product stays within 2^(+-960), no denormal
+    // (a bound on pp[5] alone let an underflowed prefix through);
+    // zero, inf and NaN fail it
+    unsigned ex = 0u;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) ex = max(ex, (unsigned)__double2hiint(nn[a]) - (unsigned)((1023 - 160) << 20));
+    const bool ok = ex < (320u << 20);
     if (__ballot(!ok)) {
 #pragma unroll
         for (int a = 0; a < 6; ++a) id[a] = ok ? id[a] : recip_fast(nn[a]) * o.scI;
@@ -2614,7 +2580,7 @@ __device__ __forceinline__ void mic2_rows(double2* rpv, int* rdc, int* rpc, doub
 }
 
 // One wave per pilot symbol (blockDim = 64 npb, npb <= 4), 16 units per block
-// (the body of k_mic_pilot and of k_ic_pair's pilot blocks: vb / vn as pic_fft_body's)
+// (vb / vn: the block index and grid size, as pic_fft_body's)
 template <int NT, int SH, int NP, bool TRACE, bool NM, bool LR>
 __device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args& ma, const StorePerfectDetect& o, int vb,
                                                int vn) {
@@ -2702,27 +2668,6 @@ __device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args
 template <int NT, int SH, int NP, bool TRACE, bool NM = false, bool LR = false>
 __global__ void __launch_bounds__(256) k_mic_pilot(SchemeK sk, Mic2Args ma, StorePerfectDetect o) {
     mic_pilot_body<NT, SH, NP, TRACE, NM, LR>(sk, ma, o, blockIdx.x, gridDim.x);
-}
-
-// The perfect-CSI chain (k_pic_fft, stage 0 included, matrix-core network) and
-// the MMSE pilot pass (k_mic_pilot, 256 threads) in ONE launch (Opts::ic_streams
-// 3): the two are independent, the chain issue-bound (VALU + MFMA 0.86 busy), the
-// pilot pass latency-bound (two barriers per stage, 0.65 busy), so a CU holding
-// a block of each fills the pilot blocks' stalls with chain work.  The grid is
-// cut into groups of 8 blocks (one per XCD); the groups are dealt to the two
-// passes evenly (Bresenham), and inside each pass group g, block x has the
-// pass-local index 8 g + x: the same XCD as in the pass's own launch, so its
-// XCD-contiguous order (xcd_remap) holds.  LDS: both bodies' tables (static).
-template <int NT, int SH, bool PNM, bool LR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-k_ic_pair(SchemeK sk, BandOrder ord, const double2* __restrict__ ir, int N, StorePerfectDetect op, int niter,
-          Mic2Args ma, StorePerfectDetect om, int npic8, int npil8) {
-    const int G = blockIdx.x >> 3, x = blockIdx.x & 7, ng = npic8 + npil8;
-    const int q0 = (int)((long long)G * npil8 / ng), q1 = (int)((long long)(G + 1) * npil8 / ng);
-    if (q1 > q0)
-        mic_pilot_body<NT, SH, 16, false, PNM, LR>(sk, ma, om, q0 * 8 + x, npil8 * 8);
-    else
-        pic_fft_body<NT, SH, false, true, true, false>(sk, ord, ir, N, op, niter, (G - q0) * 8 + x, npic8 * 8);
 }
 
 // 64 units x one data symbol per block (4 waves x 16 units)
@@ -3169,25 +3114,15 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
     if (!pic_fft_ok(op, sk, ch, b, niter))
         throw std::logic_error("launch_perfect_chain: no chain kernel for this scheme (perfect_chain_ok is false)");
     StorePerfectDetect o = chain_detect(sk, b, pd, 1);
-    o.skip = op.pic_skip;
     const BandOrder om{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
     const dim3 grid((b.U / WAVE) * sk.QH.nblk), blk(256);
     // stage0: the chain also runs stage 0 of the branch (with k_mic_pilot /
     // k_mic_data); otherwise stage 0 came from the stage kernel (u in HBM)
-    // the fixed-point exit (Opts::pic_skip) is its own variant (its loop state
-    // costs the plain chain ~40 register copies per iteration), matrix-core
-    // network only
-    if (op.pic_skip && !op.pic_net)
-        throw std::invalid_argument("launch_perfect_chain: pic_skip needs pic_net 1");
     if (!(o.scI != 0.0))
         throw std::logic_error("launch_perfect_chain: the chain's slicer scale is zero");
 #define LAUNCH_PF(NTV, SHV, S0V, NMV)                                                                               \
     do {                                                                                                             \
-        if (NMV && op.pic_skip && b.tr)                                                                              \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V, NMV, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
-        else if (NMV && op.pic_skip)                                                                                 \
-            hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V, NMV, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
-        else if (b.tr)                                                                                               \
+        if (b.tr)                                                                                                    \
             hipLaunchKernelGGL((k_pic_fft<NTV, SHV, true, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter);  \
         else                                                                                                         \
             hipLaunchKernelGGL((k_pic_fft<NTV, SHV, false, S0V, NMV>), grid, blk, 0, s, sk, om, b.ir, ch.N, o, niter); \
@@ -3207,38 +3142,6 @@ unsigned launch_perfect_chain(hipStream_t s, const Opts& op, const SchemeK& sk, 
 #undef LAUNCH_PF2
 #undef LAUNCH_PF
     return PATH_PIC_FFT;
-}
-
-// k_ic_pair (Opts::ic_streams 3): the perfect-CSI chain with its stage 0 and the
-// MMSE pilot pass in one launch; the variant the C2 path runs (matrix-core
-// networks, low-rank taps, 4 pilot symbols, no trace, no fixed-point exit) and
-// both grids in whole 8-block groups.  Otherwise the caller launches the two.
-bool ic_pair_ok(const Opts& op, const SchemeK& sk, const MmseK& mm, const McBuffers& b, bool lr) {
-    const long long npic = (long long)(b.U / WAVE) * sk.QH.nblk, npil = b.U / 16;
-    return op.pic_net && !op.pic_skip && !b.tr && lr && (op.mic_net & 2) && mm.npb == 4 && mm.Bz && mm.Tw &&
-           mm.Ts && b.za && npic % 8 == 0 && npil % 8 == 0 && npic + npil < (1ll << 31);
-}
-
-unsigned launch_ic_pair(hipStream_t s, const Opts& op, const SchemeK& sk, const MmseK& mm, const ChannelK& ch,
-                        McBuffers& b, const PerfectDetectArgs* pd, int niter, bool lr) {
-    if (!ic_pair_ok(op, sk, mm, b, lr) || !pic_fft_ok(op, sk, ch, b, niter))
-        throw std::logic_error("launch_ic_pair: not eligible (ic_pair_ok / pic_fft_ok)");
-    StorePerfectDetect op_ = chain_detect(sk, b, pd, 1);
-    op_.skip = 0;
-    if (!(op_.scI != 0.0)) throw std::logic_error("launch_ic_pair: the chain's slicer scale is zero");
-    const StorePerfectDetect om = chain_detect(sk, b, pd, 0);
-    const Mic2Args ma = mic2_args(sk, mm, ch, b, pd, niter);
-    const BandOrder ord{b.U / WAVE, b.U / b.R, b.R / WAVE, op.xcd};
-    const int npic8 = (int)((long long)(b.U / WAVE) * sk.QH.nblk / 8), npil8 = (b.U / 16) / 8;
-    const dim3 grid(8 * (npic8 + npil8)), blk(256);
-    const int sh = pic_fft_shift(ch);
-    if (ch.ntap == 1)
-        hipLaunchKernelGGL((k_ic_pair<1, 0, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
-    else if (sh == 1)
-        hipLaunchKernelGGL((k_ic_pair<2, 1, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
-    else
-        hipLaunchKernelGGL((k_ic_pair<2, 2, true, true>), grid, blk, 0, s, sk, ord, b.ir, ch.N, op_, niter, ma, om, npic8, npil8);
-    return PATH_PIC_FFT | PATH_MIC_FFT | PATH_MIC_STAGES | PATH_MIC_LR;
 }
 
 // ---------------------------------------------------------------------------

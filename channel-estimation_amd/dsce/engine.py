@@ -23,10 +23,13 @@ EXPORTED = [
     "dsce_enable_timing", "dsce_kernel_time", "dsce_work_model", "dsce_mmse_onetap", "dsce_tx_matrices",
     "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse", "dsce_trace_unit_ex",
     "dsce_scheme_dims", "dsce_path_info", "dsce_set_option", "dsce_get_option", "dsce_fp64_mfma_peak",
-    "dsce_kernel_work", "dsce_structured_check",
+    "dsce_kernel_work", "dsce_structured_check", "dsce_create_multi", "dsce_group_info",
 ]
 
-ABI_VERSION = 6
+ABI_VERSION = 7
+
+# dsce_group_info reduce kinds (include/dsce.h DSCE_REDUCE_*)
+REDUCE = {0: "none", 1: "rccl", 2: "host"}
 
 # dsce_path_info bits (include/dsce.h DSCE_PATH_*)
 PATH_BITS = {
@@ -94,6 +97,8 @@ def load_library(path=None):
     lib.dsce_abi_version.restype = C.c_int
     lib.dsce_device_count.argtypes = [C.POINTER(C.c_int)]
     lib.dsce_create.argtypes = [C.c_int, C.POINTER(vp)]
+    lib.dsce_create_multi.argtypes = [C.POINTER(C.c_int32), C.c_int32, C.POINTER(vp)]
+    lib.dsce_group_info.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.dsce_destroy.argtypes = [vp]
     lib.dsce_destroy.restype = C.c_int
     lib.dsce_last_error.argtypes = [vp]
@@ -149,14 +154,24 @@ class DsceError(RuntimeError):
 
 
 class Engine:
-    """One engine context = one GPU + one HIP stream (dsce_create)."""
+    """One engine context = one GPU + one HIP stream (dsce_create), or, with a
+    sequence of devices, one multi-device context (dsce_create_multi, ABI 7):
+    every configuration call reaches every member, run() shards the
+    realisations over the members and sums their counters with one in-library
+    RCCL all-reduce (host sum when a device repeats)."""
 
     def __init__(self, device=0, lib_path=None):
         self.lib = load_library(lib_path)
         h = C.c_void_p()
-        rc = self.lib.dsce_create(int(device), C.byref(h))
+        if isinstance(device, (list, tuple, np.ndarray)):
+            devs = np.ascontiguousarray(device, dtype=np.int32)
+            rc = self.lib.dsce_create_multi(devs.ctypes.data_as(C.POINTER(C.c_int32)), int(devs.size), C.byref(h))
+            what = "dsce_create_multi(devices=%s)" % list(devs)
+        else:
+            rc = self.lib.dsce_create(int(device), C.byref(h))
+            what = "dsce_create(device=%d)" % device
         if rc != 0 or not h.value:
-            raise DsceError("dsce_create(device=%d) failed with %d (no HIP device?)" % (device, rc))
+            raise DsceError("%s failed with %d (no HIP device?)" % (what, rc))
         self.h = h
         self._keep = []
         self.schemes = []
@@ -376,6 +391,17 @@ class Engine:
         pw = np.zeros((ns, self.nsnr))
         self._chk(self.lib.dsce_get_mse(self.h, _dptr(err), _dptr(pw)), "dsce_get_mse")
         return err, pw
+
+    def group_info(self):
+        """(devices, reduce) of the context (dsce_group_info): the members' HIP
+        devices and how run() sums them ('none' | 'rccl' | 'host')."""
+        n = C.c_int32()
+        self._chk(self.lib.dsce_group_info(self.h, C.byref(n), None, None), "dsce_group_info")
+        devs = np.zeros(n.value, dtype=np.int32)
+        red = C.c_int32()
+        self._chk(self.lib.dsce_group_info(self.h, None, devs.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(red)),
+                  "dsce_group_info")
+        return [int(d) for d in devs], REDUCE.get(red.value, str(red.value))
 
     # -- measurement -----------------------------------------------------------
     def enable_timing(self, on=True):

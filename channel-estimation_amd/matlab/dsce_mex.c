@@ -18,7 +18,12 @@
  * (dsce_scheme_dims), never from caller arguments.  MATLAB indices (scheme id,
  * SNR index, pilot / data positions) are 1-based here, 0-based at the ABI.
  *
- *   dsce_mex('create' [, device])
+ *   dsce_mex('create' [, device])                                  % device: HIP device (default 0), or a
+ *            vector of devices: one multi-device context (dsce_create_multi, ABI 7) whose 'run'
+ *            shards the realisations over the devices and sums the counters with one RCCL
+ *            all-reduce; every other command is unchanged
+ *   [devices, reduce] = dsce_mex('group_info')                      % the context's HIP devices; reduce 0 single
+ *            device, 1 RCCL all-reduce, 2 host sum (a device repeats)
  *   dsce_mex('destroy')
  *   dsce_mex('set_channel', SamplingRate, PDPnormalized, N, fD, Paths, DopplerModel)
  *            DopplerModel: 0 'Jakes', 1 'Uniform', 2 'Discrete-Jakes', 3 'Discrete-Uniform'
@@ -519,6 +524,18 @@ static void c_get_mse(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]
     else mxDestroyArray(pw);
 }
 
+static void c_group_info(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    int32_t n = 0, red = 0, k;
+    int32_t devs[64];
+    (void)nrhs; (void)prhs;
+    check(dsce_group_info(g_ctx, &n, NULL, NULL), "dsce_group_info");
+    if (n < 1 || n > 64) mexErrMsgIdAndTxt("dsce:state", "group size");
+    check(dsce_group_info(g_ctx, NULL, devs, &red), "dsce_group_info");
+    plhs[0] = mxCreateDoubleMatrix(1, (mwSize)n, mxREAL);
+    for (k = 0; k < n; ++k) DSCE_DOUBLES(plhs[0])[k] = devs[k];
+    if (nlhs > 1) plhs[1] = mxCreateDoubleScalar(red);
+}
+
 static void c_structured_check(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     double c[7];
     int k;
@@ -553,6 +570,7 @@ static const struct {
     {"enable_mse", 2, 2, 0, c_enable_mse},
     {"get_mse", 1, 1, 2, c_get_mse},
     {"structured_check", 2, 2, 1, c_structured_check},
+    {"group_info", 1, 1, 2, c_group_info},
 };
 
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
@@ -562,8 +580,22 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
         mexErrMsgIdAndTxt("dsce:usage", "dsce_mex(cmd, ...): cmd must be a command name");
     g_cmd = cmd;
     if (!strcmp(cmd, "create")) {
-        if (nrhs > 2) mexErrMsgIdAndTxt("dsce:usage", "dsce_mex('create' [, device])");
-        {
+        if (nrhs > 2) mexErrMsgIdAndTxt("dsce:usage", "dsce_mex('create' [, device or device vector])");
+        if (nrhs > 1 && mxGetNumberOfElements(prhs[1]) != 1) {
+            /* a device vector: one multi-device context (dsce_create_multi) */
+            int32_t devs[64];
+            const size_t n = mxGetNumberOfElements(prhs[1]);
+            const double* d;
+            size_t k;
+            if (n < 1 || n > 64) bad(1, "a device or a vector of 1 to 64 devices");
+            d = real_doubles(prhs[1], 1, n);
+            for (k = 0; k < n; ++k) {
+                if (d[k] != floor(d[k]) || d[k] < 0 || d[k] > 1e6) bad(1, "a vector of device indices >= 0");
+                devs[k] = (int32_t)d[k];
+            }
+            cleanup();
+            check(dsce_create_multi(devs, (int32_t)n, &g_ctx), "dsce_create_multi");
+        } else {
             const int dev = nrhs > 1 ? (int)integer(prhs[1], 1, 0) : 0;
             cleanup();
             check(dsce_create(dev, &g_ctx), "dsce_create");

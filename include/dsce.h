@@ -79,13 +79,20 @@
 extern "C" {
 #endif
 
-#define DSCE_ABI_VERSION 6
+#define DSCE_ABI_VERSION 7
 
 #define DSCE_OK 0
 #define DSCE_EINVAL -1      /* bad argument / shape */
 #define DSCE_EHIP -2        /* HIP runtime error */
 #define DSCE_ESTATE -3      /* call order (e.g. run before build_mmse) */
 #define DSCE_ENOMEM -4
+
+/* How dsce_run sums the members of a context (dsce_group_info) */
+#define DSCE_REDUCE_NONE 0  /* a single-device context (dsce_create)                       */
+#define DSCE_REDUCE_RCCL 1  /* ncclAllReduce (sum) of the members' device counters, RCCL    */
+                            /* over xGMI: dsce_create_multi with distinct devices           */
+#define DSCE_REDUCE_HOST 2  /* a device repeats in dsce_create_multi's list (one RCCL rank  */
+                            /* per device): the members' counters are summed on the host    */
 
 typedef struct dsce_ctx dsce_ctx;
 
@@ -220,6 +227,35 @@ int dsce_create(int hip_device, dsce_ctx** out);
 int dsce_destroy(dsce_ctx* ctx);
 const char* dsce_last_error(const dsce_ctx* ctx);
 
+/* Multi-device context (ABI 7; SURVEY §8e, north_star: "realisations shard
+ * embarrassingly across the 8 GPUs of one node with a single RCCL all-reduce"),
+ * so a host that stays one MATLAB process (README.md:19-20; the loop of
+ * DoublySelectiveChannelEstimation.m:350-564) drives every GPU through one
+ * handle.  Member i is a context on devices[i] (member 0 is the returned
+ * handle).
+ *  - Every configuration call — dsce_set_channel, dsce_set_snr,
+ *    dsce_add_scheme, dsce_build_mmse (members in parallel: setup is
+ *    replicated per device), dsce_set_batch, dsce_set_noise_slot,
+ *    dsce_set_interpolation, dsce_set_option, dsce_enable_mse,
+ *    dsce_enable_timing — applies to every member (member 0 first; a member's
+ *    failure is reported through the handle's dsce_last_error).
+ *  - dsce_run splits [first_rep, first_rep + n_rep) into n_devices contiguous
+ *    slices on multiples of 64 realisations (dsce/parallel.py shard_range), runs
+ *    member i's slice on its own host thread, then sums the members' int64
+ *    counters (and MSE sums) with ONE ncclAllReduce per buffer over
+ *    communicators from ncclCommInitAll (DSCE_REDUCE_RCCL; devices distinct,
+ *    n_devices = 1 included) or on the host when a device repeats
+ *    (DSCE_REDUCE_HOST), and adds the total into err_counts once.  The Philox
+ *    streams are keyed by the global realisation index, so the counts equal a
+ *    single context's bit for bit for any member count.
+ *  - Every other call (probes, queries, dsce_kernel_time: member 0's own
+ *    launches, i.e. its slice) uses member 0.
+ * dsce_destroy on the handle frees every member and communicator. */
+int dsce_create_multi(const int32_t* devices, int32_t n_devices, dsce_ctx** out);
+/* Members of a context: *n_devices, their HIP devices (optional, n_devices
+ * entries) and *reduce = DSCE_REDUCE_* (each pointer optional). */
+int dsce_group_info(dsce_ctx* ctx, int32_t* n_devices, int32_t* devices, int32_t* reduce);
+
 int dsce_set_channel(dsce_ctx* ctx, const dsce_channel_desc* desc);
 int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_iter);
 int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* desc, int32_t* scheme_id);
@@ -325,27 +361,17 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   serving SNR points [b, ...) of a sweep draws the one-rank run's noise),
  *   mic_lr (1: the MMSE IC's estimated taps in the low-rank form T_k Z where the
  *   fit reproduces Bv to rounding, dsce_structured_check; 0: the tap GEMM Bv hP),
- *   pic_skip (1: k_pic_fft stops a wave of 16 units x one symbol at the
- *   perfect-CSI IC's fixed point — an iteration that repeats the previous
- *   decisions of every data row is repeated exactly by every later one, whose
- *   counts it copies; 0, the default: every iteration computed — whole waves
- *   rarely converge and the test costs more than it saves), pic_poly (1: the
- *   perfect-CSI IC passes of a scheme whose G and Q factorise as real windows x
+ *   pic_poly (1: the perfect-CSI IC passes of a scheme whose G and Q factorise as real windows x
  *   subcarrier tones, G[n, l + L k] = A_k[n] e^(2 pi i l n / L) C[l][k], checked
  *   entry by entry to 1e-12 at dsce_add_scheme, with L = 24 or 48, as an IDFT-L
  *   per symbol, window sums per residue n mod L around the channel, and a DFT-L
  *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes),
  *   wrow (1: the unfused W contraction of 32-row blocks — FBMC, C5 — as one
  *   GEMM per 16-row tile over (column, pilot) with B = hP v_c, no per-tile
- *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles), ic_streams (2: on
- *   the FFT-form OFDM path the perfect-CSI chain k_pic_fft runs on the
- *   context's second stream beside k_mic_pilot -> k_mic_data, forked after the
- *   receiver front and joined before the counters, the per-kernel spans then
- *   overlap; 3: the chain and the pilot pass in one launch, k_ic_pair —
- *   timed as "ic_pair" — then k_mic_data, where the variant exists (matrix-
- *   core networks, low-rank taps, 4 pilot symbols, no trace, no pic_skip;
- *   else as 1); 1, the default: one stream, the three in sequence; in every
- *   case dsce_kernel_time's "ic_stages" spans the group).
+ *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles).
+ * Retired in r06 (measured neutral in r04 / r05; DSCE_EINVAL): pic_skip (the
+ * perfect-CSI fixed-point exit), ic_streams (the chain on a second stream /
+ * beside the pilot pass in one launch, k_ic_pair).
  * Retired in r03 (the r01-r02 variants they selected are gone; DSCE_EINVAL):
  * wpair_3m, wda_3m, streams, qidx, stage0_fft, mic_mfma, pilot_fft, mic_yic,
  * pilot_fuse, mic2.  Unknown names return DSCE_EINVAL. */
@@ -355,9 +381,8 @@ int dsce_get_option(dsce_ctx* ctx, const char* name, int64_t* value);
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, dsce_run records HIP events around every launch of each kernel
  * on the stream it runs on; dsce_kernel_time returns (launches, total ms).
- * "ic_stages" is the span of the FFT-form OFDM IC group on the main stream
- * (k_pic_fft with ic_streams 2 on the second stream, k_mic_pilot, k_mic_data;
- * with ic_streams 3 "ic_pair" = k_ic_pair, then k_mic_data). */
+ * "ic_stages" is the span of the FFT-form OFDM IC group (k_pic_fft,
+ * k_mic_pilot, k_mic_data, in sequence on the context's stream). */
 int dsce_enable_timing(dsce_ctx* ctx, int32_t enable);
 int dsce_kernel_time(dsce_ctx* ctx, const char* kernel, int64_t* launches, double* total_ms);
 /* Algorithmic work of one realisation of a scheme (support-aware): complex

@@ -109,7 +109,12 @@ static mxArray* S(const char* s);
 static mxArray* Lg(size_t n);
 static mxArray* default_arg(const char* cmd, int pos) {
     if (pos == 0) return S(cmd);
-    if (!strcmp(cmd, "create")) return D(0);
+    if (!strcmp(cmd, "create")) {
+        /* a device vector [0 1 ... 7] (dsce_create_multi) */
+        mxArray* v = mxCreateDoubleMatrix(1, 8, mxREAL);
+        for (size_t i = 0; i < 8; ++i) tst_set_c(v, i, (double)i, 0.0);
+        return v;
+    }
     if (!strcmp(cmd, "set_channel")) {
         const double v[7] = {0, 360e3, 0, 540, 1158.2, 200, 0};
         return pos == 2 ? M(2, 1, 0) : D(v[pos < 7 ? pos : 0]);
@@ -239,6 +244,18 @@ int main(int argc, char** argv) {
     call("get_mse_extra_arg", 2, 2, a);
     a[0] = S("structured_check"); a[1] = D(1);
     call("structured_check", 1, 2, a);
+    a[0] = S("group_info");
+    call("group_info_single", 2, 1, a);
+    a[0] = S("create"); a[1] = M(1, 8, 0);
+    call("create_multi_8", 0, 2, a);        /* devices 1 + i % 7: device 1 repeats -> host sum */
+    a[0] = S("group_info");
+    call("group_info_multi", 2, 1, a);
+    a[0] = S("run"); a[1] = D(1); a[2] = D(0); a[3] = D(64);
+    call("run_multi", 1, 4, a);
+    a[0] = S("create"); a[1] = M(0, 0, 0);
+    call("create_empty_devices", 0, 2, a);
+    a[0] = S("create"); a[1] = D(0);
+    call("create_again", 0, 2, a);
     a[0] = S("no_such_command");
     call("unknown", 0, 1, a);
     a[0] = S("destroy");

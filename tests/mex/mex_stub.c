@@ -183,7 +183,29 @@ void mexUnlock(void) {}
 enum { SN = 540, STAPS = 2, SLK = 336, SNP = 16, SND = 320, SSNR = 7, SIT = 4 };
 struct dsce_ctx { int dummy; };
 static struct dsce_ctx g_stub;
-int dsce_create(int dev, dsce_ctx** out) { (void)dev; *out = &g_stub; return 0; }
+static int32_t g_devs[64], g_ndev = 1, g_reduce = 0;
+int dsce_create(int dev, dsce_ctx** out) { g_devs[0] = dev; g_ndev = 1; g_reduce = 0; *out = &g_stub; return 0; }
+int dsce_create_multi(const int32_t* devs, int32_t n, dsce_ctx** out) {
+    int distinct = 1;
+    if (n < 1 || n > 64) return DSCE_EINVAL;
+    for (int i = 0; i < n; ++i) {
+        g_devs[i] = devs[i];                        /* read every entry (ASAN: an undersized list overflows) */
+        for (int j = 0; j < i; ++j) distinct = distinct && devs[j] != devs[i];
+    }
+    g_ndev = n;
+    g_reduce = distinct ? 1 : 2;
+    printf("  create_multi n=%d reduce=%d\n", n, g_reduce);
+    *out = &g_stub;
+    return 0;
+}
+int dsce_group_info(dsce_ctx* c, int32_t* n, int32_t* devs, int32_t* reduce) {
+    (void)c;
+    if (n) *n = g_ndev;
+    if (devs)
+        for (int i = 0; i < g_ndev; ++i) devs[i] = g_devs[i];
+    if (reduce) *reduce = g_reduce;
+    return 0;
+}
 int dsce_destroy(dsce_ctx* c) { (void)c; return 0; }
 const char* dsce_last_error(const dsce_ctx* c) { (void)c; return "stub"; }
 int dsce_scheme_dims(dsce_ctx* c, int32_t id, dsce_dims* d) {

@@ -69,3 +69,5 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("a GPU is present")
     with pytest.raises(engine.DsceError):
         engine.Engine(0)
+    with pytest.raises(engine.DsceError):
+        engine.Engine([0, 1])                    # dsce_create_multi (ABI 7) fails loudly too

@@ -2,11 +2,20 @@
 restated in NumPy.  Six rows' scI / |hd|^2 from ONE reciprocal (prefix
 products, one reciprocal, two products per row back) agree with the per-row
 quotients to a few ulp over the dynamic range a channel estimate spans, and
-the fallback bound [2^-1000, 2^1000] on the product catches the lanes whose
-product would over- or underflow (a zero or vanishing estimate)."""
+the fallback bound [2^-160, 2^160] on every factor (r06, ADVICE r05: r05
+bounded only the full product) catches the lanes whose product or any prefix
+would over- or underflow (a zero or vanishing estimate)."""
 import numpy as np
 
-LO, HI = 2.0 ** -1000, 2.0 ** 1000
+LO, HI = 2.0 ** -160, 2.0 ** 160
+
+
+def factor_ok(nn):
+    """mic_detect's test: max over the rows of hi(nn) - (863 << 20) as unsigned
+    < 320 << 20, i.e. every exponent field in [1023 - 160, 1023 + 160)."""
+    hi = (np.asarray(nn, dtype=np.float64).view(np.uint64) >> np.uint64(32)).astype(np.int64)
+    ex = ((hi - ((1023 - 160) << 20)) & 0xFFFFFFFF).max()
+    return bool(ex < (320 << 20))
 
 
 def batch_inverse(nn, sc):
@@ -25,7 +34,8 @@ def _batch_inverse(nn, sc):
         out[a] = inv * pp[a - 1]
         inv *= nn[a]
     out[0] = inv
-    ok = LO < pp[5] < HI
+    ok = factor_ok(nn)
+    assert ok == bool(np.all((nn >= LO) & (nn < HI)))        # the integer test is the interval
     return out, ok
 
 
@@ -51,3 +61,9 @@ def test_fallback_bound_catches_vanishing_and_huge_products():
     assert not batch_inverse(np.full(6, 1e-60), sc)[1]      # product 1e-360 underflows
     assert not batch_inverse(np.full(6, 1e60), sc)[1]       # 1e360 overflows
     assert batch_inverse(np.full(6, 1e-40), sc)[1]          # 1e-240 is representable
+    assert not batch_inverse(np.array([1.0, np.inf, 1.0, 1.0, 1.0, 1.0]), sc)[1]
+    assert not batch_inverse(np.array([1.0, np.nan, 1.0, 1.0, 1.0, 1.0]), sc)[1]
+    # a prefix in the denormals while the full product is back in range: r05's
+    # bound on pp[5] alone accepted this lane (and lost precision)
+    nn = np.array([1e-160, 1e-160, 1e200, 1e100, 1.0, 1.0])
+    assert 2.0 ** -1000 < np.prod(nn) < 2.0 ** 1000 and not batch_inverse(nn, sc)[1]

@@ -477,14 +477,12 @@ def test_stage_variants_agree(name):
     lane (k_tx_symbols, the fallback for non-row-local precoders), k_pic_fft's
     4-point network by DPP instead of on the matrix cores (and k_mic_pilot /
     k_mic_data's, with the tap GEMM's exchange by ds_bpermute), the tap GEMM
-    Bv hP instead of the low-rank operator T_k Z (mic_lr 0), every perfect-CSI
-    iteration stopping at the fixed point instead of computed (pic_skip 1), the
-    perfect-CSI passes banded instead of polyphase (pic_poly 0; FBMC) and
-    polyphase for OFDM too (pic_poly 1 with pic_chain 0: OFDM's chain is
-    otherwise k_pic_fft), the FBMC contraction as k_wpair3's pair tiles instead
-    of k_wrow3's row-tile GEMM (wrow 0), the perfect-CSI chain on a second
-    stream (ic_streams 2) or in one launch with the MMSE pilot pass (k_ic_pair,
-    ic_streams 3; with mic_lr 0 it falls back to the two launches)."""
+    Bv hP instead of the low-rank operator T_k Z (mic_lr 0), the perfect-CSI
+    passes banded instead of polyphase (pic_poly 0; FBMC) and polyphase for
+    OFDM too (pic_poly 1 with pic_chain 0: OFDM's chain is otherwise
+    k_pic_fft), the FBMC contraction as k_wpair3's pair tiles instead of
+    k_wrow3's row-tile GEMM (wrow 0).  (pic_skip and ic_streams 2 / 3, measured
+    neutral, were retired in r06.)"""
     S = harness.setup("default", schemes=(name,), snr_db=[10.0, 25.0, 40.0])
     eng = harness.engine(S, batch=512)
     eng.set_option("stage_split", 1)
@@ -501,9 +499,8 @@ def test_stage_variants_agree(name):
                 {"jakes_win": 0}, {"txrx_fft": 0}, {"mmse_ic": 0, "fuse_stage": 0, "pic_chain": 0},
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
-                {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3}, {"pic_skip": 1},
-                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0}, {"ic_streams": 2},
-                {"ic_streams": 3}, {"ic_streams": 3, "mic_lr": 0})
+                {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3},
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
@@ -527,7 +524,7 @@ def test_options_are_validated():
     # the r01-r02 variants pruned in r03 (4M k_wpair, the per-stage k_mic_fft
     # path, the second stream): their options are gone
     for name in ("wpair_3m", "wda_3m", "streams", "qidx", "stage0_fft", "mic_mfma", "pilot_fft", "mic_yic",
-                 "pilot_fuse", "mic2"):
+                 "pilot_fuse", "mic2", "pic_skip", "ic_streams"):         # the last two retired in r06
         with pytest.raises(DsceError):
             eng.set_option(name, 0)
     assert eng.get_option("fuse_stage") == 1
@@ -570,25 +567,3 @@ def test_setup_with_gpu_tx_matrices_gives_the_same_counts():
         np.testing.assert_array_equal(ea.run(SEED, 0, 256), eb.run(SEED, 0, 256))
         ea.close()
         eb.close()
-
-
-
-def test_pic_fixed_point_skip_is_exact():
-    """k_pic_fft's early exit (option pic_skip): a wave whose iteration repeats
-    the previous decisions of every data row copies that iteration's counts and
-    traces into the later ones instead of computing them.  Exact by construction
-    (same inputs, same instructions); checked here against the full computation
-    at every SNR point of the script (where most waves converge at high SNR):
-    identical counts over 512 realisations, and an identical per-stage trace of
-    a unit, decisions and y_perf included."""
-    S = harness.setup("default", schemes=("ofdm",))
-    full = harness.engine(S, batch=256, options={"pic_skip": 0})
-    fast = harness.engine(S, batch=256, options={"pic_skip": 1})
-    np.testing.assert_array_equal(fast.run(SEED, 0, 512), full.run(SEED, 0, 512))
-    for k in (0, 6):
-        a, b = fast.trace_unit(0, SEED, 21, k), full.trace_unit(0, SEED, 21, k)
-        np.testing.assert_array_equal(a["dec_p"], b["dec_p"])
-        np.testing.assert_array_equal(np.nan_to_num(a["yperf"]), np.nan_to_num(b["yperf"]))
-    assert "pic_fft" in fast.path_info(0)
-    full.close()
-    fast.close()

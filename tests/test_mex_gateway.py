@@ -202,6 +202,10 @@ def test_outputs_sized_from_engine_state(results):
     assert results["tx_matrices_ofdm"] == ("OK", "540x336") and results["tx_matrices_fbmc"] == ("OK", "540x720")
     assert results["get_mse"] == ("OK", "5x7")                          # [iter+1, snr, scheme]
     assert results["structured_check"] == ("OK", "1x7")
+    # a device vector makes one multi-device context (ABI 7); 'group_info' reports it
+    assert results["group_info_single"] == ("OK", "1x1")
+    assert results["create_multi_8"] == ("OK", "") and results["group_info_multi"] == ("OK", "1x8")
+    assert results["run_multi"] == ("OK", "5x28") and results["create_again"][0] == "OK"
 
 
 def test_arity_and_argument_checks(results):
@@ -215,6 +219,7 @@ def test_arity_and_argument_checks(results):
             "tx_matrices_real_signal", "tx_matrices_phydyas")
     for k in args:
         assert results[k] == ("ERR", "dsce:args"), (k, results[k])
+    assert results["create_empty_devices"] == ("ERR", "dsce:args")
     assert results["run_before_create"] == ("ERR", "dsce:state")
     assert results["after_destroy"] == ("ERR", "dsce:state")
 

@@ -1,7 +1,6 @@
 """CPU: tools/prof_summary.group_span over synthetic rocprofv3 kernel traces —
 the IC group's span per step is first start -> last end of the (k_pic_fft,
-k_mic_pilot, k_mic_data) triple, or of the (k_ic_pair, k_mic_data) pair when
-the chain and the pilot pass share one launch (ic_streams 3)."""
+k_mic_pilot, k_mic_data) triple."""
 import csv
 import os
 import sys
@@ -19,21 +18,15 @@ def _trace(path, rows):
             w.writerow({"Kernel_Name": name, "Start_Timestamp": t0, "End_Timestamp": t1})
 
 
-def test_group_span_triple_and_pair(tmp_path):
+def test_group_span_triple(tmp_path):
     import prof_summary
     tri = tmp_path / "tri"
     _trace(str(tri), [("void dsce::k_jakes_grp<28, 16>(x)", 0, 50),
-                      ("void dsce::k_pic_fft<2, 2, false, true, true, false>(x)", 100, 300),
+                      ("void dsce::k_pic_fft<2, 2, false, true, true>(x)", 100, 300),
                       ("void dsce::k_mic_pilot<2, 2, 16, false, true, true>(x)", 300, 420),
                       ("void dsce::k_mic_data<2, 2, 16, false, true, true>(x)", 420, 620),
-                      ("void dsce::k_pic_fft<2, 2, false, true, true, false>(x)", 1000, 1210),
+                      ("void dsce::k_pic_fft<2, 2, false, true, true>(x)", 1000, 1210),
                       ("void dsce::k_mic_pilot<2, 2, 16, false, true, true>(x)", 1210, 1330),
                       ("void dsce::k_mic_data<2, 2, 16, false, true, true>(x)", 1330, 1540)])
     assert prof_summary.group_span(str(tri)) == (520 + 540) / 2
-    pair = tmp_path / "pair"
-    _trace(str(pair), [("void dsce::k_ic_pair<2, 2, true, true>(x)", 100, 420),
-                       ("void dsce::k_mic_data<2, 2, 16, false, true, true>(x)", 420, 620),
-                       ("void dsce::k_ic_pair<2, 2, true, true>(x)", 1000, 1300),
-                       ("void dsce::k_mic_data<2, 2, 16, false, true, true>(x)", 1300, 1500)])
-    assert prof_summary.group_span(str(pair)) == (520 + 500) / 2
     assert prof_summary.group_span(str(tmp_path / "none")) is None

@@ -58,7 +58,7 @@ GROUPS = (("k_jakes", "k_jakes"), ("k_tx_rows", "tx"), ("k_tx_symbols", "tx"), (
           ("k_pic_fft", "perfect_ic"), ("k_poly_", "perfect_ic"), ("k_mic_pilot", "k_mic_pilot"),
           ("k_mic_data", "k_mic_data"), ("k_wpair3", "k_wcontract"), ("k_wrow3", "k_wcontract"),
           ("k_wcontract_valu", "k_wcontract"), ("k_pilot_pre", "k_pilot_pre"), ("k_stage", "k_stage"),
-          ("k_precode", "k_stage"), ("k_ls", "k_stage"), ("k_detect", "k_stage"), ("k_ic_pair", "ic_pair"))
+          ("k_precode", "k_stage"), ("k_ls", "k_stage"), ("k_detect", "k_stage"))
 
 
 def short(name):
@@ -68,15 +68,13 @@ def short(name):
 
 def group_span(sdir):
     """Mean span (ns) of the i-th k_pic_fft / k_mic_pilot / k_mic_data dispatch
-    triple (ic_streams 3: k_ic_pair / k_mic_data pair) in the stats run's kernel
-    trace: first start to last end."""
+    triple in the stats run's kernel trace: first start to last end."""
     try:
         tr = one(os.path.join(sdir, "**", "*_kernel_trace.csv"))
     except SystemExit:                          # one(): no trace in this run
         return None
     rows = list(csv.DictReader(open(tr)))
-    pair = any("k_ic_pair" in r["Kernel_Name"] for r in rows)
-    seq = {"k_ic_pair": [], "k_mic_data": []} if pair else {"k_pic_fft": [], "k_mic_pilot": [], "k_mic_data": []}
+    seq = {"k_pic_fft": [], "k_mic_pilot": [], "k_mic_data": []}
     for r in rows:
         n = r["Kernel_Name"]
         for k in seq:
@@ -119,15 +117,11 @@ def main_all(argv):
         e["avg_duration_ns_rocprof"] += avg.get(k, 0.0)
         for c in sq:
             e["sq_per_launch"][c] += sq[c].get(k, 0.0)
-    # the concurrent IC group of the FFT-form OFDM path (ic_streams 2 / 3): its
-    # members' counters (the --pmc passes serialise the dispatches, so these are
-    # the kernels' isolated counts) and, from the stats run's kernel trace, the
-    # mean span first start -> last end of each (pic, pilot, data) triple
+    # the IC group of the FFT-form OFDM path: its members' counters and, from
+    # the stats run's kernel trace, the mean span first start -> last end of
+    # each (pic, pilot, data) triple
     mem = [g for g in ("perfect_ic", "k_mic_pilot", "k_mic_data") if g in groups]
-    if "ic_pair" in groups and "k_mic_data" in groups:
-        mem = ["ic_pair", "k_mic_data"]         # ic_streams 3: k_ic_pair, then k_mic_data
-    if (mem == ["ic_pair", "k_mic_data"] or
-            (len(mem) == 3 and any("k_pic_fft" in k for k in groups["perfect_ic"]["kernels"]))):
+    if len(mem) == 3 and any("k_pic_fft" in k for k in groups["perfect_ic"]["kernels"]):
         e = {"kernels": sum((groups[g]["kernels"] for g in mem), []), "members": mem}
         for key in ("fetch_size_kb_per_launch", "write_size_kb_per_launch", "avg_duration_ns_rocprof"):
             e[key] = sum(groups[g][key] for g in mem)
