@@ -10,6 +10,9 @@ option):
     python -m dsce.simulate --config default --reps 4096 --out run.json --figures figs/
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
         -m dsce.simulate --config c5 --reps 10048 --out c5.json     # BASELINE config 5
+    python -m dsce.simulate --config c5 --devices 0,1,2,3,4,5,6,7   # one process, one multi-device
+                                                                    # context (dsce_create_multi: the
+                                                                    # in-library RCCL all-reduce)
 
 Progress lines mirror the script's `disp` (script:567); results go through
 dsce.results (JSON [+ NPZ], Figures 2-5)."""
@@ -40,6 +43,9 @@ def main(argv=None):
                     help="doubly_flat: PSACE interpolation method (the script uses 'linear')")
     ap.add_argument("--shard", choices=("reps", "snr"), default="reps",
                     help="multi-rank split: realisation slices (default) or SNR points")
+    ap.add_argument("--devices", default=None,
+                    help="comma-separated HIP devices of ONE multi-device context (dsce_create_multi, ABI 7): "
+                         "the engine shards the realisations and all-reduces the counters itself (RCCL)")
     a = ap.parse_args(argv)
 
     from dsce import results
@@ -58,6 +64,9 @@ def main(argv=None):
     # and the all-reduce run at every world size, 1 included: the RCCL path of
     # the counters is the same code with one rank or eight
     distributed = "WORLD_SIZE" in os.environ
+    devices = [int(d) for d in a.devices.split(",")] if a.devices else None
+    if devices and distributed:
+        raise SystemExit("--devices is the single-process multi-device path; do not combine it with a launcher")
     if distributed:
         import torch
         import torch.distributed as dist
@@ -67,7 +76,7 @@ def main(argv=None):
         dist.init_process_group(os.environ.get("DSCE_DIST_BACKEND", "nccl"))
     names = tuple(a.schemes.split(","))
     from dsce.engine import gpu_tx
-    S = build_setup(a.config, schemes=names, tx=gpu_tx(device))      # G / Q on the GPU (row f1)
+    S = build_setup(a.config, schemes=names, tx=gpu_tx(devices[0] if devices else device))   # G / Q on the GPU (row f1)
     reps = a.reps if a.reps is not None else S.n_repetitions    # script:19 / :44, exactly (no rounding)
     if reps < 1:
         raise SystemExit("--reps must be >= 1")
@@ -89,13 +98,13 @@ def main(argv=None):
     bits = None
     setup_s, t0 = 0.0, time.perf_counter()
     if mine:                                         # a rank with an empty shard contributes zeros
-        eng = build_engine(Sr, device=device, batch=max(64, min(a.batch, mine)), options=options)
+        eng = build_engine(Sr, device=devices or device, batch=max(64, min(a.batch, mine)), options=options)
         setup_s = time.perf_counter() - t0
         sub = np.zeros(eng.counter_shape(), dtype=np.int64)
         if a.mse:
             eng.enable_mse()
         done, t0 = 0, time.perf_counter()
-        step = min(a.batch, mine)
+        step = min(a.batch * (len(devices) if devices else 1), mine)
         while done < mine:
             n = min(step, mine - done)
             eng.run(a.seed, first + done, n, sub)
@@ -111,6 +120,8 @@ def main(argv=None):
             pw[:, s0:s0 + ns] = p_
         eng.close()
     extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world, "shard": a.shard}
+    if devices:
+        extra["devices"] = devices
     if distributed:
         dev = "cuda" if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl" else None
         info = {}

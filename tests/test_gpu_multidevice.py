@@ -81,3 +81,23 @@ def test_multi_device_rejects_bad_devices():
         Engine([0, 4096])
     with pytest.raises(DsceError):
         Engine([])
+
+
+def test_simulate_devices_flag_equals_one_device(tmp_path):
+    """`python -m dsce.simulate --devices ...` (one process, one multi-device
+    context: the MATLAB host's path through the Python twin) counts exactly
+    like the single-device run, through RCCL ([0]) and the host sum ([0, 0])."""
+    import json
+    import os
+    import subprocess
+    import sys
+    args = ["--config", "default", "--schemes", "ofdm", "--reps", "300", "--batch", "128"]
+    env = dict(os.environ, PYTHONPATH=harness.PKG)
+    runs = {}
+    for tag, extra in (("one", []), ("rccl", ["--devices", "0"]), ("host", ["--devices", "0,0"])):
+        out = tmp_path / (tag + ".json")
+        subprocess.run([sys.executable, "-m", "dsce.simulate", *args, *extra, "--out", str(out)], cwd=harness.PKG,
+                       env=env, check=True, timeout=240, capture_output=True)
+        runs[tag] = json.load(open(out))
+    for tag in ("rccl", "host"):
+        assert np.array_equal(np.array(runs[tag]["counts"]), np.array(runs["one"]["counts"])), tag
