@@ -2309,6 +2309,57 @@ int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_
     API_END
 }
 
+int dsce_transmission_matrix(dsce_ctx* ctx, int32_t id, uint64_t seed, uint64_t rep, double* d_out) {
+    API_BEGIN
+    check_ctx(ctx);
+    Scheme& s = get_scheme(ctx, id);
+    if (!d_out) throw ApiError(DSCE_EINVAL, "null output");
+    // the realisation at lane rep % 8 of a 64-realisation Jakes batch, every
+    // sample formed (as dsce_channel_realise without realise_win)
+    const int N = ctx->ch.N, R = 64, lane = (int)(rep % 8), LK = s.LK;
+    std::vector<int> qlo(LK, 0), qhi(LK, 0);
+    for (int c = 0; c < LK; ++c) {
+        int lo = N, hi = 0;
+        for (int n = 0; n < N; ++n)
+            if (nz(s.Q[(size_t)c * N + n])) {
+                lo = std::min(lo, n);
+                hi = n + 1;
+            }
+        qlo[c] = lo < hi ? lo : 0;
+        qhi[c] = hi;
+    }
+    std::vector<void*> tmp;
+    auto talloc = [&](size_t bytes) {
+        void* p;
+        DSCE_HIP_CHECK(hipMalloc(&p, bytes ? bytes : 1));
+        tmp.push_back(p);
+        return p;
+    };
+    try {
+        double2* ir = (double2*)talloc((size_t)ctx->ch.ntap * N * R * sizeof(double2));
+        double2* G = (double2*)talloc((size_t)N * LK * sizeof(double2));
+        double2* Q = (double2*)talloc((size_t)N * LK * sizeof(double2));
+        double2* hg = (double2*)talloc((size_t)N * LK * sizeof(double2));
+        double2* D = (double2*)talloc((size_t)LK * LK * sizeof(double2));
+        int* dq = (int*)talloc(2 * (size_t)LK * sizeof(int));
+        launch_jakes(ctx->stream, ctx->op, ctx->ch, seed, rep - (uint64_t)lane, R, ir);
+        DSCE_HIP_CHECK(hipMemcpyAsync(G, s.G.data(), s.G.size() * sizeof(double2), hipMemcpyHostToDevice, ctx->stream));
+        DSCE_HIP_CHECK(hipMemcpyAsync(Q, s.Q.data(), s.Q.size() * sizeof(double2), hipMemcpyHostToDevice, ctx->stream));
+        DSCE_HIP_CHECK(hipMemcpyAsync(dq, qlo.data(), LK * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        DSCE_HIP_CHECK(hipMemcpyAsync(dq + LK, qhi.data(), LK * sizeof(int), hipMemcpyHostToDevice, ctx->stream));
+        setup_transmission_matrix(ctx->stream, ctx->ch, LK, ir, R, lane, G, Q, dq, dq + LK, hg, D);
+        DSCE_HIP_CHECK(hipGetLastError());
+        DSCE_HIP_CHECK(hipMemcpyAsync(d_out, D, (size_t)LK * LK * sizeof(double2), hipMemcpyDeviceToHost, ctx->stream));
+        DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    } catch (...) {
+        (void)hipStreamSynchronize(ctx->stream);
+        for (void* p : tmp) (void)hipFree(p);
+        throw;
+    }
+    for (void* p : tmp) DSCE_HIP_CHECK(hipFree(p));
+    API_END
+}
+
 int dsce_get_correlation(dsce_ctx* ctx, int32_t id, double* r_hp, double* r_est, double* r_noi) {
     API_BEGIN
     check_ctx(ctx);

@@ -265,6 +265,10 @@ struct TxDesc {
 static constexpr int PEAK_MFMA_PER_ITER = 8;
 void launch_mfma_f64_peak(hipStream_t s, int blocks, int iters, double* out);
 void setup_tx_matrix(hipStream_t s, const TxDesc& d, const double* proto, double2* G, double2* Q);
+// D = Q^H H G of lane `lane` of a Jakes batch `ir` (dsce_transmission_matrix, test probe)
+void setup_transmission_matrix(hipStream_t s, const ChannelK& ch, int LK, const double2* ir, int R, int lane,
+                               const double2* G, const double2* Q, const int* qlo, const int* qhi, double2* hg,
+                               double2* D);
 void setup_fused_stage(hipStream_t s, const Band& Wb, int LK, int NP, const double2* w, long long w_elems,
                        const double2* wd, int nslices, const int* pil_blk, const int* pilot_pos, int ncol,
                        double2* wpil, double2* wda);

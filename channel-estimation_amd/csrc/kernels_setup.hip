@@ -465,6 +465,51 @@ void setup_wpair(hipStream_t s, const Band& Wb, int NP, const double2* w, long l
     if (w3) hipLaunchKernelGGL(k_wpair_pack3, dim3(256, nslices), dim3(256), 0, s, wp_elems, P.nks, wp, w3);
 }
 
+// ---------------------------------------------------------------------------
+// D = Q^H H G of one realisation (dsce_transmission_matrix, the parity probe of
+// SURVEY §8(b); script:381-393, H = GetConvolutionMatrix{1}, FastFading.m:276-295:
+// H[n, n - d_q] = IR_q[n] for n >= d_q).  Two passes over the dense operators:
+// HG[n][c] = sum_q IR_q[n] G[n - d_q][c], then D[r][c] = sum_n conj(Q[n][r])
+// HG[n][c] over Q column r's support [qlo[r], qhi[r]).  Test-only: the hot path
+// never forms D (diag(D) and D u only).
+// ---------------------------------------------------------------------------
+__global__ void k_hg(ChannelK ch, int LK, const double2* __restrict__ ir, int R, int lane,
+                     const double2* __restrict__ G, double2* __restrict__ hg) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)ch.N * LK) return;
+    const int n = (int)(i % ch.N);
+    const size_t c = i / ch.N;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int q = 0; q < ch.ntap; ++q) {
+        const int m = n - ch.tap_delay[q];
+        if (m >= 0) c_fma(acc, ir[((size_t)q * ch.N + n) * R + lane], G[c * ch.N + m]);
+    }
+    hg[i] = acc;
+}
+
+__global__ void k_qh_hg(int N, int LK, const double2* __restrict__ Q, const int* __restrict__ qlo,
+                        const int* __restrict__ qhi, const double2* __restrict__ hg, double2* __restrict__ D) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)LK * LK) return;
+    const int r = (int)(i % LK);
+    const size_t c = i / LK;
+    double2 acc = make_double2(0.0, 0.0);
+    for (int n = qlo[r]; n < qhi[r]; ++n) {
+        const double2 q = Q[(size_t)r * N + n], h = hg[c * N + n];
+        acc.x = fma(q.x, h.x, fma(q.y, h.y, acc.x));          // conj(q) h
+        acc.y = fma(q.x, h.y, fma(-q.y, h.x, acc.y));
+    }
+    D[i] = acc;
+}
+
+void setup_transmission_matrix(hipStream_t s, const ChannelK& ch, int LK, const double2* ir, int R, int lane,
+                               const double2* G, const double2* Q, const int* qlo, const int* qhi, double2* hg,
+                               double2* D) {
+    const size_t nhg = (size_t)ch.N * LK, nd = (size_t)LK * LK;
+    hipLaunchKernelGGL(k_hg, dim3((unsigned)((nhg + 255) / 256)), dim3(256), 0, s, ch, LK, ir, R, lane, G, hg);
+    hipLaunchKernelGGL(k_qh_hg, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, ch.N, LK, Q, qlo, qhi, hg, D);
+}
+
 // G[n, l + L k] in closed form (OFDM.m:153-165, :184-203; FBMC.m:255-285,
 // :318-342) and Q = G * rx_scale with OFDM cyclic-prefix samples zeroed
 // (OFDM.m:205-218).  The IFFT of a unit impulse at bin b is

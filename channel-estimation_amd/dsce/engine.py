@@ -24,6 +24,7 @@ EXPORTED = [
     "dsce_set_noise_slot", "dsce_set_interpolation", "dsce_enable_mse", "dsce_get_mse", "dsce_trace_unit_ex",
     "dsce_scheme_dims", "dsce_path_info", "dsce_set_option", "dsce_get_option", "dsce_fp64_mfma_peak",
     "dsce_kernel_work", "dsce_structured_check", "dsce_create_multi", "dsce_group_info",
+    "dsce_transmission_matrix",
 ]
 
 ABI_VERSION = 7
@@ -112,6 +113,7 @@ def load_library(path=None):
     lib.dsce_bits_per_rep.argtypes = [vp, C.c_int32, i64p]
     lib.dsce_channel_realise.argtypes = [vp, C.c_uint64, C.c_uint64, dp]
     lib.dsce_get_correlation.argtypes = [vp, C.c_int32, dp, dp, dp]
+    lib.dsce_transmission_matrix.argtypes = [vp, C.c_int32, C.c_uint64, C.c_uint64, dp]
     lib.dsce_get_W.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, dp]
     lib.dsce_trace_unit.argtypes = [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32, dp, dp, dp, dp]
     lib.dsce_enable_timing.argtypes = [vp, C.c_int32]
@@ -306,6 +308,15 @@ class Engine:
         out = np.zeros(2 * self.N * self.ntaps)
         self._chk(self.lib.dsce_channel_realise(self.h, int(seed), int(rep), _dptr(out)), "dsce_channel_realise")
         return out.view(np.complex128).reshape(self.N, self.ntaps, order="F")
+
+    def transmission_matrix(self, sid, seed, rep):
+        """D = Q^H H G (LK x LK) of realisation `rep` (dsce_transmission_matrix,
+        script:381-393)."""
+        LK = self.schemes[sid].LK
+        out = np.zeros(2 * LK * LK)
+        self._chk(self.lib.dsce_transmission_matrix(self.h, int(sid), int(seed), int(rep), _dptr(out)),
+                  "dsce_transmission_matrix")
+        return out.view(np.complex128).reshape(LK, LK, order="F")
 
     def correlation(self, sid):
         NP = self.schemes[sid].n_pilots

@@ -307,6 +307,12 @@ int dsce_set_interpolation(dsce_ctx* ctx, int32_t scheme_id, const double* inter
 /* ---- parity probes (same kernels as dsce_run) ---------------------------- */
 /* ImpulseResponse of realisation `rep`: N x n_taps complex, column-major. */
 int dsce_channel_realise(dsce_ctx* ctx, uint64_t seed, uint64_t rep, double* ir_out);
+/* D = Q^H H G of realisation `rep` for a scheme (script:381-393, the matrix whose
+ * diagonal is the perfect-CSI one-tap channel h and whose off-diagonal part the
+ * perfect-CSI IC subtracts, script:541-543): LK x LK complex, column-major.  The
+ * Monte-Carlo kernels never form D; this probe builds it
+ * from the context's dense G / Q and the run's Jakes realisation (ABI 7). */
+int dsce_transmission_matrix(dsce_ctx* ctx, int32_t scheme_id, uint64_t seed, uint64_t rep, double* d_out);
 /* R_hP (NP x NP), R_est / R_noI (n_snr x NP x NP, each NP x NP column-major). */
 int dsce_get_correlation(dsce_ctx* ctx, int32_t scheme_id, double* r_hp, double* r_est, double* r_noi);
 /* W (variant 0) or W0 (variant 1) of SNR index k in the reference layout:

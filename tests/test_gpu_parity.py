@@ -567,3 +567,30 @@ def test_setup_with_gpu_tx_matrices_gives_the_same_counts():
         np.testing.assert_array_equal(ea.run(SEED, 0, 256), eb.run(SEED, 0, 256))
         ea.close()
         eb.close()
+
+
+def test_transmission_matrix_probe_matches_oracle():
+    """SURVEY §8(b)'s probe dsce_transmission_matrix: D = Q' H G of one
+    realisation (script:381-393) from the engine's operators and the run's
+    Jakes realisation equals the oracle's literal product (sparse
+    GetConvolutionMatrix H, refsim.conv_matrix) to 1e-12 max|D|, for OFDM and
+    FBMC and realisations at several lanes of the Jakes batch; its diagonal is
+    the perfect-CSI one-tap channel h the hot path forms without D
+    (dsce_trace_unit_ex's h_perfect)."""
+    S = harness.setup("default", schemes=("ofdm", "fbmc_aux"), snr_db=[25.0])
+    eng = harness.engine(S, batch=256)
+    ch = S.chan
+    try:
+        for sid, name in enumerate(("ofdm", "fbmc_aux")):
+            sc = S.schemes[name]
+            for rep in (3, 64, 1 << 33):
+                D = eng.transmission_matrix(sid, SEED, rep)
+                ir = refsim.jakes_ir(SEED, rep, S.N, ch["dt"], ch["pdp_norm"], ch["idx_taps"], ch["fD"], ch["paths"])
+                H = refsim.conv_matrix(ir, ch["pdp"], S.N)
+                Do = sc["Q"].conj().T @ (H @ sc["G"])
+                scale = np.abs(Do).max()
+                np.testing.assert_allclose(D, Do, rtol=0, atol=1e-12 * scale, err_msg="%s rep %d" % (name, rep))
+                h = eng.trace_unit(sid, SEED, rep, 0)["h"]
+                np.testing.assert_allclose(h, np.diag(D), rtol=0, atol=1e-12 * scale, err_msg=name)
+    finally:
+        eng.close()
