@@ -1383,15 +1383,34 @@ void update_jakes_groups(dsce_ctx* c) {
     const int L = JakesChunks::LEN;
     const std::vector<int>& n0 = jk.n0h;
     if (n0.empty() || !(th > 0.0) || th * 0.5 * (L - 1) > JAKES_XMAX) return;
-    std::vector<int2> g;
-    double xmax = 0.0;
-    for (size_t i = 0; i < n0.size();) {
-        size_t j = i + 1;
-        while (j < n0.size() && th * 0.5 * (n0[j] + L - 1 - n0[i]) <= JAKES_XMAX) ++j;
-        g.push_back(make_int2((int)i, (int)(j - i)));
-        xmax = std::max(xmax, th * 0.5 * (n0[j - 1] + L - 1 - n0[i]));
-        i = j;
+    // greedy runs of span <= smax samples (first to last sample of the run)
+    auto runs = [&](double smax) {
+        std::vector<int2> g;
+        for (size_t i = 0; i < n0.size();) {
+            size_t j = i + 1;
+            while (j < n0.size() && (double)(n0[j] + L - 1 - n0[i]) <= smax) ++j;
+            g.push_back(make_int2((int)i, (int)(j - i)));
+            i = j;
+        }
+        return g;
+    };
+    // the fewest runs within |theta k| <= JAKES_XMAX, then (r06) the smallest span
+    // that still needs no more runs: C2's 14 windows split 7 + 7 instead of
+    // 11 + 3, so the widest run needs MT 24 instead of 28 terms and the anchor
+    // lanes' Horner work is balanced
+    const int smax_x = (int)std::min(std::floor(2.0 * JAKES_XMAX / th), 1e9);
+    std::vector<int2> g = runs(smax_x);
+    {
+        int lo = L - 1, hi = smax_x;
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (runs(mid).size() <= g.size()) hi = mid;
+            else lo = mid + 1;
+        }
+        g = runs(hi);
     }
+    double xmax = 0.0;
+    for (const int2& r : g) xmax = std::max(xmax, th * 0.5 * (n0[r.x + r.y - 1] + L - 1 - n0[r.x]));
     if (2 * g.size() > n0.size()) return;
     int mt = 0;
     for (int m : {16, 24, 28}) {                           // 28 covers x <= 3 (7.7e-18)
@@ -2760,7 +2779,7 @@ int dsce_fp64_mfma_peak(dsce_ctx* ctx, double* tflops) {
 // Kernel-selection options (Opts); the defaults are the measured-best path.
 #define DSCE_OPTIONS(X)                                                                                  \
     X(xcd) X(fuse_stage) X(pic_chain) X(pfuse) X(stage_split) X(stage_rb) X(noise_fuse) \
-    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(mic_lr) X(pic_poly) X(wrow)
+    X(snr_chunk) X(jakes_rpw) X(wtrim) X(wcontract_valu) X(mmse_ic) X(jakes_win) X(txrx_fft) X(snr_base) X(jakes_mom) X(realise_win) X(tx_rows) X(pic_net) X(mic_net) X(mic_lr) X(pic_poly) X(wrow) X(jakes_grp2)
 
 static int set_option_one(dsce_ctx* ctx, const char* name, int64_t value) {
     API_BEGIN

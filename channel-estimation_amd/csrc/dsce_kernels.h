@@ -39,6 +39,8 @@ struct Opts {
                               // (r04 box, C3: 14.3 -> 8.7 ms per iteration); 0 = the banded passes
     int wrow = 1;             // unfused W contraction of 32-row blocks (FBMC, C5) as one GEMM per row tile
                               // (k_wrow3: X = hP v_c as the B operand, no per-tile epilogue); 0 = k_wpair3
+    int jakes_grp2 = 1;       // two-tap channels: k_jakes_grp2 (both taps per wave, each Philox block drawn
+                              // once, LG = 16 / anchor groups); 0 = k_jakes_grp per tap
     int jakes_mom = 2;        // Jakes taps of the read windows: 2 = Taylor anchors over groups of windows
                               // (k_jakes_grp), 1 = one anchor per window (k_jakes_mom), 0 = recurrence;
                               // each where its truncation is below rounding, else the next lower

@@ -612,6 +612,120 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
+// k_jakes_grp for channels with two non-zero taps (r06; C2-C4's VehicularA at
+// 360 kHz): a wave holds 2 realisations x 2 taps x NG anchor groups of LG =
+// 16 / NG lanes.  One Philox block of the THETA / PHI streams carries path p's
+// uniforms of BOTH taps (element e = tap + 2 p, counter e >> 1 = p: words (x, y)
+// for tap 0, (z, w) for tap 1), so each block is drawn once instead of once per
+// tap (k_jakes_grp's grid is per tap), and the four (realisation, tap) pairs of
+// a wave split its lanes four ways: an anchor's moments sum over LG = 8 lanes at
+// C2 (three DPP stages instead of four).  LDS: [wave][realisation][tap]{d, phi}
+// per path; theta = 2 pi d dt is formed where it is used (the same expression
+// as k_jakes_grp's table).  Same moments, anchors and Horner evaluation.
+template <int MT, int LG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_jakes_grp2(ChannelK ch, uint64_t seed, uint64_t rep0, int R, double2* __restrict__ ir,
+             const int* __restrict__ chunk_n0, const int2* __restrict__ grp, int ngrp) {
+    static_assert(LG == 4 || LG == 8 || LG == 16, "lanes per anchor");
+    constexpr int JCH = JakesChunks::LEN, RPW = 2, NG = 16 / LG;
+    extern __shared__ double sm[];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int P = ch.paths;
+    double* wbase = sm + (size_t)wv * RPW * 4 * P;              // [sub][tap][d | phi][P]
+    {
+        const int sub = lane >> 5, sl = lane & 31;
+        const uint64_t rep = rep0 + (uint64_t)((blockIdx.x * 4 + wv) * RPW + sub);
+        double* d = wbase + (size_t)sub * 4 * P;
+        for (int p = sl; p < P; p += 32) {
+            const uint4 wt = stream_block(seed, rep, STREAM_THETA, 0, (uint32_t)p);
+            const uint4 wp = stream_block(seed, rep, STREAM_PHI, 0, (uint32_t)p);
+            const double t0 = u53(wt.x, wt.y), t1 = u53(wt.z, wt.w);
+            d[p] = (ch.model == 0) ? cos((t0 * 2.0) * M_PI) * ch.fD : (2.0 * (t0 - 0.5)) * ch.fD;
+            d[P + p] = u53(wp.x, wp.y);
+            d[2 * P + p] = (ch.model == 0) ? cos((t1 * 2.0) * M_PI) * ch.fD : (2.0 * (t1 - 0.5)) * ch.fD;
+            d[3 * P + p] = u53(wp.z, wp.w);
+        }
+    }
+    __syncthreads();
+    // lane -> (realisation sub, tap, anchor group gi), LG lanes per anchor
+    const int g = lane / LG, li = lane % LG;
+    const int sub = g / (2 * NG), tap = (g / NG) & 1, gi = g % NG;
+    if (gi >= ngrp) return;
+    const double* ds = wbase + (size_t)sub * 4 * P + (size_t)tap * 2 * P;
+    const double* ph = ds + P;
+    const int rl = (blockIdx.x * 4 + wv) * RPW + sub;
+    const int2 gr = grp[gi];
+    const int na = chunk_n0[gr.x], nb = chunk_n0[gr.x + gr.y - 1];
+    const double cen = 0.5 * ((double)na + (double)nb + (JCH - 1));
+    const double tc = cen * ch.dt;
+    double2 M[MT + 1];
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) M[m] = make_double2(0.0, 0.0);
+    int p = li;
+    for (; p + LG < P; p += 2 * LG) {
+        const double d0 = ds[p], d1 = ds[p + LG];
+        const double2 z0 = cis_turns(ph[p] + d0 * tc), z1 = cis_turns(ph[p + LG] + d1 * tc);
+        const double t0 = TWO_PI * (d0 * ch.dt), t1 = TWO_PI * (d1 * ch.dt);
+        M[0].x += z0.x + z1.x;
+        M[0].y += z0.y + z1.y;
+        double w0 = 1.0, w1 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            w1 *= t1;
+            M[m].x = fma(z1.x, w1, fma(z0.x, w0, M[m].x));
+            M[m].y = fma(z1.y, w1, fma(z0.y, w0, M[m].y));
+        }
+    }
+    if (p < P) {
+        const double d0 = ds[p];
+        const double2 z0 = cis_turns(ph[p] + d0 * tc);
+        const double t0 = TWO_PI * (d0 * ch.dt);
+        M[0].x += z0.x;
+        M[0].y += z0.y;
+        double w0 = 1.0;
+#pragma unroll
+        for (int m = 1; m <= MT; ++m) {
+            w0 *= t0;
+            M[m].x = fma(z0.x, w0, M[m].x);
+            M[m].y = fma(z0.y, w0, M[m].y);
+        }
+    }
+    double f = 1.0;
+#pragma unroll
+    for (int m = 0; m <= MT; ++m) {
+        double mx = M[m].x, my = M[m].y;
+        mx += dpp_d<QP_XOR1>(mx);
+        my += dpp_d<QP_XOR1>(my);
+        mx += dpp_d<QP_XOR2>(mx);
+        my += dpp_d<QP_XOR2>(my);
+        if constexpr (LG >= 8) {
+            mx += dpp_d<0x141>(mx);                             // row_half_mirror: the other quad of 8
+            my += dpp_d<0x141>(my);
+        }
+        if constexpr (LG >= 16) {
+            mx += dpp_d<0x128>(mx);                             // row_ror 8: the other half of the row
+            my += dpp_d<0x128>(my);
+        }
+        if (m >= 2) f /= (double)m;                             // constant-folded
+        M[m] = make_double2(mx * f, my * f);
+    }
+    const double gs = ch.sqrt_pdp[tap] / sqrt((double)P);
+    const int ns = gr.y * JCH;
+    for (int j = li; j < ns; j += LG) {
+        const int n = chunk_n0[gr.x + j / JCH] + j % JCH;
+        const double kp = (double)n - cen;
+        double2 acc = M[MT];
+#pragma unroll
+        for (int m = MT - 1; m >= 0; --m) {
+            const double ax = acc.x;
+            acc.x = fma(-kp, acc.y, M[m].x);
+            acc.y = fma(kp, ax, M[m].y);
+        }
+        if (n < ch.N) ir[((size_t)tap * ch.N + n) * R + rl] = make_double2(gs * acc.x, gs * acc.y);
+    }
+}
+
 // Box-Muller pair of the random-stream spec (include/dsce.h): u1 = u53(w0,w1),
 // u2 = u53(w2,w3), (re, im) = sqrt(-2 log(1-u1)) (cos, sin)(2 pi u2).
 //
@@ -793,6 +907,23 @@ int launch_jakes(hipStream_t s, const Opts& op, const ChannelK& ch, uint64_t see
     if (jc && jc->n0 && op.jakes_win && R % 8 == 0 && (size_t)8 * 4 * ch.paths * sizeof(double) <= 64 * 1024) {
         // the phase-moment form where its Taylor remainder is negligible
         // (|theta| (LEN - 1) / 2 <= 0.3), else the recurrence
+        // two non-zero taps and 1 / 2 / 4 anchor groups: both taps in one wave
+        // (k_jakes_grp2: each Philox block drawn once, LG = 16 / groups)
+        if (op.jakes_mom == 2 && jc->ngrp > 0 && op.jakes_grp2 && ch.ntap == 2 &&
+            (jc->ngrp == 1 || jc->ngrp == 2 || jc->ngrp == 4) && (size_t)32 * ch.paths * sizeof(double) <= 64 * 1024) {
+            const dim3 grid(R / 8);
+            const size_t lds = (size_t)32 * ch.paths * sizeof(double);
+#define LAUNCH_JGRP2(MT_, NG_)                                                                                 \
+    if (jc->mt == MT_ && jc->ngrp == NG_) {                                                                   \
+        hipLaunchKernelGGL((k_jakes_grp2<MT_, 16 / NG_>), grid, dim3(256), lds, s, ch, seed, rep0, R, ir,     \
+                           jc->n0, jc->grp, jc->ngrp);                                                        \
+        return JAKES_KIND_GRP;                                                                                \
+    }
+            LAUNCH_JGRP2(16, 1) LAUNCH_JGRP2(16, 2) LAUNCH_JGRP2(16, 4)
+            LAUNCH_JGRP2(24, 1) LAUNCH_JGRP2(24, 2) LAUNCH_JGRP2(24, 4)
+            LAUNCH_JGRP2(28, 1) LAUNCH_JGRP2(28, 2) LAUNCH_JGRP2(28, 4)
+#undef LAUNCH_JGRP2
+        }
         if (op.jakes_mom == 2 && jc->ngrp > 0) {
             constexpr int RPW = 2;
             const int gpb = WAVE / RPW / jc->lg;

@@ -36,16 +36,18 @@ def test_jakes_ir_matches_oracle(ofdm):
         np.testing.assert_allclose(ir_g, ir_o, rtol=0, atol=1e-12)
 
 
-@pytest.mark.parametrize("mom", [2, 1, 0])
-def test_jakes_window_kernels_match_oracle(ofdm, mom):
+@pytest.mark.parametrize("mom,grp2", [(2, 1), (2, 0), (1, 1), (0, 1)])
+def test_jakes_window_kernels_match_oracle(ofdm, mom, grp2):
     """The run's Jakes kernels (only the samples the Q^H windows read):
-    k_jakes_grp (Taylor anchors over runs of windows), k_jakes_mom (one anchor
-    per window) and the recurrence, each against the oracle's per-sample sum of
-    sinusoids at the window samples, 1e-12."""
+    k_jakes_grp2 (Taylor anchors over runs of windows, both taps per wave; the
+    default for two-tap channels since r06), k_jakes_grp (one tap per block),
+    k_jakes_mom (one anchor per window) and the recurrence, each against the
+    oracle's per-sample sum of sinusoids at the window samples, 1e-12."""
     S, eng, _ = ofdm
     ch = S.chan
     eng.set_option("realise_win", 1)
     eng.set_option("jakes_mom", mom)
+    eng.set_option("jakes_grp2", grp2)
     try:
         for rep in (0, 1, 6, 77, 1 << 33):
             ir_g = eng.channel_impulse_response(SEED, rep)
@@ -57,6 +59,7 @@ def test_jakes_window_kernels_match_oracle(ofdm, mom):
     finally:
         eng.set_option("realise_win", 0)
         eng.set_option("jakes_mom", 2)
+        eng.set_option("jakes_grp2", 1)
 
 
 @pytest.mark.parametrize("mom", [2, 1, 0])
@@ -500,7 +503,7 @@ def test_stage_variants_agree(name):
                 {"jakes_mom": 1}, {"jakes_mom": 0}, {"tx_rows": 0}, {"pic_net": 0},
                 {"pic_net": 0, "mmse_ic": 0}, {"mic_net": 0}, {"mic_net": 2}, {"mic_net": 3},
                 {"mic_net": 0, "pic_net": 0}, {"mic_lr": 0}, {"mic_lr": 0, "mic_net": 3},
-                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0})
+                {"pic_poly": 0}, {"pic_poly": 1, "pic_chain": 0}, {"wrow": 0}, {"jakes_grp2": 0})
     for env in variants:
         old = {k: eng.get_option(k) for k in env}
         for k, v in env.items():
