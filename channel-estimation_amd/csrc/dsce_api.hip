@@ -965,15 +965,20 @@ void build_mic_lr(dsce_ctx* c, Scheme& s, const SetupArgs& a, const std::vector<
     s.lr_resid = rel;
     s.lr_ratio = worst;
     if (worst > 1.0) return;
+    // Tw holds T_k minus its window mean (r06): the taps the IC stages form from
+    // it, sum_k Tw_k Z[q k], are the estimated taps minus their window mean,
+    // whose DFT-24 chain is exactly Q' H_hat G - diag(D_hat) (a constant tap over
+    // the window maps to that diagonal), so y_ic = y - chain needs no
+    // diag(D_hat) v term; Ts keeps the full window sums (diag(D_hat) itself)
     std::vector<double> tw((size_t)nblk * MIC_NB * 24), ts((size_t)nblk * MIC_NB);
     for (int b = 0; b < nblk; ++b)
         for (int k = 0; k < MIC_NB; ++k) {
-            long double sum = 0.0L;
+            long double sum = 0.0L, t[24];
             for (int m = 0; m < 24; ++m) {
-                const long double t = Tk(k, s.qband.klo[b] + m);
-                tw[((size_t)b * MIC_NB + k) * 24 + m] = (double)t;
-                sum += t;
+                t[m] = Tk(k, s.qband.klo[b] + m);
+                sum += t[m];
             }
+            for (int m = 0; m < 24; ++m) tw[((size_t)b * MIC_NB + k) * 24 + m] = (double)(t[m] - sum / 24.0L);
             ts[(size_t)b * MIC_NB + k] = (double)sum;
         }
     s.Bz = dupload(c, bz);

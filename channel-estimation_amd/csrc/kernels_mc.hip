@@ -1813,7 +1813,8 @@ __device__ __forceinline__ void dft6(double2 (&x)[6]) {
 // transforms are linear, so acc = c D u, and with Yo = c y / h + (ofI, 0) the
 // folded slicer input is
 //   fI = Yo.x + us.x - (acc / h).x,  fQ = (Yo.y + us.y - (acc / h).y) scQ / scI + ofQ
-// (7 FP64 operations per row).  Re-precoded decisions read the scaled
+// (7 FP64 operations per row; r06: the taps are centred over the window, acc =
+// c (D - diag h) u, and the us terms go: 5).  Re-precoded decisions read the scaled
 // constellation; the constant rows of u (pilots) are per-lane LDS slots read
 // through the same address select, so a row's new u is one LDS read.
 // (vb / vn = the block's index in the grid and the grid's size, vb % 8 = the XCD)
@@ -1898,6 +1899,27 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
         }
     }
     __syncthreads();
+    // the taps minus their window mean (r06): a tap constant over the FFT window
+    // maps to the diagonal of Q' H G, so the chain now forms (D - diag h) u
+    // itself and the one-tap input is y / h - acc / h (no + u per row and
+    // iteration); the mean over the unit's four quarters by the all-ones MFMA
+    // (NM: quarters on the K rows) or two DPP exchanges (quad layout)
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        double2 sq = taps[0][q];
+#pragma unroll
+        for (int m = 1; m < 6; ++m) sq = c_add(sq, taps[m][q]);
+        if (NM) {
+            sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.x, 0.0, 0, 0, 0),
+                              __builtin_amdgcn_mfma_f64_4x4x4f64(1.0, sq.y, 0.0, 0, 0, 0));
+        } else {
+            sq = c_add(sq, dpp_c<QP_XOR1>(sq));
+            sq = c_add(sq, dpp_c<QP_XOR2>(sq));
+        }
+        const double2 mq = make_double2(sq.x * (1.0 / 24.0), sq.y * (1.0 / 24.0));
+#pragma unroll
+        for (int m = 0; m < 6; ++m) taps[m][q] = c_sub(taps[m][q], mq);
+    }
     // u scaled by c; the constant rows into the lane's own LDS slots (every row:
     // the data rows' slots are never read; no barrier, only this lane reads them)
 #pragma unroll
@@ -2032,19 +2054,19 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
                 yh[a] = make_double2(fma(ys.x, cs, o.ofI), ys.y * cs); // c y / h + (ofI, 0)
             }
         // epilogue per row 4a + r: the folded slicer input of z = y / h - acc / h
-        // + u (above), slicer, counts, re-precoded decision into u
+        // (acc = c (D - diag h) u: centred taps), slicer, counts, re-precoded
+        // decision into u
         int dp[6];
         double fI[6], fQ[6];
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             const double2 xa = x[p6(a)], hh = hc[a];
-            fI[a] = fma(-xa.x, hh.x, fma(xa.y, hh.y, yh[a].x + u[a].x));
-            fQ[a] = fma(fma(-xa.x, hh.y, fma(-xa.y, hh.x, yh[a].y + u[a].y)), rq, o.ofQ);
+            fI[a] = fma(-xa.x, hh.x, fma(xa.y, hh.y, yh[a].x));
+            fQ[a] = fma(fma(-xa.x, hh.y, fma(-xa.y, hh.x, yh[a].y)), rq, o.ofQ);
             if (TRACE && ((dmask >> a) & 1) && unit == o.tr->unit) {
                 const int row = row0 + 4 * a + r;
-                const double2 yv = o.y[(size_t)row * U + unit], hv = o.h[(size_t)row * R + rl];
-                o.tr->yperf[(size_t)it * o.tr->LK + row] =
-                    c_add(c_sub(yv, make_double2(xa.x / cs, xa.y / cs)), c_mul(hv, make_double2(u[a].x / cs, u[a].y / cs)));
+                const double2 yv = o.y[(size_t)row * U + unit];
+                o.tr->yperf[(size_t)it * o.tr->LK + row] = c_sub(yv, make_double2(xa.x / cs, xa.y / cs));
             }
         }
         // a decision exactly on a mid-point (measure zero): the smallest symbol
@@ -2501,13 +2523,17 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 mic_chain<NT, SH, NM>(x, ltp, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
             else
                 mic_chain<NT, SH, NM>(x, taps, tb.twa, tb.amt, (l & 3) + 4 * (l >> 4) + oz, l, ro, sg1, sg2);
-            // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484)
+            // y_ic = y - (D_hat_{s-1} - diag) v  (script:482-484); LR: the taps are
+            // mean-free over the window (centred Tw, build_mic_lr), so the chain
+            // already is (D_hat - diag) v (r06: 48 FP64 operations per stage fewer)
 #pragma unroll
             for (int a = 0; a < 6; ++a) {
-                double2 hpv = sp0;
-                c_fma(hpv, sp1, wrow[4 * a + ro]);
                 ye[a] = c_sub(yv[a], x[p6(a)]);
-                c_fma(ye[a], hpv, v[a]);
+                if constexpr (!LR) {
+                    double2 hpv = sp0;
+                    c_fma(hpv, sp1, wrow[4 * a + ro]);
+                    c_fma(ye[a], hpv, v[a]);
+                }
             }
         }
         // this stage's LS pilot estimates (script:412-414 / :487-489)
