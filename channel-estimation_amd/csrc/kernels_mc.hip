@@ -2402,7 +2402,15 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     double2 hb[LR ? 1 : NP / 4], hn4[LR ? 1 : NP / 4];
     // LR: Z of this stage (diag, then the next stage's taps), whole unit per lane
     // (the data kernel; the pilot kernel reads them from its LDS szz instead)
-    constexpr int NZR = LR && !PIL ? NZ : 1;
+    // MLR (r06, the row layout NM): the low-rank taps and window sums on the
+    // matrix cores.  MIC_NB = 4 pilot symbols = the K rows of v_mfma_f64_4x4x4f64:
+    // the lane of quarter k (row k = l >> 4, unit l & 15 = 4 c + n) holds its
+    // unit's Z[q][k] (B[k][n]) and T_k[6 i + a] with i = l & 3 (A[i][k], the same
+    // for every block c), so D[i][n] = sum_k T_k[6 i + a] Z_n[q][k] is the tap of
+    // sample 6 i + a in the unit's quarter-i lane: 2 MFMAs per (sample, tap)
+    // instead of 8 FMAs, and a lane reads 2 of the NZ = 8 Z values per stage
+    constexpr bool MLR = LR && NM && MIC_NB == 4;
+    constexpr int NZR = LR && !PIL ? (MLR ? NT : NZ) : 1;
     double2 zc[NZR];
     // LR data kernel: the next stage's estimated taps, formed at the end of a stage
     // from its Z (r05: carrying the previous stage's Z instead cost 16 register
@@ -2410,7 +2418,23 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     // stage's land in the same registers)
     constexpr int NTL = LR && !PIL ? 6 : 1;
     double2 ltp[NTL][NT];
+    // Z[q][l >> 4] of the lane's unit (MLR)
+    auto zrow = [&](int sp, int q) -> double2 { return PIL ? szz[sp & 1][q * MIC_NB + (l >> 4)][ul] : zc[q % NZR]; };
     auto lr_taps = [&](double2 (&tp)[6][NT], int sp, int ozz) {
+        if constexpr (MLR) {
+            double2 zq[NT];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) zq[q] = zrow(sp, q);
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+                const double ta = twl[(l >> 4) * 24 + 6 * (l & 3) + a + ozz];
+#pragma unroll
+                for (int q = 0; q < NT; ++q)
+                    tp[a][q] = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(ta, zq[q].x, 0.0, 0, 0, 0),
+                                            __builtin_amdgcn_mfma_f64_4x4x4f64(ta, zq[q].y, 0.0, 0, 0, 0));
+            }
+            return;
+        }
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
             double tk[MIC_NB];
@@ -2436,7 +2460,22 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
     auto diag_sums = [&](int s, int ro, double2& sn0, double2& sn1) {
         sn0 = sn1 = make_double2(0.0, 0.0);
         bool f0 = true, f1 = true;                          // compile-time: first tap of each sum assigns
-        if constexpr (LR) {
+        if constexpr (MLR) {
+            const double tsr = tsl[l >> 4];
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const double2 z = zrow(s, q);
+                const double2 sq = make_double2(__builtin_amdgcn_mfma_f64_4x4x4f64(tsr, z.x, 0.0, 0, 0, 0),
+                                                __builtin_amdgcn_mfma_f64_4x4x4f64(tsr, z.y, 0.0, 0, 0, 0));
+                if ((SH >> q) & 1) {
+                    sn1 = f1 ? sq : c_add(sn1, sq);
+                    f1 = false;
+                } else {
+                    sn0 = f0 ? sq : c_add(sn0, sq);
+                    f0 = false;
+                }
+            }
+        } else if constexpr (LR) {
 #pragma unroll
             for (int q = 0; q < NT; ++q) {
                 double2 zk[MIC_NB];
@@ -2490,7 +2529,11 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
         asm volatile("" : "+v"(oz));
         const int ro = r + oz;
         double2 sn0, sn1;
-        if (LR && !PIL) {
+        if (MLR && !PIL) {
+#pragma unroll
+            for (int q = 0; q < NZR; ++q)
+                zc[q] = buf_ld2(rza, (unsigned)(unit + (l >> 4) * U) * 16u, (unsigned)((s * NZ + q * MIC_NB) * U) * 16u);
+        } else if (LR && !PIL) {
 #pragma unroll
             for (int j = 0; j < NZR; ++j) zc[j] = buf_ld2(rza, (unsigned)unit * 16u, (unsigned)((s * NZ + j) * U) * 16u);
         } else if (!LR && !PIL) {
