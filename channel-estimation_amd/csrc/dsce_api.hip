@@ -393,6 +393,90 @@ void build_poly(dsce_ctx* c, Scheme& s) {
     k.poly_ok = 1;
 }
 
+// The chain kernels' LDS tables (SchemeK::ct_*), evaluated with the kernels'
+// own operations in the same order (the host code is built with
+// -ffp-contract=off like the kernels, std::fma where they use fma), so the
+// staged values are bit-identical to what each block derived from its thread
+// index before r06.
+static const double kW24h[12][2] = {
+    {1.0, 0.0},
+    {0.96592582628906829, 0.25881904510252076},
+    {0.86602540378443865, 0.5},
+    {0.70710678118654752, 0.70710678118654752},
+    {0.5, 0.86602540378443865},
+    {0.25881904510252076, 0.96592582628906829},
+    {0.0, 1.0},
+    {-0.25881904510252076, 0.96592582628906829},
+    {-0.5, 0.86602540378443865},
+    {-0.70710678118654752, 0.70710678118654752},
+    {-0.86602540378443865, 0.5},
+    {-0.96592582628906829, 0.25881904510252076}};
+
+static double2 w24_signed(int e) {                 // w24^e, e in 0..23, as kW24[e % 12] negated past 12
+    const double2 t = make_double2(kW24h[e % 12][0], kW24h[e % 12][1]);
+    return e >= 12 ? make_double2(-t.x, -t.y) : t;
+}
+
+void build_chain_tables(dsce_ctx* c, Scheme& s, const std::vector<int>& grid, const std::vector<int>& row_data,
+                        const std::vector<int>& row_cons, const std::vector<int>& row_pcol,
+                        const std::vector<double2>& row_pval) {
+    SchemeK& k = s.k;
+    const int LK = s.LK, NP = s.d.n_pilots, M = s.d.mod_order;
+    const double2 scale = k.pf_scale;
+    const double cs = (1.0 / k.data_div) * k.slI;             // chain_detect's scI
+    std::vector<double2> symc(256), sym(256), amt(192), twa(48), rpv, wrow;
+    std::vector<int> rdc, rpc;
+    for (int t = 0; t < 256; ++t) {
+        const double2 a = t < M ? s.symbols[t] : make_double2(0.0, 0.0);
+        double2 sa = a;
+        if (k.pv_uni) {                                         // stage_sym: c_fma(0, pv, a)
+            const double2 pv = k.pv_data;
+            double x = std::fma(pv.x, a.x, 0.0);
+            x = std::fma(-pv.y, a.y, x);
+            double y = std::fma(pv.x, a.y, 0.0);
+            y = std::fma(pv.y, a.x, y);
+            sa = make_double2(x, y);
+        }
+        sym[t] = sa;
+        symc[t] = make_double2(sa.x * cs, sa.y * cs);
+    }
+    for (int t = 0; t < 192; ++t) {                             // amt[dir][m][i + 4 k]
+        const int dir = t / 96, m = (t / 16) % 6, ii = t & 3, kk = (t >> 2) & 3;
+        const double2 v = w24_signed((6 * ii * kk + (dir ? ii : kk) * m) % 24);
+        amt[t] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+    }
+    for (int t = 0; t < 48; ++t) {                              // twa[dir][r][m']
+        const double2 v = w24_signed(((t / 6) % 4) * (t % 6));
+        twa[t] = t >= 24 ? c_mul(scale, make_double2(v.x, -v.y)) : v;
+    }
+    std::vector<unsigned> gw(64, 0u);
+    for (int t = 0; t < 256; ++t) {
+        const int gi = t >> 4, gq = t & 15;
+        const unsigned g = gi < k.nI && gq < k.nQ ? (unsigned)grid[std::min(gi * k.nQ + gq, k.nI * k.nQ - 1)] & 0xffu : 0u;
+        gw[t >> 2] |= g << (8 * (t & 3));
+    }
+    const size_t nblk = s.qband.row0.size();
+    for (size_t b = 0; b < nblk; ++b)
+        for (int rt = 0; rt < 24; ++rt) {
+            const int r = std::min(s.qband.row0[b] + rt, LK - 1);
+            const int dr = row_data[r], pc = row_pcol[r];
+            rpv.push_back(row_pval[r]);
+            rdc.push_back(dr >= 0 ? (dr << 1) | (row_cons[r] ? 1 : 0) : -1);
+            rpc.push_back(dr < 0 && pc >= 0 && pc < NP ? pc : -1);
+            const double2 wl = w24_signed(rt);
+            wrow.push_back(c_mul(scale, make_double2(wl.x, -wl.y)));
+        }
+    k.ct_symc = dupload(c, symc);
+    k.ct_sym = dupload(c, sym);
+    k.ct_amt = dupload(c, amt);
+    k.ct_twa = dupload(c, twa);
+    k.ct_grid = dupload(c, gw);
+    k.ct_rpv = dupload(c, rpv);
+    k.ct_rdc = dupload(c, rdc);
+    k.ct_rpc = dupload(c, rpc);
+    k.ct_wrow = dupload(c, wrow);
+}
+
 // ---------------------------------------------------------------------------
 // operator packing
 // ---------------------------------------------------------------------------
@@ -667,6 +751,7 @@ void pack_scheme(dsce_ctx* c, Scheme& s) {
             for (int v : seen) onto = onto && v == 1;
             s.k.tx_rows = onto ? 1 : 0;
         }
+        if (s.k.pf_ok) build_chain_tables(c, s, grid, row_data, row_cons, row_pcol, row_pval);
     }
     // bits per realisation
     s.bits_all = (int64_t)s.d.n_data * s.d.bits_per_symbol;

@@ -198,6 +198,19 @@ struct SchemeK {
     int pf_ok;
     double2 pf_scale;
     double2 pf_gs, pf_qs;         // the two factors: G block = gs w^(l m), Q^H block = qs w^(-l m)
+    // LDS tables of the chain kernels (pf_ok schemes), precomputed at
+    // dsce_add_scheme (r06, build_chain_tables): a block's prologue copies entry
+    // tid instead of deriving it from tid (the index arithmetic, twiddle lookups
+    // and scale products were ~5 % of the chain kernels' VALU instructions)
+    const double2* ct_symc;       // [256] stage_sym(symbol) * scI (k_pic_fft); 0 past M
+    const double2* ct_sym;        // [256] stage_sym(symbol) (k_mic_pilot / k_mic_data); 0 past M
+    const double2* ct_amt;        // [2][6][16] the matrix-core network's A_m (flat = the LDS order)
+    const double2* ct_twa;        // [2][4][6] the DPP network's lane twiddles (flat = the LDS order)
+    const unsigned* ct_grid;      // [64] slice6's byte grid [iI][iQ] (row stride 16) as words
+    const double2* ct_rpv;        // [QH blk][24] row precoder value
+    const int* ct_rdc;            // [QH blk][24] data index << 1 | no-edge, or -1
+    const int* ct_rpc;            // [QH blk][24] pilot column of a pilot row, or -1
+    const double2* ct_wrow;       // [QH blk][24] diag(D_hat) weight qs gs w^(-l) of a delayed tap
     // polyphase form (poly_ok, build_poly): with w = e^(2 pi i / L) and F = L,
     //   G[n, l + L k] = A_k[n] w^(l n) C[l][k],   Q^H[l + L k, n] = B_k[n] w^(-l n) E[l][k]
     // (A_k, B_k real windows), so G u = sum_k A_k IDFT(C u_k)(n mod F) and

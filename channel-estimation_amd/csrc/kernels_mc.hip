@@ -1831,7 +1831,8 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
     const int row0 = sk.QH.row0[blk], klo = sk.QH.klo[blk];
     const double cs = o.scI, rq = o.rQ;                        // the chain's scale (host: scI != 0), scQ / scI
     __shared__ double2 sym[256];
-    __shared__ unsigned char sgrid[256];
+    __shared__ unsigned sgridw[64];                            // slice6's byte grid as words
+    const unsigned char* sgrid = (const unsigned char*)sgridw;
     __shared__ double2 rpv[24];
     __shared__ int rdc[24];
     __shared__ double2 twa[2][4][6];                            // [IFFT / FFT][lane r][m']
@@ -1849,23 +1850,16 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
     {
         // table loads, then the per-unit loads (raw y and h into yh / hc), then
         // the LDS writes: the writes wait only for the tables (vmcnt retires in
-        // order), the per-unit data arrives during the barrier
-        const double2 a = o.symbols[min(tid, o.M - 1)];
-        const int gi = tid >> 4, gq = tid & 15;
-        const int g = o.grid_sym[min(gi * o.nQ + gq, o.nI * o.nQ - 1)];
+        // order), the per-unit data arrives during the barrier.  r06: the tables
+        // come precomputed per scheme (SchemeK::ct_*, build_chain_tables), thread
+        // t copies entry t (clamped, unconditional: threads past a table's end
+        // rewrite its last entry with the same value)
+        const double2 a = sk.ct_symc[tid];
+        const unsigned gw = sk.ct_grid[min(tid, 63)];
         const int rt = min(tid, 23);
-        const double2 pv = o.row_pval[row0 + rt];
-        const int dr = o.row_data[row0 + rt], cns = o.row_cons[row0 + rt];
-        const int e = ((min(tid, 47) / 6) % 4) * (min(tid, 47) % 6);   // twa: w24^(r m')
-        const double2 tw = kW24[e % 12];
-        const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-        // NM: A_m[i][k], inverse w24^(6 i k + k m), forward qs gs w24^-(6 i k + i m);
-        // its constant read issued here with the other table reads (inside the
-        // tid < 192 branch it came after the per-unit loads, and its vmcnt(0)
-        // made the table writes wait for all of them)
-        const int tn = min(tid, 191), ndir = tn / 96, nm_ = (tn / 16) % 6, nii = tn & 3, nkk = (tn >> 2) & 3;
-        const int nea = (6 * nii * nkk + (ndir ? nii : nkk) * nm_) % 24;
-        const double2 nt0 = kW24[nea % 12];
+        const double2 pv = sk.ct_rpv[blk * 24 + rt];
+        const int rdv = sk.ct_rdc[blk * 24 + rt];
+        const double2 nt = NM ? sk.ct_amt[min(tid, 191)] : sk.ct_twa[min(tid, 47)];
         const RowView vu = S0 ? RowView(o.xs, row0, R, r, rl, 16) : RowView(o.u, row0, U, r, unit, 16);
         const RowView vs(o.sidr, row0, R, r, rl, 2), vy(o.y, row0, U, r, unit, 16), vh(o.h, row0, R, r, rl, 16);
 #pragma unroll
@@ -1879,24 +1873,12 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
         for (int m = 0; m < 6; ++m)
 #pragma unroll
             for (int q = 0; q < NT; ++q) taps[m][q] = buf_ld2(trs, tv0, (unsigned)((q * N + m) * R) * 16u);
-        const double2 sa = stage_sym(make_double2(tid < o.M ? a.x : 0.0, tid < o.M ? a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
-        sym[tid] = make_double2(sa.x * cs, sa.y * cs);
-        sgrid[tid] = (unsigned char)(gi < o.nI && gq < o.nQ ? g : 0);
-        // unconditional (clamped) table writes: a write under `if (tid < 24)`
-        // lets the compiler sink the table loads into the branch, behind a
-        // vmcnt(0) that also waits for every per-unit load
+        sym[tid] = a;
+        sgridw[min(tid, 63)] = gw;
         rpv[rt] = pv;
-        rdc[rt] = dr >= 0 ? (dr << 1) | (cns ? 1 : 0) : -1;    // data index << 1 | no-edge, or -1
-        if (!NM) {
-            // IFFT w24^(r m'); FFT qs gs w24^-(r m') (the output scale of Q' H G)
-            const int tc = min(tid, 47), dir = tc / 24;
-            const double2 v = e >= 12 ? make_double2(-tw.x, -tw.y) : tw;
-            twa[dir][(tc / 6) % 4][tc % 6] = dir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        } else {
-            // unconditional (clamped: threads 192.. rewrite entry 191's value)
-            const double2 v = nea >= 12 ? make_double2(-nt0.x, -nt0.y) : nt0;
-            amt[ndir][nm_][nii + 4 * nkk] = ndir ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-        }
+        rdc[rt] = rdv;
+        if (!NM) (&twa[0][0][0])[min(tid, 47)] = nt;
+        else (&amt[0][0][0])[min(tid, 191)] = nt;
     }
     __syncthreads();
     // the taps minus their window mean (r06): a tap constant over the FFT window
@@ -2266,7 +2248,7 @@ __device__ __forceinline__ void mic_chain(double2 (&xx)[6], const double2 (&tp)[
 // the wave's symbol, lane twiddles, the per-row diag(D_hat) weight of a delayed tap.
 struct Mic2Tables {
     double2 sym[256];
-    unsigned char sgrid[256];          // slice6's byte grid [iI][iQ], row stride 16
+    alignas(16) unsigned char sgrid[256];   // slice6's byte grid [iI][iQ], row stride 16
     double2 twa[2][4][6];
     double2 amt[2][6][16];            // NM network: A_m[i][k] at [dir][m][i + 4 k] (k_pic_fft's)
 };
@@ -2693,46 +2675,36 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
 // only for the table reads (vmcnt retires in order).  A read under a branch
 // waited with vmcnt(0) for everything issued before it.
 struct Mic2TabLoad {
-    double2 a, tw, t0, pv, tr;
-    int g, dr, cs, pcr;
+    double2 a, tw, t0, pv, wr;
+    int rd, pc;
+    unsigned g;
 };
-__device__ __forceinline__ void mic2_tab_load(Mic2TabLoad& L, const StorePerfectDetect& o, const SchemeK& sk, int row0,
-                                              int tid, int t) {
-    const int gi = tid >> 4, gq = tid & 15;
-    L.a = o.symbols[min(tid, o.M - 1)];
-    L.g = o.grid_sym[min(gi * o.nQ + gq, o.nI * o.nQ - 1)];
-    const int tc = min(tid, 47), e = ((tc / 6) % 4) * (tc % 6);
-    L.tw = kW24[e % 12];
-    const int tn = min(tid, 191), dir = tn / 96, m = (tn / 16) % 6, ii = tn & 3, kk = (tn >> 2) & 3;
-    L.t0 = kW24[((6 * ii * kk + (dir ? ii : kk) * m) % 24) % 12];
-    const int rt = min(t, 23);
-    L.pv = o.row_pval[row0 + rt];
-    L.dr = o.row_data[row0 + rt];
-    L.cs = o.row_cons[row0 + rt];
-    L.pcr = sk.row_pcol[row0 + rt];
-    L.tr = kW24[rt % 12];
+// r06: the tables come precomputed per scheme (SchemeK::ct_*, build_chain_tables);
+// thread tid copies entry tid of each (clamped, unconditional), and thread t the
+// row entries of QH block blk (rows row0 .. row0 + 23)
+__device__ __forceinline__ void mic2_tab_load(Mic2TabLoad& L, const SchemeK& sk, int blk, int tid, int t) {
+    L.a = sk.ct_sym[tid];
+    L.g = sk.ct_grid[min(tid, 63)];
+    L.tw = sk.ct_twa[min(tid, 47)];
+    L.t0 = sk.ct_amt[min(tid, 191)];
+    const int i = blk * 24 + min(t, 23);
+    L.pv = sk.ct_rpv[i];
+    L.rd = sk.ct_rdc[i];
+    L.pc = sk.ct_rpc[i];
+    L.wr = sk.ct_wrow[i];
 }
 __device__ __forceinline__ void mic2_tab_store(const Mic2TabLoad& L, Mic2Tables& tb, double2* rpv, int* rdc, int* rpc,
-                                               double2* wrow, const StorePerfectDetect& o, const SchemeK& sk, int tid,
-                                               int t) {
-    const double2 scale = make_double2(o.pf_scale_re, o.pf_scale_im);
-    const int gi = tid >> 4, gq = tid & 15;
-    tb.sym[tid] = stage_sym(make_double2(tid < o.M ? L.a.x : 0.0, tid < o.M ? L.a.y : 0.0), o.pv_uni, o.pv_re, o.pv_im);
-    tb.sgrid[tid] = (unsigned char)(gi < o.nI && gq < o.nQ ? L.g : 0);
-    const int tc = min(tid, 47), e = ((tc / 6) % 4) * (tc % 6);
-    const double2 v = e >= 12 ? make_double2(-L.tw.x, -L.tw.y) : L.tw;
-    tb.twa[tc / 24][(tc / 6) % 4][tc % 6] = tc >= 24 ? c_mul(scale, make_double2(v.x, -v.y)) : v;
-    const int tn = min(tid, 191), dir = tn / 96, m = (tn / 16) % 6, ii = tn & 3, kk = (tn >> 2) & 3;
-    const int ea = (6 * ii * kk + (dir ? ii : kk) * m) % 24;
-    const double2 vn = ea >= 12 ? make_double2(-L.t0.x, -L.t0.y) : L.t0;
-    tb.amt[dir][m][ii + 4 * kk] = dir ? c_mul(scale, make_double2(vn.x, -vn.y)) : vn;
+                                               double2* wrow, int tid, int t) {
+    tb.sym[tid] = L.a;
+    ((unsigned*)tb.sgrid)[min(tid, 63)] = L.g;
+    (&tb.twa[0][0][0])[min(tid, 47)] = L.tw;
+    (&tb.amt[0][0][0])[min(tid, 191)] = L.t0;
     // row tables (threads t >= 24 rewrite row 23's entries)
     const int rt = min(t, 23);
     rpv[rt] = L.pv;
-    rdc[rt] = L.dr >= 0 ? (L.dr << 1) | (L.cs ? 1 : 0) : -1;
-    rpc[rt] = L.dr < 0 && L.pcr >= 0 && L.pcr < sk.NP ? L.pcr : -1;
-    const double2 wl = rt >= 12 ? make_double2(-L.tr.x, -L.tr.y) : L.tr;
-    wrow[rt] = c_mul(scale, make_double2(wl.x, -wl.y));
+    rdc[rt] = L.rd;
+    rpc[rt] = L.pc;
+    wrow[rt] = L.wr;
 }
 
 __device__ __forceinline__ void mic2_tables(Mic2Tables& tb, const StorePerfectDetect& o, int tid, int nth) {
@@ -2816,9 +2788,9 @@ __device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args
     Mic2Unit mu;
     if (blockDim.x == 256) {
         Mic2TabLoad tl;
-        mic2_tab_load(tl, o, sk, row0, tid, l);
+        mic2_tab_load(tl, sk, blk, tid, l);
         mu.load(o, row0, r, unit, rl);
-        mic2_tab_store(tl, tb, rpv[w], rdc[w], rpc[w], wrow[w], o, sk, tid, l);
+        mic2_tab_store(tl, tb, rpv[w], rdc[w], rpc[w], wrow[w], tid, l);
     } else {
         mu.load(o, row0, r, unit, rl);
         mic2_tables(tb, o, tid, blockDim.x);
@@ -2901,9 +2873,9 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
         const int i = min(tid, MIC_NB * 25 - 1);
         const double t = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
         Mic2TabLoad tl;
-        mic2_tab_load(tl, o, sk, row0, tid, tid);
+        mic2_tab_load(tl, sk, blk, tid, tid);
         mu.load(o, row0, r, unit, rl);
-        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, o, sk, tid, tid);
+        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, tid, tid);
         if (tid < MIC_NB * 25) twd[tid] = t;
     } else {
         // every global load before the first LDS write (clamped, unconditional)
@@ -2918,9 +2890,9 @@ k_mic_data(SchemeK sk, BandOrder ord, Mic2Args ma, StorePerfectDetect o) {
         const int ib = min(tid, 2 * NT * NP - 1), var = ib / (NT * NP), q = (ib / NP) % NT, p = ib % NP;
         const double2 bsv = ma.bs[(((size_t)(var * ma.nsnr + snr) * ma.nblk + blk) * NT + q) * NP + p];
         Mic2TabLoad tl;
-        mic2_tab_load(tl, o, sk, row0, tid, tid);
+        mic2_tab_load(tl, sk, blk, tid, tid);
         mu.load(o, row0, r, unit, rl);
-        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, o, sk, tid, tid);
+        mic2_tab_store(tl, tb, rpv, rdc, rpc, wrow, tid, tid);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int i = min(tid + 256 * k, NBV - 1);
