@@ -2333,15 +2333,20 @@ static void run_multi(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t
     if (ctx->reduce == DSCE_REDUCE_RCCL) {
         // stream-ordered behind each member's kernels; one group = one collective
         // launch per buffer and device
+        // (the group is always closed, also when an enqueue fails: an open
+        // group would swallow the next call's collectives)
         DSCE_NCCL_CHECK(ncclGroupStart());
-        for (size_t m = 0; m < n; ++m) {
+        ncclResult_t first = ncclSuccess;
+        for (size_t m = 0; m < n && first == ncclSuccess; ++m) {
             dsce_ctx* c = member(ctx, m);
-            DSCE_NCCL_CHECK(ncclAllReduce(c->d_counters, c->d_counters, c->counters_n, ncclUint64, ncclSum,
-                                          ctx->comms[m], c->stream));
-            if (c->mse)
-                DSCE_NCCL_CHECK(ncclAllReduce(c->d_mse, c->d_mse, c->mse_n, ncclFloat64, ncclSum, ctx->comms[m], c->stream));
+            first = ncclAllReduce(c->d_counters, c->d_counters, c->counters_n, ncclUint64, ncclSum, ctx->comms[m],
+                                  c->stream);
+            if (first == ncclSuccess && c->mse)
+                first = ncclAllReduce(c->d_mse, c->d_mse, c->mse_n, ncclFloat64, ncclSum, ctx->comms[m], c->stream);
         }
-        DSCE_NCCL_CHECK(ncclGroupEnd());
+        const ncclResult_t end = ncclGroupEnd();
+        DSCE_NCCL_CHECK(first);
+        DSCE_NCCL_CHECK(end);
         for (size_t m = 1; m < n; ++m) {
             check_ctx(member(ctx, m));
             finish_run(member(ctx, m), nullptr, nullptr);
