@@ -168,6 +168,10 @@ struct dsce_ctx {
     std::vector<void*> buf_allocs;
     unsigned long long* d_counters = nullptr;
     size_t counters_n = 0;
+    // pinned host copy of the counters (r06: the per-run copy back is a direct
+    // DMA instead of a staged pageable copy)
+    unsigned long long* h_counters = nullptr;
+    size_t h_counters_n = 0;
     // channel-estimation MSE (dsce_enable_mse): device sums of the current
     // dsce_run, host totals since the last enable
     bool mse = false;
@@ -2030,6 +2034,7 @@ int dsce_destroy(dsce_ctx* ctx) {
     if (ctx->stream) note(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     for (void* p : ctx->buf_allocs) note(hipFree(p), "hipFree (batch buffers)");
     for (void* p : ctx->allocs) note(hipFree(p), "hipFree (operators)");
+    if (ctx->h_counters) note(hipHostFree(ctx->h_counters), "hipHostFree (counters)");
     for (auto& e : ctx->pending) {
         note(hipEventDestroy(e.a), "hipEventDestroy");
         note(hipEventDestroy(e.b), "hipEventDestroy");
@@ -2270,13 +2275,20 @@ static void run_reps(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t 
 // The member's device counters added into err_counts (null: none), its MSE sums
 // into *mse_dst (the handle's totals), its timing events collected
 static void finish_run(dsce_ctx* ctx, int64_t* err_counts, std::vector<double>* mse_dst) {
-    std::vector<unsigned long long> h(err_counts ? ctx->counters_n : 0);
-    if (err_counts)
-        DSCE_HIP_CHECK(hipMemcpyAsync(h.data(), ctx->d_counters, h.size() * sizeof(unsigned long long),
+    const size_t n = err_counts ? ctx->counters_n : 0;
+    if (n && ctx->h_counters_n < n) {
+        if (ctx->h_counters) DSCE_HIP_CHECK(hipHostFree(ctx->h_counters));
+        ctx->h_counters = nullptr;
+        ctx->h_counters_n = 0;
+        DSCE_HIP_CHECK(hipHostMalloc((void**)&ctx->h_counters, n * sizeof(unsigned long long), hipHostMallocDefault));
+        ctx->h_counters_n = n;
+    }
+    if (n)
+        DSCE_HIP_CHECK(hipMemcpyAsync(ctx->h_counters, ctx->d_counters, n * sizeof(unsigned long long),
                                       hipMemcpyDeviceToHost, ctx->stream));
     DSCE_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     if (ctx->timing) collect_timing(ctx);
-    for (size_t i = 0; i < h.size(); ++i) err_counts[i] += (int64_t)h[i];
+    for (size_t i = 0; i < n; ++i) err_counts[i] += (int64_t)ctx->h_counters[i];
     if (mse_dst) collect_mse(ctx, *mse_dst);
 }
 

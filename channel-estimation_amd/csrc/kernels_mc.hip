@@ -2060,7 +2060,7 @@ __device__ __forceinline__ void pic_fft_body(const SchemeK& sk, const BandOrder&
             ncnt += __umul24(__popc((unsigned)(dp[a] ^ (int)((txp[a >> 2] >> (8 * (a & 3))) & 0xffu))), cweight(a));
             if (TRACE && data && unit == o.tr->unit) o.tr->dec_p[(size_t)it * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
         }
-        reprecode(dp);
+        if (it < niter) reprecode(dp);                           // the last iteration's decisions are only counted
         cntl[w][it] = wave_sum_dpp(rl < o.rvalid ? ncnt : 0);    // uniform: every lane writes the same word
         ncnt = 0;
     }
@@ -2622,7 +2622,9 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 if (data) o.tr->dec_e[(size_t)s * o.tr->ND + (rdc[4 * a + r] >> 1)] = dp[a];
             }
         }
-        if (PIL) {
+        if (s == ma.niter) {
+            // the last stage's decisions are only counted (no re-precoding)
+        } else if (PIL) {
             reprecode6(v, dp, dmask, rpv, r, tb.sym, o.pv_uni);
         } else {
             double2 nv[6];
