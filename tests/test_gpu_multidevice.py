@@ -75,6 +75,26 @@ def test_multi_device_configuration_reaches_every_member(setup_c2):
         ref.close()
 
 
+def test_eight_members_on_one_gpu_rehearse_the_node(setup_c2):
+    """The 8-GPU node's control flow on the one-GPU box: eight members (all on
+    device 0, so the host sum stands in for the RCCL all-reduce), eight member
+    threads, eight 64-aligned slices of an odd realisation count (389 = 6 x 64
+    + 5: member 0's slice is empty, member 7's a partial wave), and the
+    configuration fanned out to all eight: counts equal the
+    single context's over the same realisations."""
+    ref = harness.engine(setup_c2, batch=128)
+    try:
+        want = ref.run(SEED, 3, 389)
+    finally:
+        ref.close()
+    eng = harness.engine(setup_c2, batch=128, device=[0] * 8)
+    try:
+        assert eng.group_info() == ([0] * 8, "host")
+        np.testing.assert_array_equal(eng.run(SEED, 3, 389), want)
+    finally:
+        eng.close()
+
+
 def test_multi_device_rejects_bad_devices():
     from dsce.engine import DsceError, Engine
     with pytest.raises(DsceError):
