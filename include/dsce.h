@@ -374,7 +374,10 @@ int dsce_path_info(dsce_ctx* ctx, int32_t scheme_id, uint32_t* flags);
  *   per symbol, DSCE_PATH_PIC_POLY, the default; 0: the two banded passes),
  *   wrow (1: the unfused W contraction of 32-row blocks — FBMC, C5 — as one
  *   GEMM per 16-row tile over (column, pilot) with B = hP v_c, no per-tile
- *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles).
+ *   epilogue, DSCE_PATH_WROW3; 0: k_wpair3's pair tiles), jakes_grp2 (1, the
+ *   default: a channel with two non-zero taps forms the Jakes taps of the read
+ *   windows with k_jakes_grp2 — both taps per wave, each Philox block drawn
+ *   once; 0: k_jakes_grp, one tap per block; r06).
  * Retired in r06 (measured neutral in r04 / r05; DSCE_EINVAL): pic_skip (the
  * perfect-CSI fixed-point exit), ic_streams (the chain on a second stream /
  * beside the pilot pass in one launch, k_ic_pair).
