@@ -2584,7 +2584,7 @@ __device__ __forceinline__ void mic2_stages(const SchemeK& sk, const Mic2Args& m
                 const int t = threadIdx.x;
                 if (t < NZ * 16) {
                     const int j = t >> 4, u = t & 15;
-                    const double2* bz = bzl + ((size_t)vs * NZ + j) * NP;
+                    const double2* bz = bzl + ((size_t)vs * NZ + j) * (NP + 1);
                     double2 acc = c_mul(bz[0], hx[u]);
 #pragma unroll
                     for (int p = 1; p < NP; ++p) c_fma(acc, bz[p], hx[p * 17 + u]);
@@ -2767,7 +2767,10 @@ __device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args
     __shared__ double2 xpb[NP][17];                         // isqk / transmitted pilot of the block's 16 units
     __shared__ double2 szz[LR ? 2 : 1][NZ][17];             // LR: Z of the block's 16 units, double-buffered
     __shared__ double twp[LR ? 4 : 1][MIC_NB * 24 + MIC_NB];   // LR: each wave's T_k window + sums
-    __shared__ double2 bzl[LR ? 2 * NZ * NP : 1];           // LR: Bz of both variants at this SNR
+    // LR: Bz of both variants at this SNR, rows padded to NP + 1 (the Z phase's
+    // 16-lane groups read rows j and j + 1: unpadded, the same banks; r06,
+    // SQ_LDS_BANK_CONFLICT of the pass -33 %)
+    __shared__ double2 bzl[LR ? 2 * NZ * (NP + 1) : 1];
     __shared__ int cntl[4][PM_MAXIT + 1];
     const int tid = threadIdx.x, l = tid & 63, r = NM ? l >> 4 : l & 3;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
@@ -2803,7 +2806,7 @@ __device__ __forceinline__ void mic_pilot_body(const SchemeK& sk, const Mic2Args
             twp[w][i] = i < MIC_NB * 24 ? ma.tw[(size_t)blk * MIC_NB * 24 + i] : ma.ts[(size_t)blk * MIC_NB + i - MIC_NB * 24];
         for (int i = tid; i < 2 * NZ * NP; i += blockDim.x) {
             const int var = i / (NZ * NP), jp = i % (NZ * NP);
-            bzl[i] = ma.bz[((size_t)var * ma.nsnr + snr) * NZ * NP + jp];
+            bzl[(var * NZ + jp / NP) * (NP + 1) + jp % NP] = ma.bz[((size_t)var * ma.nsnr + snr) * NZ * NP + jp];
         }
     } else {
         const int i = min(l, 2 * NT * NP - 1), var = i / (NT * NP), q = (i / NP) % NT, p = i % NP;
