@@ -13,6 +13,14 @@ option):
     python -m dsce.simulate --config c5 --devices 0,1,2,3,4,5,6,7   # one process, one multi-device
                                                                     # context (dsce_create_multi: the
                                                                     # in-library RCCL all-reduce)
+    python -m dsce.simulate --config paper --checkpoint ck.json --stop-after 4096   # time-boxed slot
+    python -m dsce.simulate --config paper --checkpoint ck.json --resume --out paper.json
+
+Checkpoint / resume (the reference has none): --checkpoint
+writes the int64 counters, the MSE sums and the next realisation after every
+batch (atomically, one file per rank).  The streams are keyed by the global
+realisation index, so a resumed run's counts equal an uninterrupted run's bit
+for bit.
 
 Progress lines mirror the script's `disp` (script:567); results go through
 dsce.results (JSON [+ NPZ], Figures 2-5)."""
@@ -46,7 +54,16 @@ def main(argv=None):
     ap.add_argument("--devices", default=None,
                     help="comma-separated HIP devices of ONE multi-device context (dsce_create_multi, ABI 7): "
                          "the engine shards the realisations and all-reduces the counters itself (RCCL)")
+    ap.add_argument("--checkpoint", default=None,
+                    help="JSON checkpoint written after every batch (counters, MSE sums, next realisation); "
+                         "one file per rank under a launcher (.rankR suffix)")
+    ap.add_argument("--resume", action="store_true", help="continue from --checkpoint if it exists")
+    ap.add_argument("--stop-after", type=int, default=None,
+                    help="process at most this many realisations (per rank) in this invocation, then leave "
+                         "the checkpoint for --resume (needs --checkpoint)")
     a = ap.parse_args(argv)
+    if (a.resume or a.stop_after is not None) and not a.checkpoint:
+        raise SystemExit("--resume / --stop-after need --checkpoint")
 
     from dsce import results
     from dsce.configs import build_setup
@@ -97,29 +114,74 @@ def main(argv=None):
     pw = np.zeros((len(names), nsnr))
     bits = None
     setup_s, t0 = 0.0, time.perf_counter()
+    ck_path = None
+    if a.checkpoint:
+        ck_path = a.checkpoint + (".rank%d" % rank if world > 1 else "")
+    ck_key = {"config": a.config, "schemes": list(names), "seed": int(a.seed), "reps": int(reps),
+              "shard": a.shard, "world": world, "rank": rank, "first": int(first), "mine": int(mine),
+              "mse": bool(a.mse), "snr": [int(s0), int(ns)]}
+    done, prior_s = 0, 0.0
     if mine:                                         # a rank with an empty shard contributes zeros
         eng = build_engine(Sr, device=devices or device, batch=max(64, min(a.batch, mine)), options=options)
         setup_s = time.perf_counter() - t0
         sub = np.zeros(eng.counter_shape(), dtype=np.int64)
+        e0 = np.zeros((len(names), ns, nst))
+        p0 = np.zeros((len(names), ns))
+        if a.resume and os.path.exists(ck_path):
+            ck = load_checkpoint(ck_path, ck_key)
+            done, prior_s = ck["done"], ck["seconds"]
+            sub[...] = np.asarray(ck["counts"], dtype=np.int64).reshape(sub.shape)
+            if a.mse:
+                e0[...] = np.asarray(ck["mse_err"]).reshape(e0.shape)
+                p0[...] = np.asarray(ck["mse_pow"]).reshape(p0.shape)
+            if rank == 0:
+                print("resumed from %s at realisation %d of %d" % (ck_path, first + done, first + mine), flush=True)
         if a.mse:
             eng.enable_mse()
-        done, t0 = 0, time.perf_counter()
+        t0 = time.perf_counter()
         step = min(a.batch * (len(devices) if devices else 1), mine)
-        while done < mine:
-            n = min(step, mine - done)
+        stop = mine if a.stop_after is None else min(mine, done + max(0, a.stop_after))
+        start = done
+        while done < stop:
+            n = min(step, stop - done)
             eng.run(a.seed, first + done, n, sub)
             done += n
             el = time.perf_counter() - t0
+            if ck_path:
+                e_, p_ = eng.mse() if a.mse else (None, None)
+                save_checkpoint(ck_path, ck_key, done, sub, prior_s + el,
+                                (e0 + e_, p0 + p_) if a.mse else None)
             if rank == 0:
-                print("%d%% Completed! Time Left: %.1f s" % (100 * done // mine, el / done * (mine - done)), flush=True)
+                print("%d%% Completed! Time Left: %.1f s"
+                      % (100 * done // mine, el / (done - start) * (mine - done)), flush=True)
         counts[:, :, :, s0:s0 + ns, :] = sub
         bits = np.array([eng.bits_per_rep(i) for i in range(len(names))])
         if a.mse:
             e_, p_ = eng.mse()
-            err[:, s0:s0 + ns, :] = e_
-            pw[:, s0:s0 + ns] = p_
+            err[:, s0:s0 + ns, :] = e0 + e_
+            pw[:, s0:s0 + ns] = p0 + p_
         eng.close()
-    extra = {"setup_s": setup_s, "seconds": time.perf_counter() - t0, "ranks": world, "shard": a.shard}
+    complete = done >= mine
+    if distributed:
+        # every rank must take the same branch before the collectives below
+        import torch
+        import torch.distributed as dist
+        f = torch.tensor([0 if complete else 1], dtype=torch.int64)
+        if os.environ.get("DSCE_DIST_BACKEND", "nccl") == "nccl":
+            f = f.to("cuda")
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        if int(f.item()):
+            complete = False
+    if not complete:
+        if rank == 0:
+            print("stopped at realisation %d of %d; resume with --checkpoint %s --resume"
+                  % (first + done, first + mine, a.checkpoint), flush=True)
+        if distributed:
+            dist.destroy_process_group()
+        return 0
+    extra = {"setup_s": setup_s, "seconds": prior_s + time.perf_counter() - t0, "ranks": world, "shard": a.shard}
+    if ck_path and a.resume:
+        extra["resumed"] = True
     if devices:
         extra["devices"] = devices
     if distributed:
@@ -166,6 +228,39 @@ def main(argv=None):
     if distributed:
         dist.destroy_process_group()
     return 0
+
+
+CHECKPOINT_VERSION = 1
+
+
+def save_checkpoint(path, key, done, counts, seconds, mse=None):
+    """Write the run state atomically (a temporary file, then os.replace): a
+    crash while writing leaves the previous checkpoint intact."""
+    d = {"version": CHECKPOINT_VERSION, "key": key, "done": int(done), "seconds": float(seconds),
+         "counts": np.asarray(counts, dtype=np.int64).ravel().tolist()}
+    if mse is not None:
+        d["mse_err"] = np.asarray(mse[0]).ravel().tolist()
+        d["mse_pow"] = np.asarray(mse[1]).ravel().tolist()
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(d, f)
+    os.replace(tmp, path)
+
+
+def load_checkpoint(path, key):
+    """The checkpoint at `path` if it belongs to this run (same configuration,
+    schemes, seed, realisation count, shard and rank); anything else is an
+    error, never a silent restart or a mixed result."""
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("version") != CHECKPOINT_VERSION:
+        raise SystemExit("checkpoint %s: version %r, expected %d" % (path, d.get("version"), CHECKPOINT_VERSION))
+    if d.get("key") != key:
+        diff = sorted(k for k in set(key) | set(d.get("key", {})) if d.get("key", {}).get(k) != key.get(k))
+        raise SystemExit("checkpoint %s belongs to another run (differs in %s)" % (path, ", ".join(diff)))
+    if not 0 <= int(d["done"]) <= key["mine"]:
+        raise SystemExit("checkpoint %s: realisation count out of range" % path)
+    return d
 
 
 def _snr_subset(S, s0, ns):
