@@ -137,3 +137,29 @@ def test_eight_rank_control_flow_on_one_gpu(tmp_path):
     line = json.loads(res.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 8 and line["config"]["parallelism"] == "dp8"
     assert line["value"] > 0 and line["steps"] == 2
+
+
+def test_two_ranks_stop_and_resume_from_checkpoints(tmp_path):
+    """--checkpoint under a launcher: one file per rank.  With --stop-after 128
+    rank 0 (128 realisations) finishes and rank 1 (192) does not, so neither
+    rank writes a result (the ranks agree by one all-reduce before the counter
+    all-reduce); the resumed launch finishes rank 1 and counts exactly like one
+    uninterrupted rank."""
+    args = ["--config", "default", "--schemes", "ofdm", "--reps", "320", "--batch", "64", "--mse"]
+    env = dict(os.environ, DSCE_DIST_BACKEND="gloo", PYTHONPATH=harness.PKG)
+    one, two, ck = tmp_path / "one.json", tmp_path / "two.json", str(tmp_path / "ck.json")
+    subprocess.run([sys.executable, "-m", "dsce.simulate", *args, "--out", str(one)], cwd=harness.PKG, env=env,
+                   check=True, timeout=240, capture_output=True)
+    launch = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+              "--master-addr", "127.0.0.1"]
+    for extra in (["--stop-after", "128"], ["--resume"]):
+        subprocess.run([*launch, "--master-port", str(_port()), "-m", "dsce.simulate", *args, "--checkpoint", ck,
+                        "--out", str(two), *extra], cwd=harness.PKG, env=env, check=True, timeout=300,
+                       capture_output=True)
+        if extra[0] == "--stop-after":
+            assert not two.exists()
+            assert [json.load(open(ck + ".rank%d" % r))["done"] for r in (0, 1)] == [128, 128]
+    a, b = json.load(open(one)), json.load(open(two))
+    assert b["ranks"] == 2 and b["resumed"] is True
+    assert np.array_equal(np.array(a["counts"]), np.array(b["counts"]))
+    np.testing.assert_allclose(np.array(a["nmse"]["ofdm"]), np.array(b["nmse"]["ofdm"]), rtol=1e-12)
