@@ -16,9 +16,20 @@
 #include <vector>
 
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "dsce.h"
 #include "dsce_kernels.h"
+
+// roctx ranges around the run, each device batch, the counter all-reduce and
+// the setup entry points (tracing): named spans on the host
+// timeline under `rocprofv3 --marker-trace`, no-ops without a profiler
+struct TraceRange {
+    explicit TraceRange(const char* m) { roctxRangePushA(m); }
+    ~TraceRange() { roctxRangePop(); }
+    TraceRange(const TraceRange&) = delete;
+    TraceRange& operator=(const TraceRange&) = delete;
+};
 
 namespace dsce {
 
@@ -1543,6 +1554,7 @@ int var_of_stage(int stage, int niter) { return (stage == 0 || stage <= niter / 
 // Realisations [rep0, rep0 + R) with R a multiple of 64; only the first nvalid
 // add to the counters / MSE sums (the rest pad a run's tail to whole waves).
 void run_batch(dsce_ctx* c, uint64_t seed, uint64_t rep0, int R, int nvalid, Trace* tr) {
+    TraceRange trace_range("dsce batch");
     McBuffers& b = c->buf;
     const Opts& op = c->op;
     if (R % 64 || nvalid < 1 || nvalid > R) throw ApiError(DSCE_EINVAL, "run_batch: bad batch geometry");
@@ -2050,6 +2062,7 @@ int dsce_destroy(dsce_ctx* ctx) {
 const char* dsce_last_error(const dsce_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 static int set_channel_one(dsce_ctx* ctx, const dsce_channel_desc* d) {
+    TraceRange trace_range("dsce_set_channel");
     API_BEGIN
     check_ctx(ctx);
     if (!d || !d->pdp_norm || d->n_samples <= 1 || d->n_taps <= 0 || d->n_paths <= 0 || d->sampling_rate <= 0)
@@ -2134,6 +2147,7 @@ int dsce_set_snr(dsce_ctx* ctx, const double* pn_time, int32_t n_snr, int32_t n_
 }
 
 static int add_scheme_one(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id) {
+    TraceRange trace_range("dsce_add_scheme");
     API_BEGIN
     check_ctx(ctx);
     if (!ctx->chan_set) throw ApiError(DSCE_ESTATE, "dsce_set_channel first");
@@ -2185,6 +2199,7 @@ int dsce_add_scheme(dsce_ctx* ctx, const dsce_scheme_desc* d, int32_t* scheme_id
 }
 
 static int build_mmse_one(dsce_ctx* ctx, double zero_threshold) {
+    TraceRange trace_range("dsce_build_mmse");
     API_BEGIN
     check_ctx(ctx);
     if (ctx->nsnr <= 0) throw ApiError(DSCE_ESTATE, "dsce_set_snr first");
@@ -2342,6 +2357,7 @@ static void run_multi(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t
             (void)hipSetDevice(ctx->device);
             throw ApiError(code[m], member_name(ctx, m) + ": " + msg[m]);
         }
+    TraceRange trace_range(ctx->reduce == DSCE_REDUCE_RCCL ? "dsce counter all-reduce (rccl)" : "dsce counter sum (host)");
     if (ctx->reduce == DSCE_REDUCE_RCCL) {
         // stream-ordered behind each member's kernels; one group = one collective
         // launch per buffer and device
@@ -2375,6 +2391,7 @@ static void run_multi(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t
 }
 
 int dsce_run(dsce_ctx* ctx, uint64_t seed, uint64_t first_rep, uint64_t n_rep, int64_t* err_counts) {
+    TraceRange trace_range("dsce_run");
     API_BEGIN
     check_ctx(ctx);
     if (!err_counts) throw ApiError(DSCE_EINVAL, "err_counts is null");

@@ -71,3 +71,15 @@ def test_no_cpu_fallback_without_gpu():
         engine.Engine(0)
     with pytest.raises(engine.DsceError):
         engine.Engine([0, 1])                    # dsce_create_multi (ABI 7) fails loudly too
+
+
+def test_library_links_rccl_and_roctx():
+    """The in-library all-reduce (dsce_create_multi) and the host trace ranges
+    (roctx) are linked dependencies of libdsce.so."""
+    import subprocess
+    if not os.path.exists(LIB):
+        pytest.skip("libdsce.so not built")
+    out = subprocess.run(["readelf", "-d", LIB], check=True, capture_output=True, text=True).stdout
+    needed = [l.split("[")[1].rstrip("]") for l in out.splitlines() if "(NEEDED)" in l]
+    assert any(n.startswith("librccl.so") for n in needed), needed
+    assert any(n.startswith("librocprofiler-sdk-roctx.so") for n in needed), needed
