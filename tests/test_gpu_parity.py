@@ -226,6 +226,29 @@ def test_error_counts_match_oracle(ofdm):
     assert b[0] == sc["n_data"] * sc["bits_per_symbol"] and b[1] == sc["considered"].sum() * sc["bits_per_symbol"]
 
 
+@pytest.mark.parametrize("first", [(1 << 32) - 30, (1 << 40) + 3])
+def test_counts_at_far_realisation_indices_match_oracle(ofdm, first):
+    """Realisations far from 0: the Philox counter carries the realisation index
+    as two 32-bit words, so 2^32 - 30 .. 2^32 + 33 crosses the low word's wrap
+    inside one wave (a 32-bit index anywhere on the path would alias rep 0..33),
+    and 2^40 + 3 sits past it; every stream (bits, pilots, THETA / PHI, noise)
+    against the oracle, through the bench kernels."""
+    S, eng, mm = ofdm
+    eng.set_batch(64)
+    try:
+        cg = eng.run(SEED, first, 64)
+        assert bench_path(eng) <= eng.path_info(0), eng.path_info(0)
+        res = harness.simulate(S, SEED, first, 64, ["ofdm"])
+        assert res["err"].sum() > 0
+        assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), cg - res["err"]
+        # the oracle keys every stream by the 64-bit index, so this also shows
+        # the counts are not those of the low word's realisations
+        if first >> 32:
+            assert not np.array_equal(cg, eng.run(SEED, first & 0xFFFFFFFF, 64))
+    finally:
+        eng.set_batch(256)
+
+
 @pytest.mark.parametrize("n_iter", [1, 2, 3, 6])
 def test_ic_iteration_counts_match_oracle(n_iter):
     """Other IC iteration counts (script:479 `NrIterations`): the estimator
