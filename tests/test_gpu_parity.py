@@ -322,6 +322,17 @@ def test_fbmc_error_counts(fbmc):
     eng.enable_mse(False)
 
 
+def test_fbmc_counts_across_the_counter_word_wrap(fbmc):
+    """FBMC's kernels (TX precoding, polyphase perfect-CSI passes, the W
+    contraction) at realisations 2^32 - 30 .. 2^32 + 33 against the oracle:
+    the realisation index crosses the Philox counter's low-word wrap."""
+    name, S, eng, mm = fbmc
+    first = (1 << 32) - 30
+    cg = eng.run(SEED, first, 64)
+    res = harness.simulate(S, SEED, first, 64, [name])
+    assert np.abs(cg - res["err"]).sum() <= 8 * res["borderline"].sum(), (name, cg - res["err"])
+
+
 def _check_mse(eng, res):
     """dsce_get_mse (build-defined channel-estimation MSE, parity unpinned vs
     MATLAB) against the oracle's sums: fp64 sums of O(1e4) terms, 1e-9
