@@ -107,6 +107,19 @@ def test_doubly_flat_counts_match_oracle(flat):
     assert got.sum() > 1000
 
 
+def test_doubly_flat_counts_across_the_counter_word_wrap(flat):
+    """The doubly-flat kernels at realisations 2^32 - 30 .. 2^32 + 33 (the
+    Philox counter's realisation low word wraps inside the wave) against the
+    oracle."""
+    S = flat.setup
+    first = (1 << 32) - 30
+    got = flat.run(SEED, first, 64)
+    ref = refsim.simulate_doubly_flat(SEED, first, 64, S.N, _oracle_schemes(S), S.pn_time)
+    diff = np.abs(got - ref["err"]).sum(axis=(1, 2))
+    assert np.all(diff <= 8 * ref["borderline"]), (got, ref["err"], ref["borderline"])
+    assert got.sum() > 1000
+
+
 @pytest.mark.parametrize("method", ["natural", "nearest"])
 def test_doubly_flat_other_interpolations_match_oracle(method):
     """PSACE's other scatteredInterpolant methods (PSACE.m:74-76) on the same
