@@ -370,6 +370,38 @@ def test_counts_are_additive_and_batch_invariant(ofdm):
     np.testing.assert_array_equal(a, c)
 
 
+def test_batch_invariance_at_full_and_largest_batches():
+    """The bench's own batch (65 536 realisations x 7 SNR points) and larger:
+    every count of [0, 262144) is the same at device batch 131 072, 65 536 and
+    8 192 through the bench kernels.  At 262 144 the realisation-major tap
+    buffer (ntap N R x 16 B) passes 4 GB, past k_pic_fft's 32-bit buffer view,
+    so the engine falls back to the W contraction and the banded perfect-CSI
+    passes (pic_fft_ok / mmse_stages_ok) instead of overflowing; that path
+    gives the same counts up to the oracle's borderline decisions (none
+    expected)."""
+    S = harness.setup("default", schemes=("ofdm",))
+    n = 262144
+    ref = None
+    for batch in (131072, 65536, 8192, 262144):
+        eng = harness.engine(S, batch=batch)
+        try:
+            c = eng.run(SEED, 0, n)
+            path = eng.path_info(0)
+        finally:
+            eng.close()
+        assert c.sum() > 0
+        if batch == 262144:
+            assert "pic_fft" not in path and "mic_stages" not in path and "wpair3_fused" in path, path
+            d = np.abs(c - ref)
+            assert d.sum() <= 8, (int(d.sum()), int(ref.sum()))
+            continue
+        assert BENCH_BASE | {"mic_lr"} <= path, (batch, path)
+        if ref is None:
+            ref = c
+        else:
+            np.testing.assert_array_equal(c, ref, err_msg=str(batch))
+
+
 def test_any_repetition_count(ofdm):
     """dsce_run takes the script's own NrRepetitions as is — 25 (script:19) and
     1000 (the paper's, script:44) — not only multiples of one wavefront: the
