@@ -86,13 +86,13 @@ def test_library_links_rccl_and_roctx():
 
 
 def test_asan_driver_is_instrumented():
-    """tools/asan/dsce_asan_driver (`make asan`, tests/test_gpu_asan.py) carries
+    """tools/asan/dsce_asan_driver (`make -f asan.mk`, tests/test_gpu_asan.py) carries
     a live host sanitizer: its --probe mode's one-past-the-end heap read is
     reported (no GPU needed)."""
     import subprocess
     b = os.path.join(harness.ROOT, "tools", "asan", "dsce_asan_driver")
     if not os.path.exists(b):
-        pytest.skip("asan driver not built (make -C channel-estimation_amd asan)")
+        pytest.skip("asan driver not built (make -C channel-estimation_amd -f asan.mk)")
     p = subprocess.run([b, "--probe"], env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"), capture_output=True,
                        text=True, timeout=60)
     assert p.returncode != 0 and "heap-buffer-overflow" in p.stderr, p.stderr[-2000:]

@@ -1,6 +1,6 @@
 """GPU: the C-ABI's host code under AddressSanitizer ("race
 detection / sanitizers"; host code only: GPU ASAN is not available on the
-pool).  `make asan` (run by __graft_entry__.build) compiles dsce_api.hip with
+pool).  `make -f asan.mk` (run by __graft_entry__.build) compiles dsce_api.hip with
 -fsanitize=address on the host side and links it with the regular kernel
 objects into tools/asan/dsce_asan_driver.  The driver replays the MATLAB
 host's call sequence from a setup dump, on a
@@ -54,7 +54,7 @@ def _dump(path, S, sc, expect):
 
 
 def test_c_abi_under_host_asan(tmp_path):
-    assert os.path.exists(BIN), "tools/asan/dsce_asan_driver missing: run __graft_entry__.build() (make asan)"
+    assert os.path.exists(BIN), "tools/asan/dsce_asan_driver missing: run __graft_entry__.build() (make -f asan.mk)"
     S = harness.setup("default", schemes=("ofdm",))
     eng = harness.engine(S, batch=BATCH)
     try:
